@@ -1,0 +1,199 @@
+"""ctypes mirror of include/dfmi.h and the loader of libdfmi.so.
+
+The product path has no fallback: if the HIP library is missing or cannot be
+loaded, ``lib()`` raises. The same struct definitions are reused by the
+tests to talk to the CPU oracle (oracle/oracle.h shares the layouts).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdfmi.so")
+
+# status codes (dfmi_status)
+DFMI_OK = 0
+DFMI_ERR_EXECUTION = 1
+DFMI_ERR_GENERAL = 2
+DFMI_ERR_INVALID_COLUMN = 3
+DFMI_ERR_NOT_IMPLEMENTED = 4
+DFMI_ERR_DIVIDE_BY_ZERO = 5
+DFMI_ERR_ARROW_COMPUTE = 6
+DFMI_ERR_PANIC = 7
+DFMI_ERR_INVALID_ARGUMENT = 8
+DFMI_ERR_CAPACITY = 9
+DFMI_ERR_DEVICE = 10
+
+DFMI_FLAG_EXT_GATHER_ALL = 0x1
+DFMI_FLAG_EXT_UTF8_COMPARE = 0x2
+
+STATUS_NAMES = {
+    DFMI_ERR_EXECUTION: "ExecutionError",
+    DFMI_ERR_GENERAL: "General",
+    DFMI_ERR_INVALID_COLUMN: "InvalidColumn",
+    DFMI_ERR_NOT_IMPLEMENTED: "NotImplemented",
+    DFMI_ERR_DIVIDE_BY_ZERO: "ArrowError(DivideByZero)",
+    DFMI_ERR_ARROW_COMPUTE: "ArrowError(ComputeError)",
+    DFMI_ERR_PANIC: "panic",
+    DFMI_ERR_INVALID_ARGUMENT: "InvalidArgument",
+    DFMI_ERR_CAPACITY: "Capacity",
+    DFMI_ERR_DEVICE: "Device",
+}
+
+
+class dfmi_error(C.Structure):
+    _fields_ = [("code", C.c_int32), ("message", C.c_char * 500)]
+
+
+class dfmi_column(C.Structure):
+    _fields_ = [
+        ("type", C.c_int32),
+        ("reserved", C.c_int32),
+        ("length", C.c_int64),
+        ("null_count", C.c_int64),
+        ("validity", C.c_void_p),
+        ("values", C.c_void_p),
+        ("offsets", C.c_void_p),
+    ]
+
+
+class dfmi_batch(C.Structure):
+    _fields_ = [
+        ("num_columns", C.c_int32),
+        ("reserved", C.c_int32),
+        ("num_rows", C.c_int64),
+        ("columns", C.POINTER(dfmi_column)),
+    ]
+
+
+class dfmi_field(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("type", C.c_int32), ("nullable", C.c_int32)]
+
+
+class dfmi_schema(C.Structure):
+    _fields_ = [("num_fields", C.c_int32), ("reserved", C.c_int32), ("fields", C.POINTER(dfmi_field))]
+
+
+class dfmi_expr_node(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("op", C.c_int32),
+        ("data_type", C.c_int32),
+        ("column", C.c_int32),
+        ("i64", C.c_int64),
+        ("f64", C.c_double),
+        ("str", C.c_char_p),
+        ("str_len", C.c_int64),
+    ]
+
+
+class dfmi_out_column(C.Structure):
+    _fields_ = [
+        ("values", C.c_void_p),
+        ("validity", C.c_void_p),
+        ("offsets", C.c_void_p),
+        ("data", C.c_void_p),
+        ("data_capacity", C.c_int64),
+        ("type", C.c_int32),
+        ("passthrough_column", C.c_int32),
+        ("length", C.c_int64),
+        ("null_count", C.c_int64),
+        ("data_length", C.c_int64),
+    ]
+
+
+# Every symbol include/dfmi.h declares (checked by the CPU test suite).
+EXPORTED = [
+    "dfmi_compile_scalar_expr",
+    "dfmi_program_name",
+    "dfmi_program_type",
+    "dfmi_program_free",
+    "dfmi_context_create",
+    "dfmi_context_destroy",
+    "dfmi_context_set_stream",
+    "dfmi_filter_project",
+    "dfmi_last_timing",
+    "dfmi_generate_column",  # include/dfmi_datasource.h
+]
+
+DFMI_GEN_UNIT_F64 = 1
+DFMI_GEN_I64 = 2
+
+
+class PostfixNodes:
+    """Keeps a ctypes node array and the bytes its string pointers reference."""
+
+    def __init__(self, nodes: Sequence[dict]):
+        self._keep: List[bytes] = []
+        self.array = (dfmi_expr_node * len(nodes))()
+        for i, d in enumerate(nodes):
+            n = self.array[i]
+            n.kind = d.get("kind", 0)
+            n.op = d.get("op", 0)
+            n.data_type = d.get("data_type", 0)
+            n.column = d.get("column", 0)
+            n.i64 = d.get("i64", 0)
+            n.f64 = d.get("f64", 0.0)
+            s = d.get("str")
+            if s is not None:
+                self._keep.append(s)
+                n.str = s
+                n.str_len = len(s)
+        self.length = len(nodes)
+
+
+def make_schema(fields) -> tuple:
+    """fields: sequence of (name, DataType, nullable). Returns (schema, keepalive)."""
+    arr = (dfmi_field * max(1, len(fields)))()
+    keep = []
+    for i, (name, dt, nullable) in enumerate(fields):
+        b = name.encode("utf-8")
+        keep.append(b)
+        arr[i].name = b
+        arr[i].type = int(dt)
+        arr[i].nullable = 1 if nullable else 0
+    s = dfmi_schema()
+    s.num_fields = len(fields)
+    s.fields = arr
+    return s, (arr, keep)
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load libdfmi.so (built in-tree by __graft_entry__.build()). Fails loudly."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libdfmi.so is not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    L.dfmi_compile_scalar_expr.argtypes = [C.POINTER(dfmi_expr_node), C.c_int32, C.POINTER(dfmi_schema),
+                                           C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(dfmi_error)]
+    L.dfmi_compile_scalar_expr.restype = C.c_int32
+    L.dfmi_program_name.argtypes = [C.c_void_p]
+    L.dfmi_program_name.restype = C.c_char_p
+    L.dfmi_program_type.argtypes = [C.c_void_p]
+    L.dfmi_program_type.restype = C.c_int32
+    L.dfmi_program_free.argtypes = [C.c_void_p]
+    L.dfmi_program_free.restype = None
+    L.dfmi_context_create.argtypes = [C.c_int32, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(dfmi_error)]
+    L.dfmi_context_create.restype = C.c_int32
+    L.dfmi_context_destroy.argtypes = [C.c_void_p]
+    L.dfmi_context_destroy.restype = None
+    L.dfmi_context_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    L.dfmi_context_set_stream.restype = C.c_int32
+    L.dfmi_filter_project.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                      C.POINTER(dfmi_batch), C.POINTER(dfmi_out_column), C.c_uint32,
+                                      C.POINTER(dfmi_error)]
+    L.dfmi_filter_project.restype = C.c_int32
+    L.dfmi_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.dfmi_last_timing.restype = C.c_int32
+    L.dfmi_generate_column.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64,
+                                       C.c_int64, C.c_int64, C.c_void_p, C.POINTER(dfmi_error)]
+    L.dfmi_generate_column.restype = C.c_int32
+    _LIB = L
+    return L

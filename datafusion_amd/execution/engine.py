@@ -1,0 +1,151 @@
+"""The HBM side of the boundary: moves Arrow buffers into HBM, allocates the
+output buffers and runs one fused dfmi_filter_project per input batch.
+
+One DeviceEngine per GPU (per process); it owns a dfmi_context whose stream
+is torch's current stream on that device, so torch events time our kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import torch
+
+from .. import _abi
+from ..arrow import Array, RecordBatch, empty_bytes
+from ..logicalplan import Column, DataType
+from .error import ExecutionError
+
+_ENGINES = {}
+
+
+def engine(device=None) -> "DeviceEngine":
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _ENGINES:
+        _ENGINES[idx] = DeviceEngine(idx)
+    return _ENGINES[idx]
+
+
+def column_struct(a: Array) -> _abi.dfmi_column:
+    c = _abi.dfmi_column()
+    c.type = int(a.data_type)
+    c.length = a.length
+    c.null_count = a.null_count
+    c.validity = a.validity.data_ptr() if a.validity is not None else None
+    c.values = a.values.data_ptr()
+    c.offsets = a.offsets.data_ptr() if a.offsets is not None else None
+    return c
+
+
+class DeviceEngine:
+    def __init__(self, index: int):
+        if not torch.cuda.is_available():
+            raise RuntimeError("the MI355X path needs a GPU (torch.cuda.is_available() is False)")
+        self.index = index
+        self.device = torch.device("cuda", index)
+        L = _abi.lib()
+        ctx = C.c_void_p()
+        err = _abi.dfmi_error()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = L.dfmi_context_create(index, C.c_void_p(stream), C.byref(ctx), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode())
+        self.ctx = ctx
+
+    def __del__(self):
+        try:
+            if self.ctx:
+                _abi.lib().dfmi_context_destroy(self.ctx)
+        except Exception:
+            pass
+
+    def last_timing(self):
+        t, m = C.c_double(), C.c_double()
+        if _abi.lib().dfmi_last_timing(self.ctx, C.byref(t), C.byref(m)) != _abi.DFMI_OK:
+            return None
+        return t.value, m.value
+
+    def to_device(self, batch: RecordBatch) -> RecordBatch:
+        if all(c.values.device == self.device for c in batch.columns):
+            return batch
+        return batch.to(self.device)
+
+    def _alloc_out(self, t: DataType, n: int, need_validity: bool, utf8_capacity: int):
+        oc = _abi.dfmi_out_column()
+        keep = {}
+        if t == DataType.Utf8:
+            keep["offsets"] = torch.zeros(max(16, n + 1 + 15), dtype=torch.int32, device=self.device)
+            keep["data"] = empty_bytes(max(utf8_capacity, 8), self.device)
+            oc.offsets = keep["offsets"].data_ptr()
+            oc.data = keep["data"].data_ptr()
+            oc.data_capacity = keep["data"].numel()
+        else:
+            nbytes = (n + 63) // 64 * 8 if t == DataType.Boolean else n * max(t.width, 1)
+            keep["values"] = empty_bytes(nbytes, self.device)
+            oc.values = keep["values"].data_ptr()
+        if need_validity:
+            keep["validity"] = empty_bytes((n + 63) // 64 * 8, self.device)
+            oc.validity = keep["validity"].data_ptr()
+        return oc, keep
+
+    def filter_project(self, predicate, projections: Optional[Sequence], batch: RecordBatch,
+                       flags: int = 0) -> List[Array]:
+        """One pull of ProjectRelation(FilterRelation(batch)). ``predicate`` /
+        ``projections`` are RuntimeExprs (None / [] when absent)."""
+        L = _abi.lib()
+        batch = self.to_device(batch)
+        n = batch.num_rows()
+        cols = batch.columns
+        projections = list(projections or [])
+        carr = (_abi.dfmi_column * max(1, len(cols)))()
+        for i, a in enumerate(cols):
+            carr[i] = column_struct(a)
+        cb = _abi.dfmi_batch()
+        cb.num_columns = len(cols)
+        cb.num_rows = n
+        cb.columns = carr
+
+        if projections:
+            out_types = [p.get_type() for p in projections]
+            src_cols = [p.expr.index if isinstance(p.expr, Column) else None for p in projections]
+        else:
+            out_types = [c.data_type for c in cols]
+            src_cols = list(range(len(cols)))
+        outs = (_abi.dfmi_out_column * max(1, len(out_types)))()
+        keeps = []
+        for o, t in enumerate(out_types):
+            passthrough = predicate is None and src_cols[o] is not None
+            if passthrough:
+                keeps.append({})
+                continue
+            cap = 0
+            if t == DataType.Utf8 and src_cols[o] is not None:
+                cap = cols[src_cols[o]].values.numel()
+            oc, keep = self._alloc_out(t, n, predicate is None, cap)
+            outs[o] = oc
+            keeps.append(keep)
+
+        progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
+        err = _abi.dfmi_error()
+        L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        rc = L.dfmi_filter_project(self.ctx, predicate.handle if predicate is not None else None,
+                                   progs, len(projections), C.byref(cb), outs, flags, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        result = []
+        for o, t in enumerate(out_types):
+            oc = outs[o]
+            if oc.passthrough_column >= 0:
+                result.append(cols[oc.passthrough_column])
+                continue
+            k = keeps[o]
+            length = oc.length
+            nulls = oc.null_count
+            if t == DataType.Utf8:
+                result.append(Array(t, length, k["data"], None, k["offsets"], 0))
+            else:
+                result.append(Array(t, length, k["values"], k.get("validity") if nulls else None, None, nulls))
+        return result

@@ -1,0 +1,230 @@
+/*
+ * dfmi.h — C ABI of the MI355X-native Selection + Projection path.
+ *
+ * This is the drop-in boundary for the only data-parallel path of the reference
+ * (ariesdevil/datafusion v0.5.1): expression compilation plus the
+ * FilterRelation/ProjectRelation per-batch evaluation in src/execution/.
+ * Every entry point names the reference interface it replaces (file:line under
+ * the reference tree). No torch or HIP types appear in the signatures: device
+ * buffers are plain pointers, streams are opaque `void*` (hipStream_t).
+ *
+ * Semantics follow the reference bit-for-bit (see DESIGN.md "Semantics"):
+ *   - comparisons never produce nulls; null ordering is arrow 0.12's bool_op
+ *     (NULL < x is true, NULL = NULL is true, ...);
+ *   - math propagates nulls, Float64 rounds once per operator (no FMA);
+ *   - a non-null zero divisor is ArrowError(DivideByZero);
+ *   - a Selection drops validity and copies raw slot bits of selected rows;
+ *   - only Float64 and Utf8 columns can be filtered unless an extension flag
+ *     is given (filter.rs:106-110).
+ */
+#ifndef DFMI_H
+#define DFMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFMI_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------
+ * Types. Subset of arrow::datatypes::DataType that logicalplan.rs can name
+ * (ScalarValue logicalplan.rs:93-108, get_supertype logicalplan.rs:443-551).
+ * ------------------------------------------------------------------------- */
+typedef enum dfmi_type {
+    DFMI_TYPE_NULL = 0, /* ScalarValue::Null only */
+    DFMI_TYPE_BOOLEAN = 1,
+    DFMI_TYPE_INT8 = 2,
+    DFMI_TYPE_INT16 = 3,
+    DFMI_TYPE_INT32 = 4,
+    DFMI_TYPE_INT64 = 5,
+    DFMI_TYPE_UINT8 = 6,
+    DFMI_TYPE_UINT16 = 7,
+    DFMI_TYPE_UINT32 = 8,
+    DFMI_TYPE_UINT64 = 9,
+    DFMI_TYPE_FLOAT32 = 10,
+    DFMI_TYPE_FLOAT64 = 11,
+    DFMI_TYPE_UTF8 = 12
+} dfmi_type;
+
+/* Status codes: ExecutionError variants (error.rs:27-35) plus the ArrowError
+ * kinds array_ops can raise, plus Rust panics and ABI failures. */
+typedef enum dfmi_status {
+    DFMI_OK = 0,
+    DFMI_ERR_EXECUTION = 1,       /* ExecutionError::ExecutionError(String) */
+    DFMI_ERR_GENERAL = 2,         /* ExecutionError::General(String) */
+    DFMI_ERR_INVALID_COLUMN = 3,  /* ExecutionError::InvalidColumn(String) */
+    DFMI_ERR_NOT_IMPLEMENTED = 4, /* ExecutionError::NotImplemented(String) */
+    DFMI_ERR_DIVIDE_BY_ZERO = 5,  /* ExecutionError::ArrowError(DivideByZero) */
+    DFMI_ERR_ARROW_COMPUTE = 6,   /* ExecutionError::ArrowError(ComputeError) */
+    DFMI_ERR_PANIC = 7,           /* the reference panics (unwrap / i64 overflow) */
+    DFMI_ERR_INVALID_ARGUMENT = 8,/* ABI misuse (bad pointer, alignment, sizes) */
+    DFMI_ERR_CAPACITY = 9,        /* caller-provided output buffer too small */
+    DFMI_ERR_DEVICE = 10          /* HIP runtime failure / device timeout */
+} dfmi_status;
+
+typedef struct dfmi_error {
+    int32_t code;       /* dfmi_status */
+    char message[500];  /* the reference's message text for that error */
+} dfmi_error;
+
+/* ---------------------------------------------------------------------------
+ * Columnar batch (Arrow 0.12 memory layout, arrow::record_batch::RecordBatch).
+ *   fixed width: `values` holds length * width bytes, native little-endian;
+ *   Boolean: `values` is an LSB-first bitmap;
+ *   Utf8 (BinaryArray): `offsets` holds length+1 int32, `values` the bytes.
+ * `validity` is an LSB-first bitmap, NULL when the column has no nulls.
+ * Bitmaps and values must be 8-byte aligned; device pointers for execution.
+ * ------------------------------------------------------------------------- */
+typedef struct dfmi_column {
+    int32_t type;            /* dfmi_type */
+    int32_t reserved;
+    int64_t length;          /* rows */
+    int64_t null_count;
+    const uint8_t* validity; /* NULL => all valid */
+    const void* values;
+    const int32_t* offsets;  /* Utf8 only */
+} dfmi_column;
+
+typedef struct dfmi_batch {
+    int32_t num_columns;
+    int32_t reserved;
+    int64_t num_rows;
+    const dfmi_column* columns;
+} dfmi_batch;
+
+typedef struct dfmi_field {     /* arrow::datatypes::Field */
+    const char* name;
+    int32_t type;               /* dfmi_type */
+    int32_t nullable;
+} dfmi_field;
+
+typedef struct dfmi_schema {    /* arrow::datatypes::Schema */
+    int32_t num_fields;
+    int32_t reserved;
+    const dfmi_field* fields;
+} dfmi_schema;
+
+/* ---------------------------------------------------------------------------
+ * Expressions: logicalplan::Expr (logicalplan.rs:133-164) flattened to
+ * postfix order (children first, left before right), i.e. the order in which
+ * compile_scalar_expr (expression.rs:244) evaluates them.
+ * ------------------------------------------------------------------------- */
+typedef enum dfmi_expr_kind {
+    DFMI_EXPR_COLUMN = 1,             /* Expr::Column(index) */
+    DFMI_EXPR_LITERAL = 2,            /* Expr::Literal(ScalarValue) */
+    DFMI_EXPR_BINARY = 3,             /* Expr::BinaryExpr{left, op, right} */
+    DFMI_EXPR_CAST = 4,               /* Expr::Cast{expr, data_type} */
+    DFMI_EXPR_IS_NULL = 5,            /* Expr::IsNull */
+    DFMI_EXPR_IS_NOT_NULL = 6,        /* Expr::IsNotNull */
+    DFMI_EXPR_SORT = 7,               /* Expr::Sort */
+    DFMI_EXPR_SCALAR_FUNCTION = 8,    /* Expr::ScalarFunction */
+    DFMI_EXPR_AGGREGATE_FUNCTION = 9  /* Expr::AggregateFunction */
+} dfmi_expr_kind;
+
+typedef enum dfmi_operator {          /* logicalplan::Operator (logicalplan.rs:67-81) */
+    DFMI_OP_EQ = 0,
+    DFMI_OP_NOT_EQ = 1,
+    DFMI_OP_LT = 2,
+    DFMI_OP_LT_EQ = 3,
+    DFMI_OP_GT = 4,
+    DFMI_OP_GT_EQ = 5,
+    DFMI_OP_PLUS = 6,
+    DFMI_OP_MINUS = 7,
+    DFMI_OP_MULTIPLY = 8,
+    DFMI_OP_DIVIDE = 9,
+    DFMI_OP_MODULUS = 10,
+    DFMI_OP_AND = 11,
+    DFMI_OP_OR = 12
+} dfmi_operator;
+
+typedef struct dfmi_expr_node {
+    int32_t kind;       /* dfmi_expr_kind */
+    int32_t op;         /* BINARY: dfmi_operator; SORT: asc (1/0) */
+    int32_t data_type;  /* LITERAL: ScalarValue variant; CAST/functions: target type */
+    int32_t column;     /* COLUMN: index; functions: argument count */
+    int64_t i64;        /* LITERAL Int*, UInt* (bit pattern), Boolean (0/1) */
+    double f64;         /* LITERAL Float32/Float64 (Float32 stored widened) */
+    const char* str;    /* LITERAL Utf8 bytes; functions: name */
+    int64_t str_len;
+} dfmi_expr_node;
+
+/* Extension flags. 0 = exactly the reference's behaviour. */
+#define DFMI_FLAG_EXT_GATHER_ALL   0x1u /* filter Int64 (and other fixed-width) columns
+                                           instead of "filter not supported for ..." */
+#define DFMI_FLAG_EXT_UTF8_COMPARE 0x2u /* Utf8 literals and Utf8 =/!= comparisons
+                                           instead of "No support for literal type" */
+
+/* Opaque compiled expression: the RuntimeExpr::Compiled of expression.rs:43-50. */
+typedef struct dfmi_program dfmi_program;
+
+/* compile_scalar_expr (expression.rs:244-451). Rejects exactly what the
+ * reference rejects at compile time, with the same error variant and text.
+ * Errors the reference raises only when the closure runs (comparison_ops,
+ * math_ops, panics) are recorded in the program and reported by execution. */
+int32_t dfmi_compile_scalar_expr(const dfmi_expr_node* nodes, int32_t num_nodes,
+                                 const dfmi_schema* input_schema, uint32_t flags,
+                                 dfmi_program** out, dfmi_error* err);
+
+/* RuntimeExpr::get_name / get_type (expression.rs:64-77). */
+const char* dfmi_program_name(const dfmi_program* program);
+int32_t dfmi_program_type(const dfmi_program* program);
+void dfmi_program_free(dfmi_program* program);
+
+/* ---------------------------------------------------------------------------
+ * Execution context: one per (GPU, stream). Holds the look-back tile-status
+ * workspace, result counters and error words. Not thread-safe; one host
+ * thread per context (the reference is single-threaded, context.rs:33).
+ * ------------------------------------------------------------------------- */
+typedef struct dfmi_context dfmi_context;
+
+int32_t dfmi_context_create(int32_t device, void* hip_stream, dfmi_context** out,
+                            dfmi_error* err);
+void dfmi_context_destroy(dfmi_context* ctx);
+/* Rebind the stream used by later calls (e.g. torch's current stream). */
+int32_t dfmi_context_set_stream(dfmi_context* ctx, void* hip_stream);
+
+/* Output column. The caller provides device buffers sized for the worst case:
+ *   values:   num_rows * width bytes (Boolean: ceil(num_rows/8), 8-padded);
+ *   validity: ceil(num_rows/8) bytes, 8-padded (only written without a predicate);
+ *   offsets:  (num_rows+1) int32 for Utf8;
+ *   data:     Utf8 bytes, data_capacity >= input column's byte length.
+ * The library fills the fields below the line. */
+typedef struct dfmi_out_column {
+    void* values;
+    uint8_t* validity;
+    int32_t* offsets;
+    uint8_t* data;
+    int64_t data_capacity;
+    /* ---- filled by dfmi_filter_project ---- */
+    int32_t type;                /* dfmi_type of the result array */
+    int32_t passthrough_column;  /* >=0: result IS that input column (Arc clone,
+                                    expression.rs:272-276); buffers untouched */
+    int64_t length;
+    int64_t null_count;          /* 0 => validity not written / not needed */
+    int64_t data_length;         /* Utf8 bytes written */
+} dfmi_out_column;
+
+/* One pull of ProjectRelation::next(FilterRelation::next(batch))
+ * (projection.rs:45-66, filter.rs:46-72, filter() filter.rs:80-111),
+ * fused into one pass over HBM.
+ *   predicate == NULL       : no Selection in the plan (projection only);
+ *   num_projections == 0    : no Projection: FilterRelation output = every
+ *                             input column filtered (outputs has num_columns);
+ * The call is synchronous: on return `outputs[i].length` is the batch's row
+ * count. Errors are the ones the reference's next() returns. */
+int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* predicate,
+                            const dfmi_program* const* projections, int32_t num_projections,
+                            const dfmi_batch* input, dfmi_out_column* outputs,
+                            uint32_t flags, dfmi_error* err);
+
+/* Device time in milliseconds of the last dfmi_filter_project's kernels
+ * (HIP events on the context stream), and the dominant kernel's share. */
+int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main_kernel_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFMI_H */

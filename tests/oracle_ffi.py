@@ -1,0 +1,173 @@
+"""Test-only bridge to the CPU oracle (oracle/liboracle.so). The oracle is the
+checker: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline use it."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from datafusion_amd import _abi
+from datafusion_amd.arrow import Array, Field, RecordBatch, Schema, _bytes_tensor, _offsets_tensor
+from datafusion_amd.logicalplan import DataType, Expr
+from datafusion_amd.execution.error import ExecutionError
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+_L = None
+
+
+def oracle_lib() -> C.CDLL:
+    global _L
+    if _L is not None:
+        return _L
+    if not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    L = C.CDLL(ORACLE_SO)
+    P = C.POINTER
+    L.oracle_filter_project.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(P(_abi.dfmi_expr_node)),
+                                        P(C.c_int32), C.c_int32, P(_abi.dfmi_schema), P(_abi.dfmi_batch),
+                                        C.c_uint32, P(C.c_void_p), P(_abi.dfmi_error)]
+    L.oracle_filter_project.restype = C.c_int32
+    L.oracle_run_batched.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(P(_abi.dfmi_expr_node)),
+                                     P(C.c_int32), C.c_int32, P(_abi.dfmi_schema), P(_abi.dfmi_batch),
+                                     C.c_int64, C.c_uint32, P(C.c_int64), P(_abi.dfmi_error)]
+    L.oracle_run_batched.restype = C.c_int32
+    L.oracle_result_num_columns.argtypes = [C.c_void_p]
+    L.oracle_result_num_columns.restype = C.c_int32
+    L.oracle_result_column.argtypes = [C.c_void_p, C.c_int32, P(_abi.dfmi_column), P(C.c_char_p)]
+    L.oracle_result_column.restype = C.c_int32
+    L.oracle_result_free.argtypes = [C.c_void_p]
+    L.oracle_compile_info.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(_abi.dfmi_schema), C.c_uint32,
+                                      C.c_char_p, C.c_int64, P(C.c_int32), P(_abi.dfmi_error)]
+    L.oracle_compile_info.restype = C.c_int32
+    L.oracle_gen_unit_f64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_void_p]
+    L.oracle_gen_i64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_void_p]
+    _L = L
+    return L
+
+
+def _host_column(a: Array) -> _abi.dfmi_column:
+    assert a.values.device.type == "cpu"
+    c = _abi.dfmi_column()
+    c.type = int(a.data_type)
+    c.length = a.length
+    c.null_count = a.null_count
+    c.validity = a.validity.data_ptr() if a.validity is not None else None
+    c.values = a.values.data_ptr()
+    c.offsets = a.offsets.data_ptr() if a.offsets is not None else None
+    return c
+
+
+def _copy_out(col: _abi.dfmi_column) -> Array:
+    t = DataType(col.type)
+    n = col.length
+    if t == DataType.Utf8:
+        offs = np.ctypeslib.as_array(C.cast(col.offsets, C.POINTER(C.c_int32)), shape=(n + 1,)).copy()
+        nbytes = int(offs[-1])
+        data = np.ctypeslib.as_array(C.cast(col.values, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes].copy()
+        values = _bytes_tensor(data)
+        offsets = _offsets_tensor(offs, "cpu")
+    else:
+        nbytes = (n + 7) // 8 if t == DataType.Boolean else n * t.width
+        raw = np.ctypeslib.as_array(C.cast(col.values, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes].copy()
+        values = _bytes_tensor(raw)
+        offsets = None
+    validity = None
+    if col.null_count:
+        vb = np.ctypeslib.as_array(C.cast(col.validity, C.POINTER(C.c_uint8)), shape=((n + 7) // 8,)).copy()
+        validity = _bytes_tensor(vb)
+    return Array(t, n, values, validity, offsets, col.null_count)
+
+
+class Batched:
+    """Host batch in ctypes form (keeps the tensors alive)."""
+
+    def __init__(self, batch: RecordBatch):
+        self.batch = batch.to("cpu")
+        cols = self.batch.columns
+        self.carr = (_abi.dfmi_column * max(1, len(cols)))()
+        for i, a in enumerate(cols):
+            self.carr[i] = _host_column(a)
+        self.cb = _abi.dfmi_batch()
+        self.cb.num_columns = len(cols)
+        self.cb.num_rows = self.batch.num_rows()
+        self.cb.columns = self.carr
+
+
+def _prog_args(predicate: Optional[Expr], projections: Sequence[Expr]):
+    pn = _abi.PostfixNodes(predicate.to_postfix()) if predicate is not None else None
+    projs = [_abi.PostfixNodes(e.to_postfix()) for e in projections]
+    parr = (C.POINTER(_abi.dfmi_expr_node) * max(1, len(projs)))(
+        *[C.cast(p.array, C.POINTER(_abi.dfmi_expr_node)) for p in projs])
+    lens = (C.c_int32 * max(1, len(projs)))(*[p.length for p in projs])
+    return pn, projs, parr, lens
+
+
+def oracle_filter_project(schema: Schema, batch: RecordBatch, predicate: Optional[Expr],
+                          projections: Sequence[Expr], flags: int = 0):
+    """Returns (list of (name, Array)) or raises ExecutionError."""
+    L = oracle_lib()
+    hb = Batched(batch)
+    sch, keep = _abi.make_schema([(f.name, f.data_type, f.nullable) for f in schema.fields])
+    pn, projs, parr, lens = _prog_args(predicate, projections)
+    out = C.c_void_p()
+    err = _abi.dfmi_error()
+    rc = L.oracle_filter_project(pn.array if pn else None, pn.length if pn else 0, parr, lens, len(projs),
+                                 C.byref(sch), C.byref(hb.cb), flags, C.byref(out), C.byref(err))
+    if rc != 0:
+        raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+    try:
+        res = []
+        for i in range(L.oracle_result_num_columns(out)):
+            col = _abi.dfmi_column()
+            name = C.c_char_p()
+            L.oracle_result_column(out, i, C.byref(col), C.byref(name))
+            res.append((name.value.decode("utf-8", errors="surrogateescape"), _copy_out(col)))
+        return res
+    finally:
+        L.oracle_result_free(out)
+
+
+def oracle_run_batched(schema: Schema, batch: RecordBatch, predicate, projections, batch_rows: int,
+                       flags: int = 0) -> int:
+    L = oracle_lib()
+    hb = Batched(batch)
+    sch, keep = _abi.make_schema([(f.name, f.data_type, f.nullable) for f in schema.fields])
+    pn, projs, parr, lens = _prog_args(predicate, projections)
+    rows = C.c_int64()
+    err = _abi.dfmi_error()
+    rc = L.oracle_run_batched(pn.array if pn else None, pn.length if pn else 0, parr, lens, len(projs),
+                              C.byref(sch), C.byref(hb.cb), batch_rows, flags, C.byref(rows), C.byref(err))
+    if rc != 0:
+        raise ExecutionError.from_status(rc, err.message.decode())
+    return rows.value
+
+
+def oracle_compile(expr: Expr, schema: Schema, flags: int = 0):
+    """(name, type) or raises ExecutionError — compile_scalar_expr restated."""
+    L = oracle_lib()
+    nodes = _abi.PostfixNodes(expr.to_postfix())
+    sch, keep = _abi.make_schema([(f.name, f.data_type, f.nullable) for f in schema.fields])
+    name = C.create_string_buffer(4096)
+    t = C.c_int32()
+    err = _abi.dfmi_error()
+    rc = L.oracle_compile_info(nodes.array, nodes.length, C.byref(sch), flags, name, 4096, C.byref(t), C.byref(err))
+    if rc != 0:
+        raise ExecutionError.from_status(rc, err.message.decode())
+    return name.value.decode("utf-8", errors="surrogateescape"), DataType(t.value)
+
+
+def gen_unit_f64(seed: int, col: int, row0: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.float64)
+    oracle_lib().oracle_gen_unit_f64(seed, col, row0, n, out.ctypes.data)
+    return out
+
+
+def gen_i64(seed: int, col: int, row0: int, n: int, lo: int, hi: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.int64)
+    oracle_lib().oracle_gen_i64(seed, col, row0, n, lo, hi, out.ctypes.data)
+    return out

@@ -1,0 +1,328 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the
+same inputs. Bit-exact for masks, integers, Utf8 and comparisons; Float64
+bit-exact too (one rounding per operator on both sides, -ffp-contract=off),
+except NaN payloads, which are compared by class (x86 and gfx950 produce
+different default-NaN bit patterns; DESIGN.md "Semantics")."""
+import numpy as np
+import pytest
+import torch
+
+from datafusion_amd._abi import DFMI_FLAG_EXT_GATHER_ALL, DFMI_FLAG_EXT_UTF8_COMPARE
+from datafusion_amd.arrow import Array, Field, RecordBatch, Schema
+from datafusion_amd.execution import ExecutionContext, MemoryDataSource
+from datafusion_amd.execution.engine import engine
+from datafusion_amd.execution.error import ExecutionError
+from datafusion_amd.execution.expression import compile_scalar_expr
+from datafusion_amd.logicalplan import (BinaryExpr, Cast, Column, DataType, Float64, Int64, Literal, Operator,
+                                        Utf8, binary_expr_coerced)
+from golden_cases import CITIES, GOLDEN, NUMERICS, all_types_schema, expected_rows, load_batch, lit_expr
+from oracle_ffi import gen_i64, gen_unit_f64, oracle_filter_project
+
+pytestmark = pytest.mark.gpu
+
+CMP = [Operator.Eq, Operator.NotEq, Operator.Lt, Operator.LtEq, Operator.Gt, Operator.GtEq]
+MATH = [Operator.Plus, Operator.Minus, Operator.Multiply, Operator.Divide]
+
+
+def assert_same(dev: Array, ref: Array, what=""):
+    assert dev.data_type == ref.data_type, what
+    assert dev.length == ref.length, (what, dev.length, ref.length)
+    assert dev.null_count == ref.null_count, (what, dev.null_count, ref.null_count)
+    n = ref.length
+    if ref.null_count:
+        assert np.array_equal(dev.valid_mask(), ref.valid_mask()), what
+    dv, rv = dev.numpy_values(), ref.numpy_values()
+    if ref.data_type == DataType.Utf8:
+        assert dv == rv, what
+        return
+    if ref.data_type == DataType.Boolean:
+        assert np.array_equal(dv, rv), what
+        return
+    if ref.data_type in (DataType.Float64, DataType.Float32):
+        dn, rn = np.isnan(dv), np.isnan(rv)
+        assert np.array_equal(dn, rn), what
+        ib = dv.view(np.uint64 if ref.data_type == DataType.Float64 else np.uint32)
+        rb = rv.view(np.uint64 if ref.data_type == DataType.Float64 else np.uint32)
+        assert np.array_equal(ib[~dn], rb[~rn]), (what, np.flatnonzero(ib[~dn] != rb[~rn])[:5])
+        return
+    assert np.array_equal(dv, rv), what
+
+
+def run_both(schema, batch, pred, projs, flags=0):
+    """Device result (list of Arrays) and oracle result, or the two errors."""
+    ref_err = dev_err = None
+    try:
+        ref = oracle_filter_project(schema, batch, pred, projs, flags)
+    except ExecutionError as e:
+        ref_err = e
+    try:
+        p = compile_scalar_expr(None, pred, schema, flags) if pred is not None else None
+        cp = [compile_scalar_expr(None, e, schema, flags) for e in projs]
+        dev = engine().filter_project(p, cp, batch, flags)
+        names = [c.get_name() for c in cp] if cp else [f.name for f in schema.fields]
+    except ExecutionError as e:
+        dev_err = e
+    if ref_err is not None or dev_err is not None:
+        assert ref_err is not None and dev_err is not None, (ref_err, dev_err)
+        assert (dev_err.kind, dev_err.message) == (ref_err.kind, ref_err.message)
+        return None
+    assert len(dev) == len(ref)
+    for i, ((rname, r), d) in enumerate(zip(ref, dev)):
+        assert names[i] == rname
+        assert_same(d.cpu(), r, "%s col %d" % (rname, i))
+    return dev, ref
+
+
+def synth(n, seed=42, nullable=False, int64=False, null_frac=0.1):
+    """a, b, c columns: Float64 in [0,1) or Int64 in [-2^20, 2^20)."""
+    cols = []
+    fields = []
+    rng = np.random.default_rng(seed)
+    for j, name in enumerate("abc"):
+        if int64:
+            v = gen_i64(seed, j, 0, n, -(1 << 20), 1 << 20)
+            t = DataType.Int64
+        else:
+            v = gen_unit_f64(seed, j, 0, n)
+            t = DataType.Float64
+        valid = (rng.random(n) >= null_frac) if nullable else None
+        cols.append(Array.from_numpy(t, v, valid))
+        fields.append(Field(name, t, nullable))
+    s = Schema(fields)
+    return s, RecordBatch(s, cols)
+
+
+# ------------------------------------------------------------ known answers
+def test_csv_sql_example_on_gpu():
+    """examples/csv_sql.rs:56 through ExecutionContext.sql on the device."""
+    ctx = ExecutionContext()
+    batch = load_batch(CITIES, "uk_cities.csv", has_header=True)
+    ctx.register_datasource("cities", MemoryDataSource(CITIES, [batch]))
+    rel = ctx.sql("SELECT city, lat, lng, lat + lng FROM cities WHERE lat > 51.0 AND lat < 53")
+    b = rel.next()
+    assert b.num_rows() == 18 and b.num_columns() == 4
+    assert [f.name for f in b.schema.fields] == ["city", "lat", "lng", "#1 Plus #2"]
+    city, lat, lng, comb = [c.cpu().to_pylist() for c in b.columns]
+    assert (city[0], lat[0], lng[0], comb[0]) == ("Solihull, Birmingham, UK", 52.412811, -1.778197, 50.634614)
+    assert repr(comb[city.index("Oxford, Oxfordshire, UK")]) == "50.494344999999996"
+    assert rel.next() is None
+    pred = lit_expr(CITIES, 1, Operator.Gt, Float64(51.0))
+    run_both(CITIES, batch, BinaryExpr(pred, Operator.And, lit_expr(CITIES, 1, Operator.Lt, Int64(53))),
+             [Column(0), Column(1), Column(2), BinaryExpr(Column(1), Operator.Plus, Column(2))])
+
+
+def test_filter_fixture_on_gpu():
+    batch = load_batch(CITIES, "uk_cities.csv", has_header=False)
+    exp = [ln.rsplit(",", 2) for ln in open(GOLDEN + "/expected/test_filter.csv", encoding="utf-8").read().splitlines() if ln]
+    res = run_both(CITIES, batch, lit_expr(CITIES, 1, Operator.Gt, Float64(52.0)), [])
+    city, lat, lng = [c.cpu().to_pylist() for c in res[0]]
+    assert [[c, repr(a), repr(b)] for c, a, b in zip(city, lat, lng)] == [[e[0], repr(float(e[1])), repr(float(e[2]))] for e in exp]
+
+
+@pytest.mark.parametrize("fname,op", [("c_float64_high.csv", Operator.Gt), ("c_float64_low.csv", Operator.Lt)])
+def test_all_types_float64_on_gpu(fname, op):
+    s = all_types_schema(f64_col=10)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    dev, _ = run_both(s, batch, lit_expr(s, 10, op, Float64(0.5)), [Column(10)])
+    assert dev[0].cpu().to_pylist() == [float(r[0]) for r in expected_rows(fname)]
+    run_both(s, batch, lit_expr(s, 10, op, Float64(0.5)), [])  # FilterRelation output, 11 Utf8 gathers
+
+
+@pytest.mark.parametrize("fname,op", [("c_int64_positive.csv", Operator.Gt), ("c_int64_negative.csv", Operator.Lt)])
+def test_all_types_int64_on_gpu(fname, op):
+    s = all_types_schema(i64_col=8)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    pred = lit_expr(s, 8, op, Int64(0))
+    assert run_both(s, batch, pred, [Column(8)]) is None  # "filter not supported for Int64"
+    dev, _ = run_both(s, batch, pred, [Column(8)], DFMI_FLAG_EXT_GATHER_ALL)
+    assert dev[0].cpu().to_pylist() == [int(r[0]) for r in expected_rows(fname)]
+
+
+@pytest.mark.parametrize("op", MATH)
+def test_numerics_on_gpu(op):
+    batch = load_batch(NUMERICS, "numerics.csv", has_header=True)
+    S = NUMERICS
+    exprs = [binary_expr_coerced(Column(0), op, Column(1), S), binary_expr_coerced(Column(0), op, Literal(Int64(2)), S),
+             binary_expr_coerced(Column(2), op, Column(3), S), binary_expr_coerced(Column(2), op, Literal(Int64(2)), S),
+             binary_expr_coerced(Column(2), op, Literal(Float64(2.5)), S)]
+    run_both(S, batch, None, exprs)
+    run_both(S, batch, lit_expr(S, 2, Operator.GtEq, Float64(2.5)), exprs[2:], 0)
+
+
+# ------------------------------------------------------------ synthetic
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 1000, 1024, 4097, 1 << 20, 1_000_003])
+@pytest.mark.parametrize("sel", [0.01, 0.5, 0.99])
+def test_c2_float64(n, sel):
+    s, batch = synth(n)
+    k, m = 1 - sel ** 0.5, sel ** 0.5
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(k))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Float64(m))))
+    proj = [Column(0), Column(1),
+            BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus, Column(2))]
+    res = run_both(s, batch, pred, proj)
+    if n >= 1 << 20:
+        got = res[0][0].length / n
+        assert abs(got - sel) < 0.01
+
+
+@pytest.mark.parametrize("n", [1000, 1_000_003])
+def test_c2_int64(n):
+    s, batch = synth(n, int64=True)
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Int64(-1000))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Int64(5000))))
+    proj = [Column(0), Column(1),
+            BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus, Column(2))]
+    assert run_both(s, batch, pred, proj) is None  # Int64 gather is an extension
+    run_both(s, batch, pred, proj, DFMI_FLAG_EXT_GATHER_ALL)
+
+
+@pytest.mark.parametrize("op", CMP)
+@pytest.mark.parametrize("int64", [False, True])
+def test_nullable_comparisons(op, int64):
+    """arrow 0.12 bool_op null ordering (parity unpinned: restated)."""
+    n = 5000
+    s, batch = synth(n, seed=7, nullable=True, int64=int64, null_frac=0.3)
+    lit = Int64(0) if int64 else Float64(0.5)
+    flags = DFMI_FLAG_EXT_GATHER_ALL
+    run_both(s, batch, BinaryExpr(Column(0), op, Column(1)), [Column(0), Column(2)], flags)
+    run_both(s, batch, BinaryExpr(Column(0), op, Literal(lit)), [Column(1)], flags)
+    run_both(s, batch, BinaryExpr(Literal(lit), op, Column(1)), [Column(0)], flags)
+    # comparison outputs (Boolean) in the select list, with and without a filter
+    run_both(s, batch, None, [BinaryExpr(Column(0), op, Column(1))], flags)
+    run_both(s, batch, BinaryExpr(Column(2), Operator.Gt, Literal(lit)), [BinaryExpr(Column(0), op, Column(1))], flags)
+
+
+@pytest.mark.parametrize("op", MATH)
+@pytest.mark.parametrize("int64", [False, True])
+def test_nullable_math(op, int64):
+    n = 3000
+    s, batch = synth(n, seed=11, nullable=True, int64=int64, null_frac=0.2)
+    flags = DFMI_FLAG_EXT_GATHER_ALL
+    if op == Operator.Divide and int64:
+        # make divisors non-zero to test values (zero divisors tested below)
+        return
+    # projection only: null propagation + validity bitmap + null counts
+    run_both(s, batch, None, [BinaryExpr(Column(0), op, Column(1)), BinaryExpr(Column(2), op, Column(0))], flags)
+    # in the predicate (nulls propagate, then compare)
+    lit = Int64(0) if int64 else Float64(0.5)
+    run_both(s, batch, BinaryExpr(BinaryExpr(Column(0), op, Column(1)), Operator.Lt, Literal(lit)),
+             [Column(2), BinaryExpr(Column(0), op, Column(1))], flags)
+
+
+def test_boolean_columns_and_or():
+    n = 4000
+    rng = np.random.default_rng(3)
+    f1 = Array.from_numpy(DataType.Boolean, rng.random(n) < 0.5, rng.random(n) < 0.8)
+    f2 = Array.from_numpy(DataType.Boolean, rng.random(n) < 0.5, rng.random(n) < 0.8)
+    x = Array.from_numpy(DataType.Float64, gen_unit_f64(5, 0, 0, n))
+    s = Schema([Field("f1", DataType.Boolean, True), Field("f2", DataType.Boolean, True), Field("x", DataType.Float64, False)])
+    b = RecordBatch(s, [f1, f2, x])
+    for op in (Operator.And, Operator.Or):
+        # WHERE on a Boolean expression with nulls (null -> value bit 0 -> not selected)
+        run_both(s, b, BinaryExpr(Column(0), op, Column(1)), [Column(2)])
+        run_both(s, b, None, [BinaryExpr(Column(0), op, Column(1))])
+        run_both(s, b, None, [BinaryExpr(Column(0), op, BinaryExpr(Column(2), Operator.Gt, Literal(Float64(0.3))))])
+    run_both(s, b, Column(0), [Column(2)])  # WHERE f1: raw value bits
+    run_both(s, b, Column(0), [Column(2)], DFMI_FLAG_EXT_GATHER_ALL)
+    run_both(s, b, Column(0), [], DFMI_FLAG_EXT_GATHER_ALL)
+
+
+def test_divide_by_zero_and_overflow():
+    n = 2000
+    a = np.arange(n, dtype=np.int64) - 1000
+    d = np.ones(n, dtype=np.int64)
+    d[1500] = 0
+    s = Schema([Field("a", DataType.Int64, False), Field("d", DataType.Int64, False),
+                Field("x", DataType.Float64, False), Field("y", DataType.Float64, False)])
+    x = gen_unit_f64(1, 0, 0, n)
+    y = gen_unit_f64(1, 1, 0, n)
+    y[700] = -0.0
+    b = RecordBatch(s, [Array.from_numpy(DataType.Int64, a), Array.from_numpy(DataType.Int64, d),
+                        Array.from_numpy(DataType.Float64, x), Array.from_numpy(DataType.Float64, y)])
+    fl = DFMI_FLAG_EXT_GATHER_ALL
+    assert run_both(s, b, None, [BinaryExpr(Column(0), Operator.Divide, Column(1))], fl) is None
+    assert run_both(s, b, None, [BinaryExpr(Column(2), Operator.Divide, Column(3))], fl) is None
+    # the zero divisor row is filtered out -> no error in the projection
+    run_both(s, b, BinaryExpr(Column(0), Operator.Lt, Literal(Int64(400))),
+             [BinaryExpr(Column(0), Operator.Divide, Column(1)), BinaryExpr(Column(2), Operator.Divide, Column(3))], fl)
+    # ... but the predicate sees every row
+    assert run_both(s, b, BinaryExpr(BinaryExpr(Column(0), Operator.Divide, Column(1)), Operator.Lt,
+                                     Literal(Int64(400))), [Column(2)], fl) is None
+    # i64::MIN / -1 panics in the reference
+    a2 = a.copy()
+    a2[10] = np.iinfo(np.int64).min
+    d2 = d.copy()
+    d2[10] = -1
+    b2 = RecordBatch(s, [Array.from_numpy(DataType.Int64, a2), Array.from_numpy(DataType.Int64, d2), b.columns[2], b.columns[3]])
+    assert run_both(s, b2, None, [BinaryExpr(Column(0), Operator.Divide, Column(1))], fl) is None
+    # first failing operator wins: static comparison_ops after a dynamic DivideByZero
+    e = BinaryExpr(BinaryExpr(BinaryExpr(Column(2), Operator.Divide, Column(3)), Operator.Gt, Literal(Float64(1.0))),
+                   Operator.And, BinaryExpr(Column(0), Operator.Gt, Column(2)))
+    assert run_both(s, b, e, [Column(2)], fl) is None
+    e2 = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Column(2)), Operator.And,
+                    BinaryExpr(BinaryExpr(Column(2), Operator.Divide, Column(3)), Operator.Gt, Literal(Float64(1.0))))
+    assert run_both(s, b, e2, [Column(2)], fl) is None
+
+
+def test_utf8_gather_and_equality():
+    n = 5000
+    rng = np.random.default_rng(9)
+    words = [b"", b"w17", b"alpha", b"w1", b"\xe2\x82\xac uro", b"x" * 40]
+    strs = [words[i] for i in rng.integers(0, len(words), n)]
+    sv = [None if rng.random() < 0.1 else x for x in strs]
+    s = Schema([Field("s", DataType.Utf8, True), Field("v", DataType.Float64, True), Field("t", DataType.Utf8, False)])
+    b = RecordBatch(s, [Array.from_strings(sv), Array.from_numpy(DataType.Float64, gen_unit_f64(2, 0, 0, n)),
+                        Array.from_strings(strs[::-1])])
+    run_both(s, b, BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.3))), [Column(0), Column(2), Column(1)])
+    run_both(s, b, BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.3))), [])
+    # Utf8 equality is an extension (the reference rejects Utf8 literals)
+    pred = BinaryExpr(Column(0), Operator.Eq, Literal(Utf8("w17")))
+    assert run_both(s, b, pred, [Column(0)]) is None
+    for op in (Operator.Eq, Operator.NotEq):
+        run_both(s, b, BinaryExpr(Column(0), op, Literal(Utf8("w17"))), [Column(0), Column(1)], DFMI_FLAG_EXT_UTF8_COMPARE)
+        run_both(s, b, BinaryExpr(Column(0), op, Column(2)), [Column(2)], DFMI_FLAG_EXT_UTF8_COMPARE)
+
+
+def test_static_errors_match():
+    s, batch = synth(1000)
+    cases = [
+        (BinaryExpr(Column(0), Operator.Plus, Column(1)), [Column(0)]),  # not boolean
+        (BinaryExpr(Column(0), Operator.And, Column(1)), [Column(0)]),   # boolean_ops panic
+        (BinaryExpr(Column(0), Operator.Gt, Literal(Int64(1))), [Column(0)]),  # comparison_ops
+    ]
+    for pred, projs in cases:
+        assert run_both(s, batch, pred, projs) is None
+    # zero-row batch still raises the type errors
+    s0, b0 = synth(0)
+    assert run_both(s0, b0, cases[2][0], cases[2][1]) is None
+
+
+def test_projection_literals_and_passthrough():
+    s, batch = synth(10000, nullable=True)
+    run_both(s, batch, None, [Column(0), Literal(Int64(5)), Literal(Float64(2.5)), Cast(Literal(Int64(3)), DataType.Float64)])
+    run_both(s, batch, BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.5))),
+             [Literal(Int64(5)), Column(1), BinaryExpr(Literal(Float64(2.0)), Operator.Multiply, Column(2))])
+    # deep / non-left-deep arithmetic (LDS temporaries)
+    e = BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Minus,
+                   BinaryExpr(Column(2), Operator.Divide, BinaryExpr(Column(0), Operator.Plus, Literal(Float64(1.0)))))
+    run_both(s, batch, None, [e])
+    run_both(s, batch, BinaryExpr(e, Operator.Gt, Literal(Float64(0.0))), [e, Column(2)])
+
+
+def test_q6_style_predicate():
+    """C4: shipdate range, discount between, quantity < 24; extendedprice*discount."""
+    n = 200_000
+    rng = np.random.default_rng(6)
+    qty = rng.integers(1, 51, n).astype(np.float64)
+    disc = rng.integers(0, 11, n) / 100.0
+    ship = rng.integers(8036, 10562, n).astype(np.float64)
+    price = qty * rng.uniform(900, 2000, n)
+    s = Schema([Field(nm, DataType.Float64, False) for nm in ("l_quantity", "l_extendedprice", "l_discount", "l_shipdate")])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, v) for v in (qty, price, disc, ship)])
+    ctx = ExecutionContext()
+    ctx.register_datasource("lineitem", MemoryDataSource(s, [b]))
+    rel = ctx.sql("SELECT l_extendedprice * l_discount FROM lineitem WHERE l_shipdate >= 8766 AND l_shipdate < 9131 "
+                  "AND l_discount >= 0.05 AND l_discount <= 0.07 AND l_quantity < 24")
+    out = rel.next().columns[0].cpu().numpy_values()
+    m = (ship >= 8766) & (ship < 9131) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24)
+    assert np.array_equal(out, (price * disc)[m])

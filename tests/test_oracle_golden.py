@@ -1,0 +1,184 @@
+"""CPU suite: pin the oracle (CPU restatement) against every known-answer
+fixture the reference tree holds for this path."""
+import numpy as np
+import pytest
+
+from datafusion_amd._abi import DFMI_FLAG_EXT_GATHER_ALL
+from datafusion_amd.arrow import Field, Schema
+from datafusion_amd.execution.error import ExecutionError
+from datafusion_amd.logicalplan import (BinaryExpr, Cast, Column, DataType, Float64, Int64, Literal, Operator,
+                                        binary_expr_coerced)
+from datafusion_amd.sqlplanner import SqlToRel
+from golden_cases import (GOLDEN, CITIES, NUMERICS, all_types_schema, expected_rows, load_batch, lit_expr,
+                          smoketest_points)
+from oracle_ffi import oracle_compile, oracle_filter_project
+
+
+class _Ctx:
+    def __init__(self, schemas):
+        self.schemas = schemas
+
+    def table_schema(self, name):
+        return self.schemas.get(name)
+
+
+def plan(sql, schema, table="t"):
+    p = SqlToRel(_Ctx({table: schema})).sql_to_rel(sql)
+    pred = p.input.expr if type(p.input).__name__ == "Selection" else None
+    return pred, p.expr
+
+
+def test_csv_sql_example():
+    """examples/csv_sql.rs:56 over test/data/uk_cities.csv, has_header=true:
+    18 of 36 rows; first row Solihull; Oxford's combined 50.494344999999996."""
+    batch = load_batch(CITIES, "uk_cities.csv", has_header=True)
+    assert batch.num_rows() == 36
+    pred, projs = plan("SELECT city, lat, lng, lat + lng FROM cities WHERE lat > 51.0 AND lat < 53",
+                       CITIES, "cities")
+    assert repr(pred) == "#1 Gt Float64(51.0) And #1 Lt CAST(Int64(53) AS Float64)"
+    out = oracle_filter_project(CITIES, batch, pred, projs)
+    names = [n for n, _ in out]
+    assert names == ["city", "lat", "lng", "#1 Plus #2"]
+    city, lat, lng, comb = [a.to_pylist() for _, a in out]
+    assert len(city) == 18
+    assert (city[0], lat[0], lng[0], comb[0]) == ("Solihull, Birmingham, UK", 52.412811, -1.778197, 50.634614)
+    i = city.index("Oxford, Oxfordshire, UK")
+    assert repr(comb[i]) == "50.494344999999996"
+    for a, b, c in zip(lat, lng, comb):
+        assert c == a + b and 51.0 < a < 53
+
+
+def test_filter_fixture():
+    """expected/test_filter.csv = SELECT * FROM uk_cities WHERE lat > 52.0
+    (FilterRelation output, Utf8 + Float64 gather, no header row)."""
+    batch = load_batch(CITIES, "uk_cities.csv", has_header=False)
+    exp = [ln.rsplit(",", 2) for ln in open(GOLDEN + "/expected/test_filter.csv", encoding="utf-8").read().splitlines() if ln]
+    out = oracle_filter_project(CITIES, batch, lit_expr(CITIES, 1, Operator.Gt, Float64(52.0)), [])
+    city, lat, lng = [a.to_pylist() for _, a in out]
+    assert len(city) == len(exp) == 20
+    for (c, la, ln), e in zip(zip(city, lat, lng), exp):
+        assert c == e[0] and la == float(e[1]) and ln == float(e[2])
+
+
+@pytest.mark.parametrize("op,section,count", [(Operator.Lt, 0, 25), (Operator.GtEq, 1, 12)])
+def test_smoketest_predicates(op, section, count):
+    """smoketest-expected.txt:4-41 and expected/test_simple_predicate.csv:
+    lat < 53.0 -> 25 rows, lat >= 53.0 -> 12 rows."""
+    batch = load_batch(CITIES, "uk_cities.csv", has_header=False)
+    out = oracle_filter_project(CITIES, batch, lit_expr(CITIES, 1, op, Float64(53.0)), [Column(1), Column(2)])
+    lat, lng = [a.to_pylist() for _, a in out]
+    exp = smoketest_points(section)
+    assert len(lat) == len(exp) == count
+    assert list(zip(lat, lng)) == exp
+    if section == 0:
+        pts = [r[0] for r in expected_rows("test_simple_predicate.csv")]
+        assert ["POINT (%s %s)" % (repr(a).rstrip("0").rstrip("."), repr(b).rstrip("0").rstrip("."))
+                for a, b in zip(lat, lng)][:3] == pts[:3]
+
+
+@pytest.mark.parametrize("fname,op,count", [("c_float64_high.csv", Operator.Gt, 119),
+                                            ("c_float64_low.csv", Operator.Lt, 137)])
+def test_all_types_float64(fname, op, count):
+    """expected/c_float64_{high,low}.csv: column 10 of all_types_flat.csv vs 0.5."""
+    s = all_types_schema(f64_col=10)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    out = oracle_filter_project(s, batch, lit_expr(s, 10, op, Float64(0.5)), [Column(10)])
+    vals = out[0][1].to_pylist()
+    exp = [float(r[0]) for r in expected_rows(fname)]
+    assert len(vals) == count == len(exp)
+    assert vals == exp
+
+
+@pytest.mark.parametrize("fname,op,count", [("c_int64_positive.csv", Operator.Gt, 134),
+                                            ("c_int64_negative.csv", Operator.Lt, 122)])
+def test_all_types_int64(fname, op, count):
+    """expected/c_int64_{positive,negative}.csv: column 8 vs 0. The reference
+    refuses to filter Int64 (filter.rs:106-110); the extension flag gathers it."""
+    s = all_types_schema(i64_col=8)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    pred = lit_expr(s, 8, op, Int64(0))
+    with pytest.raises(ExecutionError) as e:
+        oracle_filter_project(s, batch, pred, [Column(8)])
+    assert e.value.kind == "ExecutionError" and e.value.message == "filter not supported for Int64"
+    out = oracle_filter_project(s, batch, pred, [Column(8)], DFMI_FLAG_EXT_GATHER_ALL)
+    vals = out[0][1].to_pylist()
+    exp = [int(r[0]) for r in expected_rows(fname)]
+    assert len(vals) == count and vals == exp
+
+
+@pytest.mark.parametrize("opname,op", [("plus", Operator.Plus), ("minus", Operator.Minus),
+                                       ("multiply", Operator.Multiply), ("divide", Operator.Divide)])
+def test_numerics(opname, op):
+    """expected/numerics_<op>_f64.csv: a OP b, a OP 2 (Int64) and
+    a_f OP b_f, a_f OP 2 (cast literal), a_f OP 2.5 (Float64) over numerics.csv."""
+    batch = load_batch(NUMERICS, "numerics.csv", has_header=True)
+    S = NUMERICS
+    exprs = [binary_expr_coerced(Column(0), op, Column(1), S), binary_expr_coerced(Column(0), op, Literal(Int64(2)), S),
+             binary_expr_coerced(Column(2), op, Column(3), S), binary_expr_coerced(Column(2), op, Literal(Int64(2)), S),
+             binary_expr_coerced(Column(2), op, Literal(Float64(2.5)), S)]
+    out = oracle_filter_project(S, batch, None, exprs)
+    got = [a.to_pylist() for _, a in out]
+    exp = expected_rows("numerics_%s_f64.csv" % opname)
+    assert len(exp) == 3
+    for r, e in enumerate(exp):
+        assert got[0][r] == int(e[0]) and got[1][r] == int(e[1])
+        for j, col in ((2, 3), (3, 4), (4, 5)):
+            assert got[j][r] == float(e[col]), (opname, r, j)
+    assert [n for n, _ in out][3] == "#2 %s CAST(Int64(2) AS Float64)" % op.name
+    # column 3 of the fixture (a OP 2.5) needs CAST(#0 AS Float64): not executable
+    with pytest.raises(ExecutionError) as e:
+        oracle_filter_project(S, batch, None, [binary_expr_coerced(Column(0), op, Literal(Float64(2.5)), S)])
+    assert e.value.message == "column reference"
+
+
+@pytest.mark.parametrize("opname,op", [("plus", Operator.Plus), ("minus", Operator.Minus),
+                                       ("multiply", Operator.Multiply), ("divide", Operator.Divide)])
+def test_numerics_float32(opname, op):
+    """expected/numerics_<op>.csv column 4: a_f OP b_f in Float32."""
+    S = Schema([Field("a", DataType.Int64, False), Field("b", DataType.Int64, False),
+                Field("a_f", DataType.Float32, False), Field("b_f", DataType.Float32, False)])
+    batch = load_batch(S, "numerics.csv", has_header=True)
+    out = oracle_filter_project(S, batch, None, [BinaryExpr(Column(2), op, Column(3))])
+    got = out[0][1].numpy_values()
+    exp = expected_rows("numerics_%s.csv" % opname)
+    for r, e in enumerate(exp):
+        assert got[r] == np.float32(e[3])
+
+
+def test_projection_unit_test():
+    """projection.rs:85-107: people.csv, project Column(0) -> one column "id"."""
+    S = Schema([Field("id", DataType.Int32, False), Field("first_name", DataType.Utf8, False)])
+    batch = load_batch(S, "people.csv", has_header=True)
+    out = oracle_filter_project(S, batch, None, [Column(0)])
+    assert len(out) == 1 and out[0][0] == "id"
+
+
+def test_compile_names_and_errors():
+    """compile_scalar_expr names/types and compile-time errors (expression.rs:244-451)."""
+    S = NUMERICS
+    assert oracle_compile(Literal(Int64(5)), S) == ("5", DataType.Int64)
+    assert oracle_compile(Literal(Float64(0.5)), S) == ("0.5", DataType.Float64)
+    assert oracle_compile(Literal(Float64(1.0)), S) == ("1", DataType.Float64)
+    assert oracle_compile(Cast(Literal(Int64(53)), DataType.Float64), S) == ("lit", DataType.Float64)
+    assert oracle_compile(BinaryExpr(Column(0), Operator.Plus, Column(1)), S) == ("#0 Plus #1", DataType.Int64)
+    assert oracle_compile(BinaryExpr(Column(2), Operator.Gt, Literal(Float64(2.0))), S) == \
+        ("#2 Gt Float64(2.0)", DataType.Boolean)
+
+    def err(e, flags=0):
+        with pytest.raises(ExecutionError) as x:
+            oracle_compile(e, S, flags)
+        return x.value.kind, x.value.message
+
+    from datafusion_amd.logicalplan import IsNull, ScalarValue, Utf8
+    assert err(Literal(Utf8("w17"))) == ("ExecutionError", 'No support for literal type Utf8("w17")')
+    assert err(Literal(ScalarValue(DataType.Boolean, True))) == ("ExecutionError",
+                                                                 "No support for literal type Boolean(true)")
+    assert err(Cast(Column(0), DataType.Float64)) == ("ExecutionError", "column reference")
+    assert err(Cast(Literal(Int64(1)), DataType.Int32)) == ("NotImplemented", "CAST from Int64 to Int32")
+    assert err(Cast(Literal(Float64(1.5)), DataType.Int64)) == ("NotImplemented",
+                                                               "CAST from Float64(1.5) to Int64")
+    assert err(Cast(BinaryExpr(Column(0), Operator.Plus, Column(1)), DataType.Float64)) == \
+        ("General", "CAST not implemented for expression #0 Plus #1")
+    assert err(BinaryExpr(Column(0), Operator.Modulus, Column(1))) == ("ExecutionError", "operator: Modulus")
+    assert err(IsNull(Column(0))) == ("ExecutionError", "expression #0 IS NULL")
+    assert err(Column(9))[0] == "panic"
