@@ -106,6 +106,8 @@ struct DLaunch {
     int32_t n_chan;
     int32_t n_tmp;
     int32_t chan_out[kMaxUtf8];   // Utf8 byte channel 1+u -> output index
+    int32_t mode;                 // diagnostics: bit0 tile=blockIdx, bit1 no look-back
+    int32_t n_lds;                // numeric columns 0..n_lds-1 staged in LDS
     DCol num[kMaxNum];
     DCol boolc[kMaxBoolCols];
     DCol utf8[kMaxUtf8];

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -20,12 +21,11 @@
 #include "../../include/dfmi_datasource.h"
 
 namespace dfmi {
-hipError_t launch_filter_project(const DLaunch& L, bool nullable, int nc, hipStream_t st);
-hipError_t launch_project(const DLaunch& L, bool nullable, int nc, hipStream_t st);
+hipError_t launch_filter_project(const DLaunch& L, bool nullable, int cfg, hipStream_t st);
+hipError_t launch_project(const DLaunch& L, bool nullable, int cfg, hipStream_t st);
 hipError_t launch_pack_bools(const uint8_t* bytes, uint8_t* bits, const unsigned long long* count,
                              long long max_rows, hipStream_t st);
-int pick_nc(int n_num);
-int tile_rows_for(int nc);
+int tile_rows_for(int cfg);
 }  // namespace dfmi
 
 using namespace dfmi;
@@ -570,14 +570,23 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         L.n_chan = n_chan;
         L.n_tmp = lw.tmp_max;
         L.n_rows = n;
+        if (const char* m = getenv("DFMI_DEBUG_MODE")) L.mode = atoi(m);  // diagnostics only
         lw.fill_columns();
 
         // ---- execute
         HIP_TRY(hipSetDevice(ctx->device));
         hipStream_t st = ctx->stream;
         ctx->timed = false;
-        const int nc = pick_nc(L.n_num);
+        int nc = 3;  // tile shape (kernels.hip host launchers): 1024 threads x 4 rows
+        if (const char* c = getenv("DFMI_TILE_CFG")) nc = atoi(c);  // diagnostics only
         const int tile = tile_rows_for(nc);
+        // stage as many numeric columns in LDS as fit 64 KiB per block
+        // (predicate columns first: Lower::collect registers them first)
+        {
+            const int cap = (int)(65536 / ((size_t)tile * 8)) - L.n_tmp;
+            L.n_lds = std::max(0, std::min(L.n_num, cap));
+            if (const char* c = getenv("DFMI_NO_LDS")) { if (atoi(c)) L.n_lds = 0; }  // diagnostics only
+        }
         const int64_t n_tiles = (n + tile - 1) / tile;
         if (n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
         L.n_tiles = (int32_t)n_tiles;
