@@ -186,7 +186,7 @@ def main():
                    "selectivity": round(h["s"], 4), "parallelism": "row-range shards, RCCL count all_gather"},
         "roofline": {"bound": "hbm", "achieved": round(h["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(h["achieved"] / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_filter_project", "kernel_ms": round(h["kms"], 4),
+                     "kernel": "dfmi_query (query-compiled filter+project)", "kernel_ms": round(h["kms"], 4),
                      "algorithmic_bytes_per_row": round(h["bpr"], 3)},
         "sweep": {("%.2f" % s): {"rows_per_s": n * world * args.steps / r["el"], "kernel_ms": round(r["kms"], 4),
                                  "hbm_gbs": round(r["achieved"], 1), "frac": round(r["achieved"] / HBM_PEAK_GBS, 4),

@@ -1,10 +1,11 @@
 // dfmi_filter_project: host side of the fused Selection + Projection pass.
 //
-// Lowers the compiled predicate / projections (dfmi_program IR) into one
-// device accumulator program (dfmi_internal.h), decides which input columns
-// the pass must load, launches k_filter_project (Selection present) or
-// k_project (projection only), and maps device error words back to the
-// reference's errors (FilterRelation::next filter.rs:46-72, filter()
+// Plans the pass from the compiled predicate / projections (dfmi_program IR):
+// static errors in the reference's evaluation order, output metadata, which
+// input columns the kernel loads (predicate columns for every row,
+// projection-only columns only where selected); gets the query kernel from
+// the query compiler (jit.cpp), launches it, and maps device error words back
+// to the reference's errors (FilterRelation::next filter.rs:46-72, filter()
 // filter.rs:80-111, ProjectRelation::next projection.rs:45-66).
 #include <hip/hip_runtime.h>
 
@@ -16,16 +17,14 @@
 #include <string>
 #include <vector>
 
-#include "dfmi_internal.h"
 #include "dfmi_program.h"
+#include "jit.h"
+#include "jit_skeleton.hip"
 #include "../../include/dfmi_datasource.h"
 
 namespace dfmi {
-hipError_t launch_filter_project(const DLaunch& L, bool nullable, int cfg, hipStream_t st);
-hipError_t launch_project(const DLaunch& L, bool nullable, int cfg, hipStream_t st);
 hipError_t launch_pack_bools(const uint8_t* bytes, uint8_t* bits, const unsigned long long* count,
                              long long max_rows, hipStream_t st);
-int tile_rows_for(int cfg);
 }  // namespace dfmi
 
 using namespace dfmi;
@@ -34,7 +33,6 @@ using namespace dfmi;
 static constexpr size_t kHdrTicket = 0;
 static constexpr size_t kHdrErr = 8;
 static constexpr size_t kHdrTotals = 16;
-static constexpr size_t kHdrBytes = 16 + 8 * (kMaxChan + kMaxOut) + 8;  // padded below
 static constexpr size_t kHdrAlloc = 512;
 
 struct dfmi_context {
@@ -46,16 +44,11 @@ struct dfmi_context {
     size_t scratch_bytes = 0;
     uint8_t* host_hdr = nullptr; // pinned copy of the header
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-    double last_total_ms = 0, last_main_ms = 0;
+    double last_total_ms = 0, last_main_ms = 0, last_compile_ms = 0;
     bool timed = false;
 };
 
 namespace {
-
-struct Fail {
-    int32_t code;
-    std::string msg;
-};
 
 void set_err(dfmi_error* err, int32_t code, const std::string& m) {
     if (!err) return;
@@ -94,247 +87,6 @@ struct Err {
     }
 };
 
-struct Opnd {
-    enum Kind { NUM, BOOL, UTF8COL, UTF8LIT } what = NUM;
-    int kind = KD_LIT;  // NUM: KD_*
-    int idx = 0;        // NUM index, bool slot, utf8 index, strlit index
-};
-
-struct Lower {
-    DLaunch L;
-    const dfmi_batch* in = nullptr;
-    uint32_t flags = 0;
-    std::vector<int> num_cols, bool_cols, utf8_cols;  // input column per slot
-    unsigned bool_used = 0;                           // bool temp slots in use
-    int tmp_depth = 0, tmp_max = 0;
-    int n_ins = 0, n_lits = 0, n_strlits = 0, strlit_bytes = 0;
-    int ordinal_base = 0;
-    bool nullable = false;
-
-    Lower() { memset(&L, 0, sizeof L); }
-
-    [[noreturn]] void limit(const std::string& what) {
-        throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: " + what};
-    }
-
-    int slot_of(std::vector<int>& v, int col, int cap, const char* what) {
-        for (size_t i = 0; i < v.size(); ++i)
-            if (v[i] == col) return (int)i;
-        if ((int)v.size() >= cap) limit(std::string("too many ") + what + " columns");
-        v.push_back(col);
-        return (int)v.size() - 1;
-    }
-
-    void collect(const dfmi_program* p) {  // pre-register referenced columns
-        for (const IrNode& n : p->ir) {
-            if (n.kind != IR_COL) continue;
-            if (n.type == DFMI_TYPE_BOOLEAN) slot_of(bool_cols, n.col, kMaxBoolCols, "Boolean");
-            else if (n.type == DFMI_TYPE_UTF8) slot_of(utf8_cols, n.col, kMaxUtf8, "Utf8");
-            else if (is8(n.type)) slot_of(num_cols, n.col, kMaxNum, "numeric");
-        }
-    }
-
-    int alloc_bool() {
-        for (int s = (int)bool_cols.size(); s < 32; ++s)
-            if (!(bool_used >> s & 1)) {
-                bool_used |= 1u << s;
-                return s;
-            }
-        limit("too many boolean temporaries");
-    }
-    void free_bool(int s) {
-        if (s >= (int)bool_cols.size()) bool_used &= ~(1u << s);
-    }
-
-    int lit(uint64_t bits) {
-        for (int i = 0; i < n_lits; ++i)
-            if (L.lits[i] == bits) return i;
-        if (n_lits >= kMaxLits) limit("too many literals");
-        L.lits[n_lits] = bits;
-        return n_lits++;
-    }
-
-    int strlit(const std::string& s) {
-        if (n_strlits >= kMaxStrLits || strlit_bytes + (int)s.size() > kStrLitBytes) limit("string literals");
-        L.strlit_off[n_strlits] = strlit_bytes;
-        L.strlit_len[n_strlits] = (int)s.size();
-        memcpy(L.strlit + strlit_bytes, s.data(), s.size());
-        strlit_bytes += (int)s.size();
-        return n_strlits++;
-    }
-
-    void emit(uint8_t op, int dst, int a, int b, int ka, int kb, int ordinal) {
-        if (n_ins >= kMaxIns) limit("too many instructions");
-        DIns& i = L.ins[n_ins++];
-        i.op = op;
-        i.dst = (uint8_t)dst;
-        i.a = (uint8_t)a;
-        i.b = (uint8_t)b;
-        i.ka = (uint8_t)ka;
-        i.kb = (uint8_t)kb;
-        i.ordinal = (uint16_t)(ordinal_base + ordinal);
-    }
-
-    static bool is_acc_producer(const dfmi_program* p, int i) {
-        const IrNode& n = p->ir[i];
-        return n.kind == IR_BIN && n.rt_code == 0 && n.op >= DFMI_OP_PLUS && n.op <= DFMI_OP_DIVIDE;
-    }
-
-    // Evaluate node i; numeric results come back as an operand (column,
-    // literal, or the accumulator), Booleans as a bool slot.
-    Opnd gen(const dfmi_program* p, int i) {
-        const IrNode& n = p->ir[i];
-        Opnd o;
-        if (n.kind == IR_COL) {
-            if (n.type == DFMI_TYPE_BOOLEAN) {
-                o.what = Opnd::BOOL;
-                o.idx = slot_of(bool_cols, n.col, kMaxBoolCols, "Boolean");
-            } else if (n.type == DFMI_TYPE_UTF8) {
-                o.what = Opnd::UTF8COL;
-                o.idx = slot_of(utf8_cols, n.col, kMaxUtf8, "Utf8");
-            } else if (is8(n.type)) {
-                o.kind = KD_COL;
-                o.idx = slot_of(num_cols, n.col, kMaxNum, "numeric");
-            } else {
-                throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
-                           std::string("device path: ") + type_debug(n.type) + " column in an expression"};
-            }
-            return o;
-        }
-        if (n.kind == IR_LIT) {
-            if (n.type == DFMI_TYPE_UTF8) {
-                o.what = Opnd::UTF8LIT;
-                o.idx = strlit(n.str);
-                return o;
-            }
-            if (!is8(n.type))
-                throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
-                           std::string("device path: ") + type_debug(n.type) + " literal"};
-            o.kind = KD_LIT;
-            o.idx = lit(n.bits);
-            return o;
-        }
-        // IR_BIN
-        if (n.rt_code) {
-            // The reference evaluates both children before failing here: lower
-            // them for their dynamic errors, then a placeholder value.
-            try {
-                Opnd a = gen(p, n.l);
-                if (a.what == Opnd::BOOL) free_bool(a.idx);
-                Opnd b = gen(p, n.r);
-                if (b.what == Opnd::BOOL) free_bool(b.idx);
-            } catch (const Fail&) {
-            }
-            if (n.type == DFMI_TYPE_BOOLEAN) {
-                o.what = Opnd::BOOL;
-                o.idx = alloc_bool();
-                emit(OP_BLIT, o.idx, 0, 0, 0, 0, n.ordinal);
-            } else {
-                o.kind = KD_LIT;
-                o.idx = lit(0);
-            }
-            return o;
-        }
-        const int op = n.op;
-        if (op == DFMI_OP_AND || op == DFMI_OP_OR) {
-            Opnd a = gen(p, n.l);
-            Opnd b = gen(p, n.r);
-            free_bool(a.idx);
-            free_bool(b.idx);
-            o.what = Opnd::BOOL;
-            o.idx = alloc_bool();
-            emit(op == DFMI_OP_AND ? OP_AND : OP_OR, o.idx, a.idx, b.idx, 0, 0, n.ordinal);
-            return o;
-        }
-        const int lt = p->ir[n.l].type;
-        if (lt == DFMI_TYPE_UTF8) {  // extension: Utf8 =, !=
-            Opnd a = gen(p, n.l);
-            Opnd b = gen(p, n.r);
-            const bool eq = op == DFMI_OP_EQ;
-            o.what = Opnd::BOOL;
-            o.idx = alloc_bool();
-            if (a.what == Opnd::UTF8LIT && b.what == Opnd::UTF8LIT) {
-                const bool same = p->ir[n.l].str == p->ir[n.r].str;
-                emit(OP_BLIT, o.idx, 0, (same == eq) ? 1 : 0, 0, 0, n.ordinal);
-            } else if (a.what == Opnd::UTF8COL && b.what == Opnd::UTF8COL) {
-                emit(eq ? OP_EQ_UTF8_COL : OP_NE_UTF8_COL, o.idx, a.idx, b.idx, 0, 0, n.ordinal);
-            } else {
-                const Opnd& c = a.what == Opnd::UTF8COL ? a : b;
-                const Opnd& s = a.what == Opnd::UTF8COL ? b : a;
-                emit(eq ? OP_EQ_UTF8_LIT : OP_NE_UTF8_LIT, o.idx, c.idx, s.idx, 0, 0, n.ordinal);
-            }
-            return o;
-        }
-        if (!is8(lt))
-            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("device path: ") + type_debug(lt) + " arithmetic"};
-        const bool f64 = lt == DFMI_TYPE_FLOAT64;
-        Opnd a, b;
-        int t = -1;
-        if (is_acc_producer(p, n.l) && is_acc_producer(p, n.r)) {
-            a = gen(p, n.l);
-            if (tmp_depth >= kMaxTmp) limit("expression too deep");
-            t = tmp_depth++;
-            tmp_max = std::max(tmp_max, tmp_depth);
-            emit(OP_SAVE, t, 0, 0, 0, 0, n.ordinal);
-            a.kind = KD_TMP;
-            a.idx = t;
-            b = gen(p, n.r);
-        } else {
-            a = gen(p, n.l);
-            b = gen(p, n.r);
-        }
-        static const uint8_t cmp_i[6] = {OP_EQ_I64, OP_NE_I64, OP_LT_I64, OP_LE_I64, OP_GT_I64, OP_GE_I64};
-        static const uint8_t cmp_f[6] = {OP_EQ_F64, OP_NE_F64, OP_LT_F64, OP_LE_F64, OP_GT_F64, OP_GE_F64};
-        static const uint8_t math_i[4] = {OP_ADD_I64, OP_SUB_I64, OP_MUL_I64, OP_DIV_I64};
-        static const uint8_t math_f[4] = {OP_ADD_F64, OP_SUB_F64, OP_MUL_F64, OP_DIV_F64};
-        if (op <= DFMI_OP_GT_EQ) {
-            o.what = Opnd::BOOL;
-            o.idx = alloc_bool();
-            emit(f64 ? cmp_f[op] : cmp_i[op], o.idx, a.idx, b.idx, a.kind, b.kind, n.ordinal);
-        } else {
-            emit(f64 ? math_f[op - DFMI_OP_PLUS] : math_i[op - DFMI_OP_PLUS], 0, a.idx, b.idx, a.kind,
-                 b.kind, n.ordinal);
-            o.kind = KD_ACC;
-            o.idx = 0;
-        }
-        if (t >= 0) --tmp_depth;
-        return o;
-    }
-
-    void fill_columns() {
-        L.n_num = (int)num_cols.size();
-        L.n_bool = (int)bool_cols.size();
-        L.n_utf8 = (int)utf8_cols.size();
-        const int64_t n = in->num_rows;
-        for (size_t i = 0; i < num_cols.size(); ++i) {
-            const dfmi_column& c = in->columns[num_cols[i]];
-            if (!c.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
-            if ((uintptr_t)c.values & 7) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values must be 8-byte aligned"};
-            L.num[i].values = c.values;
-            L.num[i].validity = (c.validity && c.null_count > 0) ? c.validity : nullptr;
-            L.num[i].bitmap_bytes = (n + 7) / 8;
-            nullable |= L.num[i].validity != nullptr;
-        }
-        for (size_t i = 0; i < bool_cols.size(); ++i) {
-            const dfmi_column& c = in->columns[bool_cols[i]];
-            if (!c.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
-            L.boolc[i].values = c.values;
-            L.boolc[i].validity = (c.validity && c.null_count > 0) ? c.validity : nullptr;
-            L.boolc[i].bitmap_bytes = (n + 7) / 8;
-            nullable |= L.boolc[i].validity != nullptr;
-        }
-        for (size_t i = 0; i < utf8_cols.size(); ++i) {
-            const dfmi_column& c = in->columns[utf8_cols[i]];
-            if (!c.values || !c.offsets) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 column buffers are NULL"};
-            L.utf8[i].values = c.values;
-            L.utf8[i].offsets = c.offsets;
-            L.utf8[i].validity = (c.validity && c.null_count > 0) ? c.validity : nullptr;
-            L.utf8[i].bitmap_bytes = (n + 7) / 8;
-            nullable |= L.utf8[i].validity != nullptr;
-        }
-    }
-};
-
 void ensure(dfmi_context* ctx, uint8_t** buf, size_t* have, size_t need) {
     if (*have >= need) return;
     if (*buf) HIP_TRY(hipFree(*buf));
@@ -343,6 +95,155 @@ void ensure(dfmi_context* ctx, uint8_t** buf, size_t* have, size_t need) {
     size_t cap = std::max(need, (size_t)1 << 20);
     HIP_TRY(hipMalloc(buf, cap));
     *have = cap;
+}
+
+// Everything about one call that does not need the device: static errors,
+// output metadata, the jit plan and the column slot tables.
+struct Built {
+    Err se;
+    jit::Plan plan;
+    jit::Launch X;
+    bool any_kernel_out = false;
+    int64_t n_tiles = 0;
+};
+
+void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
+                dfmi_out_column* outs, uint32_t flags, Built& B) {
+    Err& se = B.se;
+    jit::Plan& plan = B.plan;
+    jit::Launch& X = B.X;
+    bool& any_kernel_out = B.any_kernel_out;
+    const int64_t n = in->num_rows;
+    const int ncols = in->num_columns;
+    auto check_schema = [&](const dfmi_program* p) {
+        if ((int)p->schema_types.size() != ncols)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch does not match the compiled schema"};
+        for (int i = 0; i < ncols; ++i)
+            if (p->schema_types[i] != in->columns[i].type)
+                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch column type does not match the schema"};
+    };
+    if (pred) check_schema(pred);
+    for (int j = 0; j < np; ++j) {
+        if (!projs[j]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL projection"};
+        check_schema(projs[j]);
+    }
+    for (int i = 0; i < ncols; ++i)
+        if (in->columns[i].length != n) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
+
+    // ---- errors every evaluation of this plan raises (reference order)
+    const int P = pred ? pred->length : 0;
+    if (pred) {
+        for (const IrNode& nd : pred->ir)
+            if (nd.rt_code) se.offer((uint64_t)nd.ordinal << 44, nd.rt_code, nd.rt_msg);
+        if (pred->type != DFMI_TYPE_BOOLEAN)
+            se.offer((uint64_t)P << 44, DFMI_ERR_EXECUTION, "Filter expression did not evaluate to boolean");
+        for (int i = 0; i < ncols; ++i)
+            if (!gatherable(in->columns[i].type, flags)) {
+                se.offer((uint64_t)(P + 1) << 44, DFMI_ERR_EXECUTION,
+                         std::string("filter not supported for ") + type_debug(in->columns[i].type));
+                break;
+            }
+    }
+    std::vector<int> proj_base(np);
+    int base = P + 2;
+    for (int j = 0; j < np; ++j) {
+        proj_base[j] = base;
+        for (const IrNode& nd : projs[j]->ir)
+            if (nd.rt_code) se.offer((uint64_t)(base + nd.ordinal) << 44, nd.rt_code, nd.rt_msg);
+        base += projs[j]->length;
+    }
+    if (base >= (1 << 19)) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: expressions too long"};
+
+    // ---- output plan
+    const int nout = np > 0 ? np : ncols;
+    if (nout > 16) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many output columns"};
+    plan.pred = pred;
+    plan.outs.resize(nout);
+    X.in = in;
+    for (int o = 0; o < nout; ++o) {
+        dfmi_out_column& oc = outs[o];
+        const dfmi_program* p = np > 0 ? projs[o] : nullptr;
+        const IrNode* root = p ? &p->ir[p->root] : nullptr;
+        const bool is_col = !p || root->kind == IR_COL;
+        const int col = p ? root->col : o;
+        oc.type = p ? p->type : in->columns[o].type;
+        oc.passthrough_column = -1;
+        oc.length = 0;
+        oc.null_count = 0;
+        oc.data_length = 0;
+        jit::OutSpec& os = plan.outs[o];
+        os.out_type = oc.type;
+        if (is_col && !pred) {  // Arc clone of the input column (expression.rs:274)
+            const dfmi_column& c = in->columns[col];
+            oc.passthrough_column = col;
+            oc.length = n;
+            oc.null_count = c.validity ? c.null_count : 0;
+            continue;
+        }
+        if (is_col) {
+            const int ct = in->columns[col].type;
+            if (!gatherable(ct, flags)) continue;  // error raised at ordinal P+1
+            if (ct == DFMI_TYPE_UTF8) {
+                if (!oc.offsets || !oc.data) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 output buffers are NULL"};
+                os.kind = jit::OutSpec::UTF8;
+            } else if (is8(ct) || ct == DFMI_TYPE_BOOLEAN) {
+                if (!oc.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output values pointer is NULL"};
+                os.kind = jit::OutSpec::GATHER;
+            } else {
+                throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
+                           std::string("device path: gather of ") + type_debug(ct) + " columns"};
+            }
+            os.col = col;
+            any_kernel_out = true;
+            continue;
+        }
+        if (oc.type == DFMI_TYPE_UTF8) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device path: Utf8-valued projection"};
+        if (!oc.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output values pointer is NULL"};
+        os.kind = jit::OutSpec::EXPR;
+        os.prog = p;
+        os.ord_base = proj_base[o];
+        any_kernel_out = true;
+    }
+
+    // ---- column slots: predicate columns first, then projection-only ones
+    auto reg_num = [&](int col, std::vector<int>& phase) {
+        for (size_t i = 0; i < X.num_cols.size(); ++i)
+            if (X.num_cols[i] == col) return;
+        X.num_cols.push_back(col);
+        phase.push_back((int)X.num_cols.size() - 1);
+    };
+    auto reg_utf8 = [&](int col) {
+        for (size_t i = 0; i < X.utf8_cols.size(); ++i)
+            if (X.utf8_cols[i] == col) return (int)i;
+        X.utf8_cols.push_back(col);
+        return (int)X.utf8_cols.size() - 1;
+    };
+    auto reg_prog = [&](const dfmi_program* p, std::vector<int>& phase) {
+        for (const IrNode& nd : p->ir) {
+            if (nd.kind != IR_COL) continue;
+            if (nd.type == DFMI_TYPE_UTF8) reg_utf8(nd.col);
+            else if (is8(nd.type) || nd.type == DFMI_TYPE_BOOLEAN) reg_num(nd.col, phase);
+        }
+    };
+    if (pred) reg_prog(pred, X.pred_slots);
+    for (int o = 0; o < nout; ++o) {
+        const jit::OutSpec& os = plan.outs[o];
+        if (os.kind == jit::OutSpec::GATHER) reg_num(os.col, X.proj_slots);
+        else if (os.kind == jit::OutSpec::EXPR) reg_prog(os.prog, X.proj_slots);
+        else if (os.kind == jit::OutSpec::UTF8) X.utf8_outs.push_back({o, reg_utf8(os.col)});
+    }
+    if ((int)X.num_cols.size() > kArgCols || X.utf8_cols.size() > (size_t)kArgUtf8)
+        throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many input columns"};
+    // rows per thread: keep the tile's column data resident in VGPRs
+    const size_t nload = X.num_cols.size();
+    X.BLOCK = 512;
+    X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
+    if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
+    const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
+    const int64_t n_tiles = (n + tile_rows - 1) / tile_rows;
+    if (n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
+
+    B.n_tiles = n_tiles;
 }
 
 }  // namespace
@@ -406,243 +307,123 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         if (!ctx || !in || (np > 0 && !projs) || !outs || (in->num_columns > 0 && !in->columns))
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        Built B;
+        build_plan(pred, projs, np, in, outs, flags, B);
+        Err& se = B.se;
+        jit::Plan& plan = B.plan;
+        jit::Launch& X = B.X;
+        const bool any_kernel_out = B.any_kernel_out;
         const int64_t n = in->num_rows;
-        const int ncols = in->num_columns;
-        auto check_schema = [&](const dfmi_program* p) {
-            if ((int)p->schema_types.size() != ncols)
-                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch does not match the compiled schema"};
-            for (int i = 0; i < ncols; ++i)
-                if (p->schema_types[i] != in->columns[i].type)
-                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch column type does not match the schema"};
-        };
-        if (pred) check_schema(pred);
-        for (int j = 0; j < np; ++j) {
-            if (!projs[j]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL projection"};
-            check_schema(projs[j]);
-        }
-        for (int i = 0; i < ncols; ++i)
-            if (in->columns[i].length != n) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
+        const int nout = (int)plan.outs.size();
+        const int64_t n_tiles = B.n_tiles;
 
-        // ---- errors every evaluation of this plan raises (reference order)
-        Err se;
-        const int P = pred ? pred->length : 0;
-        if (pred) {
-            for (const IrNode& nd : pred->ir)
-                if (nd.rt_code) se.offer((uint64_t)nd.ordinal << 44, nd.rt_code, nd.rt_msg);
-            if (pred->type != DFMI_TYPE_BOOLEAN)
-                se.offer((uint64_t)P << 44, DFMI_ERR_EXECUTION, "Filter expression did not evaluate to boolean");
-            for (int i = 0; i < ncols; ++i)
-                if (!gatherable(in->columns[i].type, flags)) {
-                    se.offer((uint64_t)(P + 1) << 44, DFMI_ERR_EXECUTION,
-                             std::string("filter not supported for ") + type_debug(in->columns[i].type));
-                    break;
-                }
-        }
-        std::vector<int> proj_base(np);
-        int base = P + 2;
-        for (int j = 0; j < np; ++j) {
-            proj_base[j] = base;
-            for (const IrNode& nd : projs[j]->ir)
-                if (nd.rt_code) se.offer((uint64_t)(base + nd.ordinal) << 44, nd.rt_code, nd.rt_msg);
-            base += projs[j]->length;
-        }
-        if (base >= 65536) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: expressions too long"};
-
-        // ---- output list
-        const int nout = np > 0 ? np : ncols;
-        if (nout > kMaxOut) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many output columns"};
-        for (int o = 0; o < nout; ++o) {
-            dfmi_out_column& oc = outs[o];
-            oc.type = np > 0 ? projs[o]->type : in->columns[o].type;
-            oc.passthrough_column = -1;
-            oc.length = 0;
-            oc.null_count = 0;
-            oc.data_length = 0;
-        }
-
-        Lower lw;
-        lw.in = in;
-        lw.flags = flags;
-        DLaunch& L = lw.L;
-        if (pred) lw.collect(pred);
-        for (int j = 0; j < np; ++j) lw.collect(projs[j]);
-
-        // predicate program
-        if (pred) {
-            lw.ordinal_base = 0;
-            L.pred_begin = lw.n_ins;
-            Opnd r;
-            try {
-                r = lw.gen(pred, pred->root);
-            } catch (const Fail& f) {
-                if (se.set) throw Fail{se.code, se.msg};
-                throw;
-            }
-            L.pred_end = lw.n_ins;
-            if (r.what == Opnd::BOOL) {
-                L.pred_slot = r.idx;
-            } else {  // not Boolean: error at ordinal P; select nothing
-                L.pred_slot = lw.alloc_bool();
-                lw.emit(OP_BLIT, L.pred_slot, 0, 0, 0, 0, P);
-                L.pred_end = lw.n_ins;
-            }
-        }
-
-        // projections (or, without projections, FilterRelation's output = every column)
-        L.proj_begin = lw.n_ins;
-        int n_chan = 1;
-        bool any_kernel_out = false;
-        std::vector<int> bool_out;  // filtered Boolean outputs (scratch bytes)
-        for (int o = 0; o < nout; ++o) {
-            const dfmi_program* p = np > 0 ? projs[o] : nullptr;
-            const IrNode* root = p ? &p->ir[p->root] : nullptr;
-            const bool is_col = !p || root->kind == IR_COL;
-            const int col = p ? root->col : o;
-            if (is_col && !pred) {  // Arc clone of the input column (expression.rs:274)
-                const dfmi_column& c = in->columns[col];
-                outs[o].passthrough_column = col;
-                outs[o].length = n;
-                outs[o].null_count = c.validity ? c.null_count : 0;
-                continue;
-            }
-            if (is_col && pred && !gatherable(in->columns[col].type, flags)) continue;  // error at P+1
-            DOut& d = L.out[o];
-            d.values = outs[o].values;
-            d.validity = outs[o].validity;
-            d.offsets = outs[o].offsets;
-            d.data = outs[o].data;
-            d.data_cap = outs[o].data_capacity;
-            lw.ordinal_base = p ? proj_base[o] : 0;
-            const int ctype = is_col ? in->columns[col].type : root->type;
-            if (is_col && ctype == DFMI_TYPE_UTF8) {
-                if (!d.offsets || !d.data) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 output buffers are NULL"};
-                d.kind = OUT_GATHER_UTF8;
-                d.slot = lw.slot_of(lw.utf8_cols, col, kMaxUtf8, "Utf8");
-                if (n_chan >= kMaxChan) lw.limit("too many Utf8 outputs");
-                d.chan = n_chan;
-                L.chan_out[n_chan - 1] = o;
-                ++n_chan;
-                any_kernel_out = true;
-                continue;
-            }
-            if (!d.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output values pointer is NULL"};
-            any_kernel_out = true;
-            if (is_col) {
-                if (ctype == DFMI_TYPE_BOOLEAN) {
-                    d.kind = OUT_GATHER_BOOL;
-                    bool_out.push_back(o);
-                    lw.emit(OP_STORE_BOOL, o, lw.slot_of(lw.bool_cols, col, kMaxBoolCols, "Boolean"), 0, 0, 0, 0);
-                } else if (is8(ctype)) {
-                    d.kind = OUT_GATHER_NUM;
-                    lw.emit(OP_STORE_COL, o, lw.slot_of(lw.num_cols, col, kMaxNum, "numeric"), 0, 0, 0, 0);
-                } else {
-                    throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
-                               std::string("device path: gather of ") + type_debug(ctype) + " columns"};
-                }
-                continue;
-            }
-            Opnd r;
-            try {
-                r = lw.gen(p, p->root);
-            } catch (const Fail& f) {
-                if (se.set) throw Fail{se.code, se.msg};
-                throw;
-            }
-            if (r.what == Opnd::BOOL) {
-                d.kind = OUT_EXPR_BOOL;
-                if (pred) bool_out.push_back(o);
-                lw.emit(OP_STORE_BOOL, o, r.idx, 0, 0, 0, 0);
-                lw.free_bool(r.idx);
-            } else if (r.what == Opnd::NUM) {
-                d.kind = OUT_EXPR_NUM;
-                if (r.kind == KD_COL) {
-                    lw.emit(OP_STORE_COL, o, r.idx, 0, 0, 0, 0);
-                } else {
-                    if (r.kind != KD_ACC) lw.emit(OP_MOVE, 0, r.idx, 0, r.kind, 0, 0);
-                    lw.emit(OP_STORE_ACC, o, 0, 0, 0, 0, 0);
-                }
-            } else {
-                throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device path: Utf8-valued projection"};
-            }
-        }
-        L.proj_end = lw.n_ins;
-        L.n_out = nout;
-        L.n_chan = n_chan;
-        L.n_tmp = lw.tmp_max;
-        L.n_rows = n;
-        if (const char* m = getenv("DFMI_DEBUG_MODE")) L.mode = atoi(m);  // diagnostics only
-        lw.fill_columns();
-
-        // ---- execute
+        // ---- compile (cached per query shape) and launch
         HIP_TRY(hipSetDevice(ctx->device));
         hipStream_t st = ctx->stream;
         ctx->timed = false;
-        int nc = 3;  // tile shape (kernels.hip host launchers): 1024 threads x 4 rows
-        if (const char* c = getenv("DFMI_TILE_CFG")) nc = atoi(c);  // diagnostics only
-        const int tile = tile_rows_for(nc);
-        // stage as many numeric columns in LDS as fit 64 KiB per block
-        // (predicate columns first: Lower::collect registers them first)
-        {
-            const int cap = (int)(65536 / ((size_t)tile * 8)) - L.n_tmp;
-            L.n_lds = std::max(0, std::min(L.n_num, cap));
-            if (const char* c = getenv("DFMI_NO_LDS")) { if (atoi(c)) L.n_lds = 0; }  // diagnostics only
-        }
-        const int64_t n_tiles = (n + tile - 1) / tile;
-        if (n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
-        L.n_tiles = (int32_t)n_tiles;
-
         const bool launch = n > 0 && (pred || any_kernel_out);
         uint64_t dev_key = ~0ull;
         int dev_kind = 0;
+        Args A;
+        memset(&A, 0, sizeof A);
         if (launch) {
-            const size_t status_bytes = pred ? (size_t)n_chan * n_tiles * 8 : 0;
-            ensure(ctx, &ctx->ws, &ctx->ws_bytes, kHdrAlloc + status_bytes);
-            if (pred && !bool_out.empty())
-                ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, bool_out.size() * (size_t)((n + 63) & ~63ll));
-            L.ticket = (unsigned*)(ctx->ws + kHdrTicket);
-            L.err = (unsigned long long*)(ctx->ws + kHdrErr);
-            L.totals = (unsigned long long*)(ctx->ws + kHdrTotals);
-            L.status = (unsigned long long*)(ctx->ws + kHdrAlloc);
-            std::vector<uint8_t*> bool_dst;
-            if (pred) {
-                for (size_t i = 0; i < bool_out.size(); ++i) {
-                    DOut& d = L.out[bool_out[i]];
-                    bool_dst.push_back((uint8_t*)d.values);
-                    d.values = ctx->scratch + i * (size_t)((n + 63) & ~63ll);
-                }
+            hipFunction_t fn;
+            try {
+                fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
+            } catch (const Fail& f) {
+                if (se.set) throw Fail{se.code, se.msg};  // the reference fails first
+                throw;
             }
-            HIP_TRY(hipMemsetAsync(ctx->ws, 0, kHdrAlloc + status_bytes, st));
-            HIP_TRY(hipEventRecord(ctx->ev0, st));
-            if (pred) HIP_TRY(launch_filter_project(L, lw.nullable, nc, st));
-            else HIP_TRY(launch_project(L, lw.nullable, nc, st));
-            HIP_TRY(hipEventRecord(ctx->ev1, st));
-            for (size_t i = 0; i < bool_dst.size(); ++i)
-                HIP_TRY(launch_pack_bools((const uint8_t*)L.out[bool_out[i]].values, bool_dst[i],
-                                          L.totals, n, st));
-            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ctx->ws, kHdrAlloc, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipEventRecord(ctx->ev2, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
+            const size_t status_bytes = (size_t)n_chan * n_tiles * 8;
+            std::vector<int> bool_out;
+            for (int o = 0; o < nout; ++o)
+                if (pred && plan.outs[o].kind != jit::OutSpec::SKIP && plan.outs[o].kind != jit::OutSpec::UTF8 &&
+                    plan.outs[o].out_type == DFMI_TYPE_BOOLEAN)
+                    bool_out.push_back(o);
+            ensure(ctx, &ctx->ws, &ctx->ws_bytes, kHdrAlloc + status_bytes);
+            if (!bool_out.empty())
+                ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, bool_out.size() * (size_t)((n + 63) & ~63ll));
+            A.n_rows = n;
+            A.n_tiles = (int)n_tiles;
+            for (size_t s = 0; s < X.num_cols.size(); ++s) {
+                const dfmi_column& c = in->columns[X.num_cols[s]];
+                if (!c.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
+                if (c.type != DFMI_TYPE_BOOLEAN && ((uintptr_t)c.values & 7))
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values must be 8-byte aligned"};
+                A.col[s] = c.values;
+                A.valid[s] = (c.validity && c.null_count > 0) ? c.validity : nullptr;
+            }
+            for (size_t u = 0; u < X.utf8_cols.size(); ++u) {
+                const dfmi_column& c = in->columns[X.utf8_cols[u]];
+                if (!c.values || !c.offsets) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 column buffers are NULL"};
+                A.offs[u] = c.offsets;
+                A.bytes[u] = (const u8*)c.values;
+                A.svalid[u] = (c.validity && c.null_count > 0) ? c.validity : nullptr;
+            }
+            std::vector<uint8_t*> bool_dst(nout, nullptr);
+            for (int o = 0; o < nout; ++o) {
+                A.out[o] = outs[o].values;
+                A.out_valid[o] = pred ? nullptr : outs[o].validity;
+                A.out_offs[o] = outs[o].offsets;
+                A.out_data[o] = outs[o].data;
+                A.out_cap[o] = outs[o].data_capacity;
+            }
+            for (size_t i = 0; i < bool_out.size(); ++i) {
+                bool_dst[bool_out[i]] = (uint8_t*)outs[bool_out[i]].values;
+                A.out[bool_out[i]] = ctx->scratch + i * (size_t)((n + 63) & ~63ll);
+            }
+            memcpy(A.lits, X.args_lits, sizeof A.lits);
+            memcpy(A.str_off, X.str_off, sizeof A.str_off);
+            memcpy(A.str_len, X.str_len, sizeof A.str_len);
+            memcpy(A.str, X.str, sizeof A.str);
+            A.ticket = (unsigned*)(ctx->ws + kHdrTicket);
+            A.err = (unsigned long long*)(ctx->ws + kHdrErr);
+            A.totals = (unsigned long long*)(ctx->ws + kHdrTotals);
+            A.status = (unsigned long long*)(ctx->ws + kHdrAlloc);
+            A.mode = 0;
+            if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
+            for (int attempt = 0; attempt < 2; ++attempt) {
+                HIP_TRY(hipMemsetAsync(ctx->ws, 0, kHdrAlloc + status_bytes, st));
+                HIP_TRY(hipEventRecord(ctx->ev0, st));
+                size_t asz = sizeof A;
+                void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz,
+                               HIP_LAUNCH_PARAM_END};
+                HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)n_tiles, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
+                HIP_TRY(hipEventRecord(ctx->ev1, st));
+                for (int o = 0; o < nout; ++o)
+                    if (bool_dst[o])
+                        HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
+                HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ctx->ws, kHdrAlloc, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipEventRecord(ctx->ev2, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                uint64_t ew;
+                memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
+                dev_key = ~0ull;
+                dev_kind = 0;
+                if (ew) {
+                    dev_key = ~ew;
+                    dev_kind = (int)(dev_key & 15);
+                    dev_key &= ~15ull;
+                }
+                // blockIdx tile order could not resolve: re-run in ticket order
+                if (dev_kind == ERRK_LOOKBACK_TIMEOUT && !(A.mode & 1)) {
+                    A.mode |= 1;
+                    continue;
+                }
+                break;
+            }
             float m1 = 0, m2 = 0;
             (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
             (void)hipEventElapsedTime(&m2, ctx->ev0, ctx->ev2);
             ctx->last_main_ms = m1;
             ctx->last_total_ms = m2;
             ctx->timed = true;
-            uint64_t ew;
-            memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
-            if (ew) {
-                dev_key = ~ew;
-                dev_kind = (int)(dev_key & 15);
-                dev_key &= ~15ull;
-            }
         }
-        (void)kHdrBytes;
 
         // ---- errors: the reference raises the first in evaluation order
-        if (dev_kind == ERRK_LOOKBACK_TIMEOUT)
-            throw Fail{DFMI_ERR_DEVICE, "device look-back timed out"};
-        if (dev_kind == ERRK_CAPACITY)
-            throw Fail{DFMI_ERR_CAPACITY, "Utf8 output data_capacity too small"};
+        if (dev_kind == ERRK_LOOKBACK_TIMEOUT) throw Fail{DFMI_ERR_DEVICE, "device look-back timed out"};
+        if (dev_kind == ERRK_CAPACITY) throw Fail{DFMI_ERR_CAPACITY, "Utf8 output data_capacity too small"};
         if (dev_kind && (!se.set || dev_key < se.key)) {
             if (dev_kind == ERRK_DIV_ZERO) throw Fail{DFMI_ERR_DIVIDE_BY_ZERO, "DivideByZero"};
             throw Fail{DFMI_ERR_PANIC, "attempt to divide with overflow"};
@@ -650,7 +431,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         if (se.set) throw Fail{se.code, se.msg};
 
         // ---- results
-        uint64_t totals[kMaxChan + kMaxOut];
+        uint64_t totals[24];
         memset(totals, 0, sizeof totals);
         if (launch) memcpy(totals, ctx->host_hdr + kHdrTotals, sizeof totals);
         const int64_t out_rows = pred ? (int64_t)totals[0] : n;
@@ -658,10 +439,12 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             dfmi_out_column& oc = outs[o];
             if (oc.passthrough_column >= 0) continue;
             oc.length = out_rows;
-            oc.null_count = pred ? 0 : (int64_t)totals[kMaxChan + o];
-            if (L.out[o].kind == OUT_GATHER_UTF8) {
-                oc.data_length = (int64_t)totals[L.out[o].chan];
-                if (!launch || out_rows == 0) {  // offsets = [0]
+            oc.null_count = pred ? 0 : (int64_t)totals[8 + o];
+            if (plan.outs[o].kind == jit::OutSpec::UTF8) {
+                oc.data_length = 0;
+                for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                    if (X.utf8_outs[j].first == o) oc.data_length = (int64_t)totals[1 + j];
+                if (!launch) {  // offsets = [0] (a launch writes the final offset itself)
                     if (oc.offsets) HIP_TRY(hipMemsetAsync(oc.offsets, 0, 4, st));
                     oc.data_length = 0;
                 }
@@ -672,6 +455,29 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
         return f.code;
+    }
+}
+
+// Internal test hook (not part of the C ABI, not declared in include/):
+// generates the query kernel a dfmi_filter_project call would launch and, if
+// compile != 0, compiles it with hipRTC -- no device needed, so the CPU test
+// suite checks code generation for every expression shape it covers.
+// Returns the source length (the text is truncated to cap), or -status.
+extern "C" int64_t dfmi_internal_jit_check(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np,
+                                           const dfmi_batch* in, dfmi_out_column* outs, uint32_t flags,
+                                           int32_t compile, char* buf, int64_t cap, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!in || (np > 0 && !projs) || !outs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        Built B;
+        build_plan(pred, projs, np, in, outs, flags, B);
+        const std::string src = jit::generate(B.plan, B.X);
+        if (compile) (void)jit::compile_code(src, nullptr);
+        if (buf && cap > 0) snprintf(buf, (size_t)cap, "%s", src.c_str());
+        return (int64_t)src.size();
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return -(int64_t)f.code;
     }
 }
 

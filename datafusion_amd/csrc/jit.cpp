@@ -1,0 +1,405 @@
+// Query compiler: writes the query's Selection + Projection as one
+// straight-line gfx950 kernel over the hand-written skeleton
+// (jit_skeleton.hip), compiles it with hipRTC once per query shape and
+// launches it. Replaces the per-row interpretation of the reference's
+// compiled closures (expression.rs:29-451, filter.rs:80-111) -- and of an
+// earlier device interpreter here, whose per-operator decode made the pass
+// scalar-issue bound (DESIGN.md "Kernels").
+//
+// Shape of every generated kernel (filtered form):
+//   1. load the predicate's columns for the thread's K rows (all loads first);
+//   2. evaluate the predicate per row -> selection bits;
+//   3. lane-masked loads of projection-only columns (only where selected);
+//   4. ballot / per-(k,wave) counts, tile scan, decoupled look-back;
+//   5. evaluate projections, store compacted rows; Utf8 gathers.
+// Literal values and buffer addresses are kernel arguments, so one binary
+// serves every instance of a query shape.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "dfmi_program.h"
+#include "jit.h"
+
+extern const char dfmi_skeleton_src[];  // jit_skeleton.hip, embedded by the Makefile
+
+namespace dfmi {
+namespace jit {
+
+namespace {
+
+const char* cmp_sym(int op) {
+    static const char* s[] = {"==", "!=", "<", "<=", ">", ">="};
+    return s[op];
+}
+const char* math_sym(int op) {
+    static const char* s[] = {"+", "-", "*", "/"};
+    return s[op - DFMI_OP_PLUS];
+}
+
+bool is8(int t) { return t == DFMI_TYPE_INT64 || t == DFMI_TYPE_FLOAT64; }
+
+struct Val {
+    std::string v;  // C++ expression / local: u64 raw bits (numeric) or bool
+    std::string n;  // validity expression ("true" when statically valid)
+};
+
+}  // namespace
+
+// ------------------------------------------------------------- generator
+struct Gen {
+    const Plan& P;
+    Launch& X;  // slot tables + Args being filled
+    std::ostringstream o;
+    int tmp = 0;
+    bool filtered_cols = false;  // projection after a Selection: columns all-valid
+
+    Gen(const Plan& p, Launch& x) : P(p), X(x) {}
+
+    std::string t() { return "t" + std::to_string(tmp++); }
+
+    // one slot per literal node (no sharing of equal values: the source text,
+    // and so the compiled kernel, must not depend on literal values)
+    int lit(uint64_t b) {
+        if (X.n_lits >= 32) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "query compiler: too many literals"};
+        X.args_lits[X.n_lits] = b;
+        return X.n_lits++;
+    }
+    int strlit(const std::string& s) {
+        if (X.n_str >= 8 || X.str_bytes + (int)s.size() > 256)
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "query compiler: string literals too long"};
+        X.str_off[X.n_str] = X.str_bytes;
+        X.str_len[X.n_str] = (int)s.size();
+        memcpy(X.str + X.str_bytes, s.data(), s.size());
+        X.str_bytes += (int)s.size();
+        return X.n_str++;
+    }
+
+    // column value for the current row k (inside a per-k loop)
+    Val col(const IrNode& n) {
+        const int s = X.slot_of_col(n.col);
+        Val r;
+        if (n.type == DFMI_TYPE_BOOLEAN) {
+            r.v = "(((bw" + std::to_string(s) + "[k] >> lane) & 1) != 0)";
+        } else {
+            r.v = "c" + std::to_string(s) + "[k]";
+        }
+        r.n = (!filtered_cols && X.col_nullable(n.col))
+                  ? "(((vw" + std::to_string(s) + "[k] >> lane) & 1) != 0)"
+                  : "true";
+        return r;
+    }
+
+    // Emit node i of program p; act = C++ bool expression "row is evaluated".
+    Val emit(const dfmi_program* p, int i, int ord_base, const char* act) {
+        const IrNode& n = p->ir[i];
+        if (n.kind == IR_COL) {
+            if (n.type == DFMI_TYPE_UTF8) return Val{"", "true"};  // only inside Utf8 compares
+            if (!is8(n.type) && n.type != DFMI_TYPE_BOOLEAN)
+                throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
+                           std::string("device path: ") + type_debug(n.type) + " column in an expression"};
+            return col(n);
+        }
+        if (n.kind == IR_LIT) {
+            if (n.type == DFMI_TYPE_UTF8) return Val{"", "true"};
+            if (!is8(n.type))
+                throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("device path: ") + type_debug(n.type) + " literal"};
+            return Val{"A.lits[" + std::to_string(lit(n.bits)) + "]", "true"};
+        }
+        const int ord = ord_base + n.ordinal;
+        if (n.rt_code) {
+            // the reference evaluates both children before failing here
+            try {
+                emit(p, n.l, ord_base, act);
+                emit(p, n.r, ord_base, act);
+            } catch (const Fail&) {
+            }
+            return n.type == DFMI_TYPE_BOOLEAN ? Val{"false", "true"} : Val{"0ull", "true"};
+        }
+        const int op = n.op;
+        const IrNode& L = p->ir[n.l];
+        if (L.type == DFMI_TYPE_UTF8 && op <= DFMI_OP_GT_EQ) {  // extension: Utf8 =, !=
+            const IrNode& R = p->ir[n.r];
+            const bool eq = op == DFMI_OP_EQ;
+            const std::string v = t();
+            if (L.kind == IR_LIT && R.kind == IR_LIT) {
+                o << "    const bool " << v << " = " << (((L.str == R.str) == eq) ? "true" : "false") << ";\n";
+            } else if (L.kind == IR_COL && R.kind == IR_COL) {
+                const int u = X.slot_of_utf8(L.col), w = X.slot_of_utf8(R.col);
+                const std::string vu = filtered_cols ? "true" : "dfmi::utf8_valid(A, " + std::to_string(u) + ", row)";
+                const std::string vw = filtered_cols ? "true" : "dfmi::utf8_valid(A, " + std::to_string(w) + ", row)";
+                o << "    bool " << v << ";\n    { const bool a_ = " << vu << ", b_ = " << vw << ";\n"
+                  << "      const bool e_ = (a_ && b_) ? dfmi::utf8_eq_col(A, " << u << ", " << w << ", row) : (!a_ && !b_);\n"
+                  << "      " << v << " = " << (eq ? "e_" : "!e_") << "; }\n";
+            } else {
+                const IrNode& C = L.kind == IR_COL ? L : R;
+                const IrNode& S = L.kind == IR_COL ? R : L;
+                const int u = X.slot_of_utf8(C.col);
+                const int sl = strlit(S.str);
+                const std::string vu = filtered_cols ? "true" : "dfmi::utf8_valid(A, " + std::to_string(u) + ", row)";
+                o << "    const bool " << v << "_e = " << vu << " && dfmi::utf8_eq_lit(A, " << u << ", row, " << sl
+                  << ");\n";
+                o << "    const bool " << v << " = " << (eq ? "" : "!") << v << "_e;\n";
+            }
+            return Val{v, "true"};
+        }
+        const Val a = emit(p, n.l, ord_base, act);
+        const Val b = emit(p, n.r, ord_base, act);
+        const bool nul = a.n != "true" || b.n != "true";
+        if (op == DFMI_OP_AND || op == DFMI_OP_OR) {
+            const std::string v = t();
+            const std::string nn = nul ? "(" + a.n + " && " + b.n + ")" : "true";
+            o << "    const bool " << v << "_n = " << nn << ";\n";
+            o << "    const bool " << v << " = " << v << "_n && (" << a.v << (op == DFMI_OP_AND ? " && " : " || ")
+              << b.v << ");\n";  // null -> zero value bit (append_null)
+            return Val{v, nul ? v + "_n" : "true"};
+        }
+        const bool f = L.type == DFMI_TYPE_FLOAT64;
+        const std::string v = t();
+        if (op <= DFMI_OP_GT_EQ) {
+            const std::string x = f ? "dfmi::f64(" + a.v + ")" : "(i64)(" + a.v + ")";
+            const std::string y = f ? "dfmi::f64(" + b.v + ")" : "(i64)(" + b.v + ")";
+            if (nul) {
+                o << "    const bool " << v << " = dfmi::cmp_opt<" << op << ">(" << a.n << ", " << b.n << ", " << x << " "
+                  << cmp_sym(op) << " " << y << ");\n";
+            } else {
+                o << "    const bool " << v << " = " << x << " " << cmp_sym(op) << " " << y << ";\n";
+            }
+            return Val{v, "true"};
+        }
+        // math: null if either side is null (zero slot), one rounding per op
+        const std::string nn = nul ? "(" + a.n + " && " + b.n + ")" : "true";
+        if (nul) o << "    const bool " << v << "_n = " << nn << ";\n";
+        const std::string valid = nul ? v + "_n" : "true";
+        if (op == DFMI_OP_DIVIDE) {
+            if (f) {
+                o << "    if ((" << act << ") && " << valid << " && dfmi::f64(" << b.v
+                  << ") == 0.0) dfmi::report_err(A.err, " << ord << ", row, dfmi::ERRK_DIV_ZERO);\n";
+                o << "    u64 " << v << " = dfmi::bits(dfmi::f64(" << a.v << ") / dfmi::f64(" << b.v << "));\n";
+            } else {
+                o << "    if ((" << act << ") && " << valid << ") {\n"
+                  << "      if ((" << b.v << ") == 0ull) dfmi::report_err(A.err, " << ord
+                  << ", row, dfmi::ERRK_DIV_ZERO);\n"
+                  << "      else if ((i64)(" << b.v << ") == -1 && (" << a.v
+                  << ") == 0x8000000000000000ull) dfmi::report_err(A.err, " << ord << ", row, dfmi::ERRK_DIV_OVERFLOW);\n"
+                  << "    }\n";
+                o << "    u64 " << v << " = dfmi::sdiv64(" << a.v << ", " << b.v << ");\n";
+            }
+        } else if (f) {
+            o << "    u64 " << v << " = dfmi::bits(dfmi::f64(" << a.v << ") " << math_sym(op) << " dfmi::f64(" << b.v
+              << "));\n";
+        } else {
+            o << "    u64 " << v << " = (" << a.v << ") " << math_sym(op) << " (" << b.v << ");\n";
+        }
+        if (nul) o << "    if (!" << v << "_n) " << v << " = 0ull;\n";
+        return Val{v, valid};
+    }
+};
+
+// ------------------------------------------------------------ compile cache
+namespace {
+struct Compiled {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+};
+std::mutex g_mu;
+std::map<std::string, Compiled> g_cache;  // key: device + source text
+}  // namespace
+
+std::vector<char> compile_code(const std::string& src, double* compile_ms) {
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "dfmi_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        throw Fail{DFMI_ERR_DEVICE, "hiprtcCreateProgram failed"};
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
+                          "-Wno-unused-variable", "-Wno-unused-but-set-variable"};
+    const auto t0 = std::chrono::steady_clock::now();
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof *opts), opts);
+    if (compile_ms)
+        *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        if (getenv("DFMI_JIT_DUMP")) fprintf(stderr, "%s\n----\n%s\n", src.c_str(), log.c_str());
+        throw Fail{DFMI_ERR_DEVICE, "query compile failed: " + log.substr(0, 400)};
+    }
+    size_t size = 0;
+    hiprtcGetCodeSize(prog, &size);
+    std::vector<char> code(size);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    return code;
+}
+
+static hipFunction_t compile(int device, const std::string& src, double* compile_ms) {
+    const std::string key = std::to_string(device) + "\n" + src;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(key);
+    if (it != g_cache.end()) return it->second.fn;
+    const std::vector<char> code = compile_code(src, compile_ms);
+    Compiled c;
+    if (hipModuleLoadData(&c.mod, code.data()) != hipSuccess) throw Fail{DFMI_ERR_DEVICE, "hipModuleLoadData failed"};
+    if (hipModuleGetFunction(&c.fn, c.mod, "dfmi_query") != hipSuccess)
+        throw Fail{DFMI_ERR_DEVICE, "hipModuleGetFunction failed"};
+    g_cache[key] = c;
+    return c.fn;
+}
+
+size_t cache_size() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_cache.size();
+}
+
+// --------------------------------------------------------------- kernels
+static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Launch& X, const char* guard,
+                       bool valid_words) {
+    for (int s : slots) {
+        const int col = X.num_cols[s];
+        if (X.col_type(col) == DFMI_TYPE_BOOLEAN) {
+            o << "  u64 bw" << s << "[K];\n";
+            o << "#pragma unroll\n  for (int k = 0; k < K; ++k) bw" << s << "[k] = dfmi::bitmap_word((const u8*)A.col["
+              << s << "], (base >> 6) + k * WAVES + wave, A.n_rows);\n";
+        } else {
+            o << "  u64 c" << s << "[K];\n  { const u64* p_ = (const u64*)A.col[" << s << "] + base;\n"
+              << "#pragma unroll\n    for (int k = 0; k < K; ++k) c" << s << "[k] = (" << guard
+              << ") ? p_[k * BLOCK + tid] : 0ull; }\n";
+        }
+        if (valid_words && X.col_nullable(col)) {
+            o << "  u64 vw" << s << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) vw" << s
+              << "[k] = dfmi::bitmap_word(A.valid[" << s << "], (base >> 6) + k * WAVES + wave, A.n_rows);\n";
+        }
+    }
+}
+
+std::string generate(const Plan& P, Launch& X) {
+    Gen g(P, X);
+    std::ostringstream& o = g.o;
+    const int K = X.K, BLOCK = X.BLOCK;
+    o << "\n// ---- generated query kernel ----\n";
+    o << "extern \"C\" __global__ __launch_bounds__(" << BLOCK << ") void dfmi_query(const dfmi::Args A) {\n";
+    o << "  constexpr int BLOCK = " << BLOCK << ", K = " << K << ", WAVES = BLOCK / 64;\n";
+    o << "  const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);\n";
+    if (P.pred) {
+        const int nch = 1 + (int)X.utf8_outs.size();
+        o << "  constexpr int NCH = " << nch << ";\n";
+        o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n  __shared__ unsigned s_tile;\n";
+        o << "  const unsigned tile = dfmi::tile_index<BLOCK>(A, &s_tile);\n";
+        o << "  const i64 base = (i64)tile * (BLOCK * K);\n";
+        o << "  const i64 rem = A.n_rows - base;\n";
+        // 1. predicate columns
+        emit_loads(o, X.pred_slots, X, "(i64)(k * BLOCK + tid) < rem", true);
+        // 2. predicate per row
+        o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
+        o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
+        const Val r = g.emit(P.pred, P.pred->root, 0, "in");
+        if (P.pred->type == DFMI_TYPE_BOOLEAN && !r.v.empty())
+            o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
+        o << "  }\n";
+        // 3. projection-only columns, loaded only where selected
+        emit_loads(o, X.proj_slots, X, "(selm >> k) & 1", false);
+        // 4. compaction offsets (rows + Utf8 bytes)
+        o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+          << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
+        for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+            const int u = X.utf8_outs[j].second;
+            o << "  unsigned len" << j << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+              << "    const i64 row = base + k * BLOCK + tid;\n"
+              << "    len" << j << "[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[" << u << "][row + 1] - A.offs[" << u
+              << "][row]) : 0u;\n    cnt[" << (j + 1) << "][k] = len" << j << "[k];\n  }\n";
+        }
+        o << "  dfmi::tile_offsets<BLOCK, K, NCH>(A, T, tile, cnt, lane, wave);\n";
+        o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
+          << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
+        // 5. projections over the selected rows (filtered batch: no validity)
+        g.filtered_cols = true;
+        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
+          << "    const i64 row = base + k * BLOCK + tid;\n    const unsigned d = dst[k];\n";
+        for (size_t oi = 0; oi < P.outs.size(); ++oi) {
+            const OutSpec& os = P.outs[oi];
+            if (os.kind == OutSpec::SKIP || os.kind == OutSpec::UTF8) continue;
+            Val v;
+            if (os.kind == OutSpec::GATHER) {
+                IrNode c;
+                c.kind = IR_COL;
+                c.col = os.col;
+                c.type = X.col_type(os.col);
+                v = g.col(c);
+            } else {
+                v = g.emit(os.prog, os.prog->root, os.ord_base, "true");
+            }
+            if (os.out_type == DFMI_TYPE_BOOLEAN)
+                o << "    ((u8*)A.out[" << oi << "] + obase)[d] = (" << v.v << ") ? 1 : 0;\n";
+            else
+                o << "    ((u64*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
+        }
+        o << "  }\n";
+        for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+            o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << X.utf8_outs[j].second << ", "
+              << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";
+        }
+        if (!X.utf8_outs.empty()) {
+            o << "  if (tid == 0 && tile == (unsigned)A.n_tiles - 1) {\n";
+            for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                o << "    A.out_offs[" << X.utf8_outs[j].first << "][T.prefix[0] + T.agg[0]] = (int)(T.prefix["
+                  << (j + 1) << "] + T.agg[" << (j + 1) << "]);\n";
+            o << "  }\n";
+        }
+    } else {
+        // projection only: dense rows, ballot-packed validity / Boolean bitmaps
+        o << "  const i64 base = (i64)blockIdx.x * (BLOCK * K);\n";
+        o << "  const i64 rem = A.n_rows - base;\n";
+        std::vector<int> all = X.pred_slots;
+        all.insert(all.end(), X.proj_slots.begin(), X.proj_slots.end());
+        emit_loads(o, all, X, "(i64)(k * BLOCK + tid) < rem", true);
+        o << "  unsigned nulls[" << std::max<size_t>(1, P.outs.size()) << "] = {0};\n";
+        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+          << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n"
+          << "    const i64 w = (base >> 6) + k * WAVES + wave;\n";
+        for (size_t oi = 0; oi < P.outs.size(); ++oi) {
+            const OutSpec& os = P.outs[oi];
+            if (os.kind != OutSpec::EXPR) continue;
+            const Val v = g.emit(os.prog, os.prog->root, os.ord_base, "in");
+            if (os.out_type == DFMI_TYPE_BOOLEAN) {
+                o << "    { const u64 vb_ = __ballot(in && (" << v.v << ")); const u64 nb_ = __ballot(in && ("
+                  << v.n << "));\n"
+                  << "      nulls[" << oi << "] += __builtin_popcountll(__ballot(in && !(" << v.n << ")));\n"
+                  << "      if (lane == 0 && w * 64 < A.n_rows) { ((u64*)A.out[" << oi << "])[w] = vb_;"
+                  << " if (A.out_valid[" << oi << "]) ((u64*)A.out_valid[" << oi << "])[w] = nb_; } }\n";
+            } else {
+                o << "    if (in) ((u64*)A.out[" << oi << "])[row] = " << v.v << ";\n";
+                o << "    { const u64 nb_ = __ballot(in && (" << v.n << "));\n"
+                  << "      nulls[" << oi << "] += __builtin_popcountll(__ballot(in && !(" << v.n << ")));\n"
+                  << "      if (lane == 0 && w * 64 < A.n_rows && A.out_valid[" << oi << "]) ((u64*)A.out_valid[" << oi
+                  << "])[w] = nb_; }\n";
+            }
+        }
+        o << "  }\n";
+        for (size_t oi = 0; oi < P.outs.size(); ++oi)
+            if (P.outs[oi].kind == OutSpec::EXPR)
+                o << "  if (lane == 0 && nulls[" << oi << "]) atomicAdd(&A.totals[8 + " << oi << "], (u64)nulls[" << oi
+                  << "]);\n";
+    }
+    o << "}\n";
+    return std::string(dfmi_skeleton_src) + o.str();
+}
+
+hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_ms) {
+    const std::string src = generate(P, X);
+    if (getenv("DFMI_JIT_PRINT")) fprintf(stderr, "%s\n", src.c_str() + strlen(dfmi_skeleton_src));
+    return compile(device, src, compile_ms);
+}
+
+}  // namespace jit
+}  // namespace dfmi

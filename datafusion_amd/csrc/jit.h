@@ -1,0 +1,75 @@
+// Query compiler interface (host side of jit.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/dfmi.h"
+#include "dfmi_program.h"
+
+namespace dfmi {
+
+struct Fail {
+    int32_t code;
+    std::string msg;
+};
+
+namespace jit {
+
+// One output column of the pass.
+struct OutSpec {
+    enum Kind { SKIP, GATHER, EXPR, UTF8 } kind = SKIP;
+    int col = -1;                      // GATHER / UTF8: input column
+    const dfmi_program* prog = nullptr;  // EXPR
+    int ord_base = 0;                  // evaluation-order base of prog's nodes
+    int out_type = 0;
+};
+
+struct Plan {
+    const dfmi_program* pred = nullptr;  // nullptr: projection only (dense kernel)
+    std::vector<OutSpec> outs;
+};
+
+// Slot tables + literal pools of one launch.
+struct Launch {
+    int K = 8, BLOCK = 512;
+    const dfmi_batch* in = nullptr;
+    std::vector<int> num_cols;   // arg slot -> input column (numeric and Boolean)
+    std::vector<int> pred_slots; // slots the predicate reads (loaded for every row)
+    std::vector<int> proj_slots; // slots only projections read (loaded where selected)
+    std::vector<int> utf8_cols;  // utf8 slot -> input column
+    std::vector<std::pair<int, int>> utf8_outs;  // (output index, utf8 slot)
+    uint64_t args_lits[32] = {};
+    int n_lits = 0;
+    int str_off[8] = {}, str_len[8] = {};
+    char str[256] = {};
+    int n_str = 0, str_bytes = 0;
+
+    int col_type(int col) const { return in->columns[col].type; }
+    bool col_nullable(int col) const {
+        return in->columns[col].validity != nullptr && in->columns[col].null_count > 0;
+    }
+    int slot_of_col(int col) const {
+        for (size_t i = 0; i < num_cols.size(); ++i)
+            if (num_cols[i] == col) return (int)i;
+        throw Fail{DFMI_ERR_INVALID_ARGUMENT, "query compiler: column not registered"};
+    }
+    int slot_of_utf8(int col) const {
+        for (size_t i = 0; i < utf8_cols.size(); ++i)
+            if (utf8_cols[i] == col) return (int)i;
+        throw Fail{DFMI_ERR_INVALID_ARGUMENT, "query compiler: Utf8 column not registered"};
+    }
+};
+
+// Generated source of the plan's kernel (skeleton + body); fills the literal pools.
+std::string generate(const Plan& P, Launch& X);
+// Compiled kernel for the plan (cached per source text and device).
+hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_ms);
+size_t cache_size();
+// hipRTC compile of a generated source to a gfx950 code object (no device needed).
+std::vector<char> compile_code(const std::string& src, double* compile_ms);
+
+}  // namespace jit
+}  // namespace dfmi

@@ -1,0 +1,291 @@
+// Device skeleton of the query-compiled Selection + Projection kernels.
+//
+// Hand-written CDNA4 code shared by every compiled query: kernel arguments,
+// wave64 helpers, the single-pass decoupled look-back, validity / Boolean
+// bitmap access, Utf8 helpers and the per-tile compaction step. The query
+// compiler (jit.cpp) appends one kernel whose body is the query's predicate
+// and projections written out as straight-line code over this skeleton, so
+// nothing is interpreted at run time (see DESIGN.md "Kernels").
+//
+// The text of this file is embedded into libdfmi.so and compiled with hipRTC
+// (-O3 -ffp-contract=off, gfx950) together with the generated body; the build
+// also compiles it with hipcc against a sample body to catch errors early.
+#ifndef DFMI_SKELETON
+#define DFMI_SKELETON
+
+typedef unsigned long long u64;
+typedef long long i64;
+typedef unsigned char u8;
+
+namespace dfmi {
+
+constexpr int kArgCols = 16;   // numeric / Boolean input columns
+constexpr int kArgUtf8 = 16;   // Utf8 input columns
+constexpr int kArgOut = 16;    // output columns
+constexpr int kArgLits = 32;   // 64-bit literals
+constexpr int kArgStr = 256;   // string literal bytes
+
+struct Args {
+    i64 n_rows;
+    int n_tiles;
+    int mode;                          // bit0: ticket order (fallback), bit1: no look-back (diag)
+    const void* col[kArgCols];         // numeric values / Boolean bits
+    const u8* valid[kArgCols];         // validity bitmaps (nullptr = all valid)
+    const int* offs[kArgUtf8];         // Utf8 offsets
+    const u8* bytes[kArgUtf8];         // Utf8 bytes
+    const u8* svalid[kArgUtf8];        // Utf8 validity
+    void* out[kArgOut];                // numeric values / Boolean bytes (filtered) / bits (dense)
+    u8* out_valid[kArgOut];            // dense kernels: validity bitmaps
+    int* out_offs[kArgOut];            // Utf8 outputs
+    u8* out_data[kArgOut];
+    i64 out_cap[kArgOut];
+    u64 lits[kArgLits];
+    int str_off[8];
+    int str_len[8];
+    char str[kArgStr];
+    u64* status;                       // [n_chan][n_tiles] look-back words
+    unsigned* ticket;
+    u64* err;                          // max(~key) error word
+    u64* totals;                       // [0..8) channel totals, [8..24) null counts
+};
+
+enum ErrKind : unsigned { ERRK_DIV_ZERO = 1, ERRK_DIV_OVERFLOW = 2, ERRK_LOOKBACK_TIMEOUT = 3, ERRK_CAPACITY = 4 };
+
+constexpr u64 FLAG_A = 1ull << 62;
+constexpr u64 FLAG_P = 2ull << 62;
+constexpr u64 VAL_MASK = (1ull << 62) - 1;
+
+__device__ __forceinline__ double f64(u64 x) { return __builtin_bit_cast(double, x); }
+__device__ __forceinline__ u64 bits(double x) { return __builtin_bit_cast(u64, x); }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ unsigned lane_rank(u64 mask) {  // set bits below this lane
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ u64 wave_incl_scan(u64 v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u64 t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ unsigned wave_incl_scan32(unsigned v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// 64 bits of an LSB-first bitmap starting at row 64*w (w wave-uniform); the
+// tail word is assembled bytewise so nothing past the bitmap is read.
+__device__ __forceinline__ u64 bitmap_word(const u8* bm, i64 w, i64 n_rows) {
+    const i64 nbytes = (n_rows + 7) >> 3;
+    const i64 b0 = w * 8;
+    if (b0 + 8 <= nbytes) return *(const u64*)(bm + b0);
+    u64 v = 0;
+    for (i64 i = b0; i < nbytes; ++i) v |= (u64)bm[i] << (8 * (i - b0));
+    return v;
+}
+
+__device__ __forceinline__ void report_err(u64* err, unsigned ordinal, i64 row, unsigned kind) {
+    const u64 key = ((u64)ordinal << 44) | ((u64)row << 4) | kind;
+    atomicMax(err, ~key);
+}
+
+// arrow 0.12 bool_op on Option<T>: eq/neq compare the Options; lt/le:
+// (None,_) => true, (_,None) => false; gt/ge: (None,_) => false,
+// (_,None) => true. The result is never null.
+template <int OP>
+__device__ __forceinline__ bool cmp_opt(bool lv, bool rv, bool res) {
+    if (lv && rv) return res;
+    if constexpr (OP == 0) return !lv && !rv;
+    else if constexpr (OP == 1) return lv || rv;
+    else if constexpr (OP == 2 || OP == 3) return !lv;
+    else return lv;
+}
+
+// Rust `/` on i64 after arrow's zero check: wraps nothing, MIN / -1 panics
+// (reported by the caller), zero divisors never reach here when valid.
+__device__ __noinline__ u64 sdiv64(u64 x, u64 y) {
+    const i64 sx = (i64)x, sy = (i64)y;
+    if (sy == 0) return 0;
+    if (sy == -1) return 0ull - x;
+    return (u64)(sx / sy);
+}
+
+__device__ __forceinline__ bool utf8_eq_lit(const Args& A, int u, i64 row, int lit) {
+    const int s = A.offs[u][row], e = A.offs[u][row + 1];
+    const int len = A.str_len[lit];
+    if (e - s != len) return false;
+    const u8* p = A.bytes[u] + s;
+    const char* q = A.str + A.str_off[lit];
+    for (int i = 0; i < len; ++i)
+        if (p[i] != (u8)q[i]) return false;
+    return true;
+}
+
+__device__ __forceinline__ bool utf8_eq_col(const Args& A, int u, int v, i64 row) {
+    const int s0 = A.offs[u][row], e0 = A.offs[u][row + 1];
+    const int s1 = A.offs[v][row], e1 = A.offs[v][row + 1];
+    if (e0 - s0 != e1 - s1) return false;
+    for (int i = 0; i < e0 - s0; ++i)
+        if (A.bytes[u][s0 + i] != A.bytes[v][s1 + i]) return false;
+    return true;
+}
+
+__device__ __forceinline__ bool utf8_valid(const Args& A, int u, i64 row) {
+    const u8* v = A.svalid[u];
+    return !v || ((v[row >> 3] >> (row & 7)) & 1);
+}
+
+__device__ __forceinline__ void st_status(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 ld_status(u64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Single-pass decoupled look-back (one wave): publish the tile aggregate, read
+// the nearest 64 predecessors' status words (one per lane) per round, summing
+// aggregates until an inclusive prefix is found, publish our own inclusive
+// prefix and return the exclusive one. 64 words per round measured best: a
+// wider window costs more in polling traffic than it saves in rounds.
+// The spin is bounded in wall time: a tile order that could never resolve
+// (blockIdx order with out-of-order dispatch) reports a timeout instead of
+// hanging, and the host re-runs the query in ticket order.
+__device__ u64 lookback(u64* st, unsigned tile, u64 agg, int lane, u64* err) {
+    if (tile == 0) {
+        if (lane == 0) st_status(st, FLAG_P | agg);
+        return 0;
+    }
+    if (lane == 0) st_status(st + tile, FLAG_A | agg);
+    u64 excl = 0;
+    i64 j = (i64)tile - 1;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    while (true) {
+        const i64 idx = j - lane;
+        const u64 w = idx >= 0 ? ld_status(st + idx) : FLAG_P;
+        const unsigned flag = (unsigned)(w >> 62);
+        const u64 xm = __ballot(flag == 0);
+        const u64 pm = __ballot(flag == 2);
+        if (pm) {
+            const int first = __builtin_ctzll(pm);
+            const u64 need = first == 63 ? ~0ull : ((2ull << first) - 1);
+            if (!(xm & need)) {
+                excl += wave_sum(lane <= first ? (w & VAL_MASK) : 0);
+                break;
+            }
+        } else if (!xm) {
+            excl += wave_sum(w & VAL_MASK);
+            j -= 64;
+            continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+            if (lane == 0) report_err(err, 0, 0, ERRK_LOOKBACK_TIMEOUT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) st_status(st + tile, FLAG_P | (excl + agg));
+    return excl;
+}
+
+// Tile placement: blockIdx order (dispatch is in order per XCD, so every
+// predecessor is running or done), or a dynamic ticket (A.mode bit 0) as the
+// fallback that needs no dispatch-order assumption.
+template <int BLOCK>
+__device__ __forceinline__ unsigned tile_index(const Args& A, unsigned* s_tile) {
+    if (!(A.mode & 1)) return blockIdx.x;
+    if (threadIdx.x == 0) *s_tile = atomicAdd(A.ticket, 1u);
+    __syncthreads();
+    return (unsigned)uni((int)*s_tile);
+}
+
+// Per-tile compaction: the selection words of every (k, wave) are counted,
+// scanned in row order, and the tile's output offsets found by look-back.
+// NCH channels: 0 = rows, 1.. = Utf8 output bytes (lens given per row).
+template <int BLOCK, int K, int NCH>
+struct Tile {
+    static constexpr int WAVES = BLOCK / 64;
+    static constexpr int NW = K * WAVES;  // 64-row words per tile
+    static_assert(NW <= 64, "one wave scans the tile's words");
+    u64 cnt[NCH][NW];
+    u64 excl[NCH][NW];
+    u64 prefix[NCH];
+    u64 agg[NCH];
+    unsigned tile;
+};
+
+// counts[ch][k] : per-lane value for row k (rows: 0/1 selection, Utf8: bytes)
+template <int BLOCK, int K, int NCH>
+__device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
+                                             const unsigned (&cnt)[NCH][K], int lane, int wave) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int NW = K * WAVES;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const u64 s = wave_sum((u64)cnt[ch][k]);
+            if (lane == 0) T.cnt[ch][k * WAVES + wave] = s;
+        }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const u64 c = lane < NW ? T.cnt[ch][lane] : 0ull;
+            const u64 incl = wave_incl_scan(c, lane);
+            if (lane < NW) T.excl[ch][lane] = incl - c;
+            const u64 agg = __shfl(incl, NW - 1, 64);
+            const u64 pre = (A.mode & 2) ? (ch == 0 ? (u64)tile * BLOCK * K : 0ull)
+                                         : lookback(A.status + (i64)ch * A.n_tiles, tile, agg, lane, A.err);
+            if (lane == 0) {
+                T.prefix[ch] = pre;
+                T.agg[ch] = agg;
+                if (tile == (unsigned)A.n_tiles - 1) A.totals[ch] = pre + agg;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// Copy the selected rows of Utf8 input u into output o (rebased i32
+// offsets + bytes, filter.rs:94-105).
+template <int BLOCK, int K, int NCH>
+__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+                                            i64 base, unsigned selm, const unsigned (&len)[K],
+                                            const unsigned (&dst)[K], int lane, int wave) {
+    constexpr int WAVES = BLOCK / 64;
+    const u64 bpre = T.prefix[ch];
+    const i64 obase = (i64)T.prefix[0];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const unsigned incl = wave_incl_scan32(len[k], lane);
+        if (!((selm >> k) & 1)) continue;
+        const i64 row = base + (i64)k * BLOCK + threadIdx.x;
+        const u64 ob = bpre + T.excl[ch][k * WAVES + wave] + (incl - len[k]);
+        A.out_offs[o][obase + dst[k]] = (int)ob;
+        if ((i64)(ob + len[k]) > A.out_cap[o]) {
+            report_err(A.err, 0, 0, ERRK_CAPACITY);
+            continue;
+        }
+        const u8* src = A.bytes[u] + A.offs[u][row];
+        u8* dd = A.out_data[o] + ob;
+        for (unsigned i = 0; i < len[k]; ++i) dd[i] = src[i];
+    }
+}
+
+}  // namespace dfmi
+
+#endif  // DFMI_SKELETON

@@ -1,0 +1,44 @@
+// Build-time check of jit_skeleton.hip: instantiates every skeleton template
+// with a representative generated body (one Float64 predicate, a gathered
+// column, a Utf8 gather), so a broken skeleton fails `make` rather than the
+// first query compile on the GPU. Not linked into libdfmi.so.
+#include <hip/hip_runtime.h>
+
+#include "jit_skeleton.hip"
+
+extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi::Args A) {
+    constexpr int BLOCK = 512, K = 8, WAVES = BLOCK / 64, NCH = 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);
+    __shared__ dfmi::Tile<BLOCK, K, NCH> T;
+    __shared__ unsigned s_tile;
+    const unsigned tile = dfmi::tile_index<BLOCK>(A, &s_tile);
+    const i64 base = (i64)tile * (BLOCK * K);
+    const i64 rem = A.n_rows - base;
+    u64 c0[K];
+    for (int k = 0; k < K; ++k) c0[k] = (k * BLOCK + tid < rem) ? ((const u64*)A.col[0] + base)[k * BLOCK + tid] : 0ull;
+    unsigned selm = 0;
+    for (int k = 0; k < K; ++k) {
+        const i64 row = base + k * BLOCK + tid;
+        selm |= (unsigned)(row < A.n_rows && dfmi::f64(c0[k]) > dfmi::f64(A.lits[0])) << k;
+    }
+    unsigned cnt[NCH][K], len0[K];
+    u64 wm[K];
+    for (int k = 0; k < K; ++k) {
+        const i64 row = base + k * BLOCK + tid;
+        wm[k] = __ballot((selm >> k) & 1);
+        cnt[0][k] = (selm >> k) & 1;
+        len0[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[0][row + 1] - A.offs[0][row]) : 0u;
+        cnt[1][k] = len0[k];
+    }
+    dfmi::tile_offsets<BLOCK, K, NCH>(A, T, tile, cnt, lane, wave);
+    const i64 obase = (i64)T.prefix[0];
+    unsigned dst[K];
+    for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);
+    for (int k = 0; k < K; ++k)
+        if ((selm >> k) & 1) ((u64*)A.out[0] + obase)[dst[k]] = c0[k];
+    dfmi::utf8_gather<BLOCK, K, NCH>(A, T, 1, 0, 1, base, selm, len0, dst, lane, wave);
+    const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0) &&
+                   dfmi::utf8_eq_col(A, 0, 1, base) && dfmi::utf8_valid(A, 0, base);
+    if (b) dfmi::report_err(A.err, 1, base, dfmi::ERRK_DIV_ZERO);
+    if (tid == 0 && dfmi::bitmap_word(A.valid[0], 0, A.n_rows) == 7) A.totals[0] = dfmi::sdiv64(A.lits[1], A.lits[2]);
+}
