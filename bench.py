@@ -76,6 +76,22 @@ class FusedStep:
         return self.outs[0].length
 
 
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r01")
+
+
+def pmc_traffic(n, sel):
+    """HBM bytes per launch of the query kernel measured by the rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes of tools/profile_round.sh on this
+    configuration (corrected by tools/traffic.py); None if not profiled."""
+    try:
+        t = json.load(open(os.path.join(PROFILE_DIR, "traffic.json")))
+    except (OSError, ValueError):
+        return None
+    if t.get("rows") != n or abs(t.get("selectivity", -1) - sel) > 1e-9:
+        return None
+    return t["traffic_bytes"]
+
+
 def cpu_baseline(sel, budget_s=12.0):
     """The oracle (reference-faithful restatement, 1 core) on a host sample,
     batch size 1024 as in csv_sql.rs:49. Sample size is calibrated so the
@@ -92,7 +108,7 @@ def cpu_baseline(sel, budget_s=12.0):
         return time.perf_counter() - t0, rows
 
     t, _ = run(1 << 20)
-    n = int(min(2e8, max(1 << 20, (1 << 20) * budget_s / max(t, 1e-6))))
+    n = int(min(4e8, max(1 << 20, (1 << 20) * budget_s / max(t, 1e-6))))
     n = (n + 1023) // 1024 * 1024
     t, rows = run(n)
     return {"value": n / t, "unit": "rows/s", "cores": 1, "kind": "port",
@@ -169,6 +185,7 @@ def main():
 
     h = results[args.sel]
     total_rows = n * world * args.steps
+    traffic = pmc_traffic(n, args.sel)
     out = {
         "metric": "filter+project rows/s (1e9-row Float64 table per GPU, SELECT a, b, a*b+c WHERE a > k AND b < m)",
         "value": total_rows / h["el"],
@@ -185,7 +202,10 @@ def main():
         "config": {"workload": "C2: 1e9-row Float64 a,b,c per GPU; s=%.2f" % args.sel, "rows_per_gpu": n,
                    "selectivity": round(h["s"], 4), "parallelism": "row-range shards, RCCL count all_gather"},
         "roofline": {"bound": "hbm", "achieved": round(h["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(h["achieved"] / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(h["achieved"] / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE passes, profiles/r01/traffic.json"
+                     if traffic else None,
                      "kernel": "dfmi_query (query-compiled filter+project)", "kernel_ms": round(h["kms"], 4),
                      "algorithmic_bytes_per_row": round(h["bpr"], 3)},
         "sweep": {("%.2f" % s): {"rows_per_s": n * world * args.steps / r["el"], "kernel_ms": round(r["kms"], 4),

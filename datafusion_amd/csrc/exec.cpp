@@ -239,6 +239,13 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
     X.BLOCK = 512;
     X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
     if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
+    if (const char* bb = getenv("DFMI_BLOCK")) X.BLOCK = atoi(bb);        // diagnostics only
+    // look-back / tile-order variants (diagnostics only)
+    if (const char* e = getenv("DFMI_LOOKBACK_R")) X.R = std::max(1, std::min(16, atoi(e)));
+    if (const char* e = getenv("DFMI_LOOKBACK_SLEEP")) X.sleep = std::max(0, std::min(127, atoi(e)));
+    if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
+    if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 64)
+        throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
     const int64_t n_tiles = (n + tile_rows - 1) / tile_rows;
     if (n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
@@ -335,7 +342,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 throw;
             }
             const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
-            const size_t status_bytes = (size_t)n_chan * n_tiles * 8;
+            const size_t status_bytes = (size_t)n_chan * n_tiles * 8 * X.spread;
             std::vector<int> bool_out;
             for (int o = 0; o < nout; ++o)
                 if (pred && plan.outs[o].kind != jit::OutSpec::SKIP && plan.outs[o].kind != jit::OutSpec::UTF8 &&
@@ -383,35 +390,24 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             A.status = (unsigned long long*)(ctx->ws + kHdrAlloc);
             A.mode = 0;
             if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
-            for (int attempt = 0; attempt < 2; ++attempt) {
-                HIP_TRY(hipMemsetAsync(ctx->ws, 0, kHdrAlloc + status_bytes, st));
-                HIP_TRY(hipEventRecord(ctx->ev0, st));
-                size_t asz = sizeof A;
-                void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz,
-                               HIP_LAUNCH_PARAM_END};
-                HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)n_tiles, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
-                HIP_TRY(hipEventRecord(ctx->ev1, st));
-                for (int o = 0; o < nout; ++o)
-                    if (bool_dst[o])
-                        HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
-                HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ctx->ws, kHdrAlloc, hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipEventRecord(ctx->ev2, st));
-                HIP_TRY(hipStreamSynchronize(st));
-                uint64_t ew;
-                memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
-                dev_key = ~0ull;
-                dev_kind = 0;
-                if (ew) {
-                    dev_key = ~ew;
-                    dev_kind = (int)(dev_key & 15);
-                    dev_key &= ~15ull;
-                }
-                // blockIdx tile order could not resolve: re-run in ticket order
-                if (dev_kind == ERRK_LOOKBACK_TIMEOUT && !(A.mode & 1)) {
-                    A.mode |= 1;
-                    continue;
-                }
-                break;
+            const unsigned grid = (unsigned)n_tiles;  // one block per tile
+            HIP_TRY(hipMemsetAsync(ctx->ws, 0, kHdrAlloc + status_bytes, st));
+            HIP_TRY(hipEventRecord(ctx->ev0, st));
+            size_t asz = sizeof A;
+            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+            HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
+            HIP_TRY(hipEventRecord(ctx->ev1, st));
+            for (int o = 0; o < nout; ++o)
+                if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
+            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ctx->ws, kHdrAlloc, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipEventRecord(ctx->ev2, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            uint64_t ew;
+            memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
+            if (ew) {
+                dev_key = ~ew;
+                dev_kind = (int)(dev_key & 15);
+                dev_key &= ~15ull;
             }
             float m1 = 0, m2 = 0;
             (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);

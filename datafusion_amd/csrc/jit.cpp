@@ -88,15 +88,14 @@ struct Gen {
     // column value for the current row k (inside a per-k loop)
     Val col(const IrNode& n) {
         const int s = X.slot_of_col(n.col);
+        const std::string id = std::to_string(s);
         Val r;
         if (n.type == DFMI_TYPE_BOOLEAN) {
-            r.v = "(((bw" + std::to_string(s) + "[k] >> lane) & 1) != 0)";
+            r.v = "(((bw" + id + "[k] >> lane) & 1) != 0)";
         } else {
-            r.v = "c" + std::to_string(s) + "[k]";
+            r.v = "c" + id + "[k]";
         }
-        r.n = (!filtered_cols && X.col_nullable(n.col))
-                  ? "(((vw" + std::to_string(s) + "[k] >> lane) & 1) != 0)"
-                  : "true";
+        r.n = (!filtered_cols && X.col_nullable(n.col)) ? "(((vw" + id + "[k] >> lane) & 1) != 0)" : "true";
         return r;
     }
 
@@ -263,24 +262,46 @@ size_t cache_size() {
 }
 
 // --------------------------------------------------------------- kernels
-static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Launch& X, const char* guard,
+// Register arrays of the given slots (suffix names a ping-pong set).
+static void emit_decls(std::ostream& o, const std::vector<int>& slots, const Launch& X, const std::string& sfx,
                        bool valid_words) {
     for (int s : slots) {
         const int col = X.num_cols[s];
-        if (X.col_type(col) == DFMI_TYPE_BOOLEAN) {
-            o << "  u64 bw" << s << "[K];\n";
-            o << "#pragma unroll\n  for (int k = 0; k < K; ++k) bw" << s << "[k] = dfmi::bitmap_word((const u8*)A.col["
-              << s << "], (base >> 6) + k * WAVES + wave, A.n_rows);\n";
-        } else {
-            o << "  u64 c" << s << "[K];\n  { const u64* p_ = (const u64*)A.col[" << s << "] + base;\n"
-              << "#pragma unroll\n    for (int k = 0; k < K; ++k) c" << s << "[k] = (" << guard
-              << ") ? p_[k * BLOCK + tid] : 0ull; }\n";
-        }
-        if (valid_words && X.col_nullable(col)) {
-            o << "  u64 vw" << s << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) vw" << s
-              << "[k] = dfmi::bitmap_word(A.valid[" << s << "], (base >> 6) + k * WAVES + wave, A.n_rows);\n";
+        o << "  u64 " << (X.col_type(col) == DFMI_TYPE_BOOLEAN ? "bw" : "c") << s << sfx << "[K];\n";
+        if (valid_words && X.col_nullable(col)) o << "  u64 vw" << s << sfx << "[K];\n";
+    }
+}
+
+// Loads of the K rows per thread of the tile at `base` (wave-uniform): a
+// branch-free form for full tiles and a guarded one for the last tile. Value
+// loads of projection-only slots are lane-masked by `guard` (selected rows).
+static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Launch& X, const std::string& sfx,
+                       const std::string& base, const char* guard, bool valid_words) {
+    if (slots.empty()) return;
+    for (int full = 1; full >= 0; --full) {
+        o << (full ? "  if (A.n_rows - " + base + " >= BLOCK * K) {\n" : "  } else {\n");
+        for (int s : slots) {
+            const int col = X.num_cols[s];
+            const std::string id = std::to_string(s) + sfx;
+            if (X.col_type(col) == DFMI_TYPE_BOOLEAN) {
+                o << "#pragma unroll\n    for (int k = 0; k < K; ++k) bw" << id
+                  << "[k] = dfmi::bitmap_word((const u8*)A.col[" << s << "], (" << base
+                  << " >> 6) + k * WAVES + wave, A.n_rows);\n";
+            } else {
+                std::string g = guard ? std::string(guard) : "";
+                if (!full) g = g.empty() ? "(" + base + " + k * BLOCK + tid < A.n_rows)"
+                                         : "(" + base + " + k * BLOCK + tid < A.n_rows) && " + g;
+                o << "    { const u64* p_ = (const u64*)A.col[" << s << "] + " << base << " + tid;\n"
+                  << "#pragma unroll\n      for (int k = 0; k < K; ++k) c" << id << "[k] = "
+                  << (g.empty() ? "p_[k * BLOCK];" : "(" + g + ") ? p_[k * BLOCK] : 0ull;") << " }\n";
+            }
+            if (valid_words && X.col_nullable(col)) {
+                o << "#pragma unroll\n    for (int k = 0; k < K; ++k) vw" << id << "[k] = dfmi::bitmap_word(A.valid[" << s
+                  << "], (" << base << " >> 6) + k * WAVES + wave, A.n_rows);\n";
+            }
         }
     }
+    o << "  }\n";
 }
 
 std::string generate(const Plan& P, Launch& X) {
@@ -294,75 +315,81 @@ std::string generate(const Plan& P, Launch& X) {
     if (P.pred) {
         const int nch = 1 + (int)X.utf8_outs.size();
         o << "  constexpr int NCH = " << nch << ";\n";
-        o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n  __shared__ unsigned s_tile;\n";
-        o << "  const unsigned tile = dfmi::tile_index<BLOCK>(A, &s_tile);\n";
-        o << "  const i64 base = (i64)tile * (BLOCK * K);\n";
-        o << "  const i64 rem = A.n_rows - base;\n";
-        // 1. predicate columns
-        emit_loads(o, X.pred_slots, X, "(i64)(k * BLOCK + tid) < rem", true);
-        // 2. predicate per row
-        o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
-        o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
-        const Val r = g.emit(P.pred, P.pred->root, 0, "in");
-        if (P.pred->type == DFMI_TYPE_BOOLEAN && !r.v.empty())
-            o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
-        o << "  }\n";
-        // 3. projection-only columns, loaded only where selected
-        emit_loads(o, X.proj_slots, X, "(selm >> k) & 1", false);
-        // 4. compaction offsets (rows + Utf8 bytes)
-        o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
-          << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
-        for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
-            const int u = X.utf8_outs[j].second;
-            o << "  unsigned len" << j << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
-              << "    const i64 row = base + k * BLOCK + tid;\n"
-              << "    len" << j << "[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[" << u << "][row + 1] - A.offs[" << u
-              << "][row]) : 0u;\n    cnt[" << (j + 1) << "][k] = len" << j << "[k];\n  }\n";
-        }
-        o << "  dfmi::tile_offsets<BLOCK, K, NCH>(A, T, tile, cnt, lane, wave);\n";
-        o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
-          << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
-        // 5. projections over the selected rows (filtered batch: no validity)
-        g.filtered_cols = true;
-        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
-          << "    const i64 row = base + k * BLOCK + tid;\n    const unsigned d = dst[k];\n";
-        for (size_t oi = 0; oi < P.outs.size(); ++oi) {
-            const OutSpec& os = P.outs[oi];
-            if (os.kind == OutSpec::SKIP || os.kind == OutSpec::UTF8) continue;
-            Val v;
-            if (os.kind == OutSpec::GATHER) {
-                IrNode c;
-                c.kind = IR_COL;
-                c.col = os.col;
-                c.type = X.col_type(os.col);
-                v = g.col(c);
-            } else {
-                v = g.emit(os.prog, os.prog->root, os.ord_base, "true");
-            }
-            if (os.out_type == DFMI_TYPE_BOOLEAN)
-                o << "    ((u8*)A.out[" << oi << "] + obase)[d] = (" << v.v << ") ? 1 : 0;\n";
-            else
-                o << "    ((u64*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
-        }
-        o << "  }\n";
-        for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
-            o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << X.utf8_outs[j].second << ", "
-              << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";
-        }
-        if (!X.utf8_outs.empty()) {
-            o << "  if (tid == 0 && tile == (unsigned)A.n_tiles - 1) {\n";
-            for (size_t j = 0; j < X.utf8_outs.size(); ++j)
-                o << "    A.out_offs[" << X.utf8_outs[j].first << "][T.prefix[0] + T.agg[0]] = (int)(T.prefix["
-                  << (j + 1) << "] + T.agg[" << (j + 1) << "]);\n";
+        o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
+        // one tile per block in dispatch order (in order per XCD, so every
+        // tile a block waits on in the look-back is running or done)
+        o << "  const unsigned t = blockIdx.x;\n";
+        emit_decls(o, X.pred_slots, X, "", true);
+        emit_decls(o, X.proj_slots, X, "", false);
+        emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
+        {
+            o << "  const i64 base = (i64)t * (BLOCK * K);\n";
+            // predicate per row
+            g.filtered_cols = false;
+            o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
+            o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
+            const Val r = g.emit(P.pred, P.pred->root, 0, "in");
+            if (P.pred->type == DFMI_TYPE_BOOLEAN && !r.v.empty())
+                o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
             o << "  }\n";
+            // projection-only columns, loaded only where selected
+            emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            // compaction offsets (rows + Utf8 bytes)
+            o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+              << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
+            for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+                const int u = X.utf8_outs[j].second;
+                o << "  unsigned len" << j << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+                  << "    const i64 row = base + k * BLOCK + tid;\n"
+                  << "    len" << j << "[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[" << u << "][row + 1] - A.offs["
+                  << u << "][row]) : 0u;\n    cnt[" << (j + 1) << "][k] = len" << j << "[k];\n  }\n";
+            }
+            o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << X.R << ", " << X.sleep << ", " << X.spread
+              << ">(A, T, t, cnt, lane, wave);\n";
+            o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
+              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
+            // projections over the selected rows (filtered batch: no validity)
+            g.filtered_cols = true;
+            o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
+              << "    const i64 row = base + k * BLOCK + tid;\n    const unsigned d = dst[k];\n";
+            for (size_t oi = 0; oi < P.outs.size(); ++oi) {
+                const OutSpec& os = P.outs[oi];
+                if (os.kind == OutSpec::SKIP || os.kind == OutSpec::UTF8) continue;
+                Val v;
+                if (os.kind == OutSpec::GATHER) {
+                    IrNode c;
+                    c.kind = IR_COL;
+                    c.col = os.col;
+                    c.type = X.col_type(os.col);
+                    v = g.col(c);
+                } else {
+                    v = g.emit(os.prog, os.prog->root, os.ord_base, "true");
+                }
+                if (os.out_type == DFMI_TYPE_BOOLEAN)
+                    o << "    ((u8*)A.out[" << oi << "] + obase)[d] = (" << v.v << ") ? 1 : 0;\n";
+                else
+                    o << "    ((u64*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
+            }
+            o << "  }\n";
+            for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+                o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << X.utf8_outs[j].second << ", "
+                  << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";
+            }
+            if (!X.utf8_outs.empty()) {
+                o << "  if (tid == 0 && t == (unsigned)A.n_tiles - 1) {\n";
+                for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                    o << "    A.out_offs[" << X.utf8_outs[j].first << "][T.prefix[0] + T.agg[0]] = (int)(T.prefix["
+                      << (j + 1) << "] + T.agg[" << (j + 1) << "]);\n";
+                o << "  }\n";
+            }
         }
     } else {
         // projection only: dense rows, ballot-packed validity / Boolean bitmaps
         o << "  const i64 base = (i64)blockIdx.x * (BLOCK * K);\n";
-        o << "  const i64 rem = A.n_rows - base;\n";
         std::vector<int> all = X.pred_slots;
         all.insert(all.end(), X.proj_slots.begin(), X.proj_slots.end());
-        emit_loads(o, all, X, "(i64)(k * BLOCK + tid) < rem", true);
+        emit_decls(o, all, X, "", true);
+        emit_loads(o, all, X, "", "base", nullptr, true);
         o << "  unsigned nulls[" << std::max<size_t>(1, P.outs.size()) << "] = {0};\n";
         o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
           << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n"

@@ -35,6 +35,10 @@ struct Plan {
 // Slot tables + literal pools of one launch.
 struct Launch {
     int K = 8, BLOCK = 512;
+    // look-back: R windows of 64 status words per round trip, s_sleep(sleep)
+    // between polls, one status word per `spread` words (16 = one per 128-byte
+    // line: polling blocks then do not contend on shared lines)
+    int R = 1, sleep = 32, spread = 16;
     const dfmi_batch* in = nullptr;
     std::vector<int> num_cols;   // arg slot -> input column (numeric and Boolean)
     std::vector<int> pred_slots; // slots the predicate reads (loaded for every row)

@@ -28,7 +28,7 @@ constexpr int kArgStr = 256;   // string literal bytes
 struct Args {
     i64 n_rows;
     int n_tiles;
-    int mode;                          // bit0: ticket order (fallback), bit1: no look-back (diag)
+    int mode;                          // bit1: no look-back (diagnostics: wrong offsets, same traffic)
     const void* col[kArgCols];         // numeric values / Boolean bits
     const u8* valid[kArgCols];         // validity bitmaps (nullptr = all valid)
     const int* offs[kArgUtf8];         // Utf8 offsets
@@ -44,7 +44,7 @@ struct Args {
     int str_len[8];
     char str[kArgStr];
     u64* status;                       // [n_chan][n_tiles] look-back words
-    unsigned* ticket;
+    unsigned* ticket;                  // spare counter (zeroed per launch)
     u64* err;                          // max(~key) error word
     u64* totals;                       // [0..8) channel totals, [8..24) null counts
 };
@@ -156,60 +156,78 @@ __device__ __forceinline__ u64 ld_status(u64* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Single-pass decoupled look-back (one wave): publish the tile aggregate, read
-// the nearest 64 predecessors' status words (one per lane) per round, summing
-// aggregates until an inclusive prefix is found, publish our own inclusive
-// prefix and return the exclusive one. 64 words per round measured best: a
-// wider window costs more in polling traffic than it saves in rounds.
-// The spin is bounded in wall time: a tile order that could never resolve
-// (blockIdx order with out-of-order dispatch) reports a timeout instead of
-// hanging, and the host re-runs the query in ticket order.
+// Single-pass decoupled look-back (one wave): publish the tile aggregate,
+// then read R windows of 64 predecessor status words (one word per lane per
+// window, all R loads in flight together) per round trip, summing aggregates
+// until an inclusive prefix is found; publish our own inclusive prefix and
+// return the exclusive one. Status words are SPREAD words apart: with one
+// word per 128-byte line the hundreds of polling waves do not serialise on a
+// few shared lines, and s_sleep(SLEEP) between polls keeps the polling
+// traffic off the data path (measured, DESIGN.md "Look-back").
+// The spin is bounded in wall time: a tile that could never resolve reports
+// a timeout instead of hanging the device.
+template <int R, int SLEEP, int SPREAD>
 __device__ u64 lookback(u64* st, unsigned tile, u64 agg, int lane, u64* err) {
     if (tile == 0) {
         if (lane == 0) st_status(st, FLAG_P | agg);
         return 0;
     }
-    if (lane == 0) st_status(st + tile, FLAG_A | agg);
+    if (lane == 0) st_status(st + (i64)tile * SPREAD, FLAG_A | agg);
     u64 excl = 0;
-    i64 j = (i64)tile - 1;
+    i64 j = (i64)tile - 1;  // highest predecessor not yet accounted for
     const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     while (true) {
-        const i64 idx = j - lane;
-        const u64 w = idx >= 0 ? ld_status(st + idx) : FLAG_P;
-        const unsigned flag = (unsigned)(w >> 62);
-        const u64 xm = __ballot(flag == 0);
-        const u64 pm = __ballot(flag == 2);
-        if (pm) {
-            const int first = __builtin_ctzll(pm);
-            const u64 need = first == 63 ? ~0ull : ((2ull << first) - 1);
-            if (!(xm & need)) {
-                excl += wave_sum(lane <= first ? (w & VAL_MASK) : 0);
+        u64 w[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const i64 idx = j - lane - 64 * r;
+            w[r] = idx >= 0 ? ld_status(st + idx * SPREAD) : FLAG_P;
+        }
+        bool done = false, stall = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const unsigned flag = (unsigned)(w[r] >> 62);
+            const u64 xm = __ballot(flag == 0);
+            const u64 pm = __ballot(flag == 2);
+            if (pm) {
+                const int first = __builtin_ctzll(pm);
+                const u64 need = first == 63 ? ~0ull : ((2ull << first) - 1);
+                if (!(xm & need)) {
+                    excl += wave_sum(lane <= first ? (w[r] & VAL_MASK) : 0);
+                    done = true;
+                } else {
+                    stall = true;
+                }
                 break;
             }
-        } else if (!xm) {
-            excl += wave_sum(w & VAL_MASK);
+            if (xm) {
+                stall = true;
+                break;
+            }
+            excl += wave_sum(w[r] & VAL_MASK);
             j -= 64;
-            continue;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
-            if (lane == 0) report_err(err, 0, 0, ERRK_LOOKBACK_TIMEOUT);
-            break;
+        if (done) break;
+        if (stall) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+                if (lane == 0) report_err(err, 0, 0, ERRK_LOOKBACK_TIMEOUT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(SLEEP);
         }
-        __builtin_amdgcn_s_sleep(1);
     }
-    if (lane == 0) st_status(st + tile, FLAG_P | (excl + agg));
+    if (lane == 0) st_status(st + (i64)tile * SPREAD, FLAG_P | (excl + agg));
     return excl;
 }
 
-// Tile placement: blockIdx order (dispatch is in order per XCD, so every
-// predecessor is running or done), or a dynamic ticket (A.mode bit 0) as the
-// fallback that needs no dispatch-order assumption.
-template <int BLOCK>
-__device__ __forceinline__ unsigned tile_index(const Args& A, unsigned* s_tile) {
-    if (!(A.mode & 1)) return blockIdx.x;
-    if (threadIdx.x == 0) *s_tile = atomicAdd(A.ticket, 1u);
-    __syncthreads();
-    return (unsigned)uni((int)*s_tile);
+// Workgroup barrier ordering LDS only. __syncthreads() also waits for every
+// outstanding global load of the wave (vmcnt(0)); the tile barriers only
+// publish LDS values, so projection-column loads stay in flight across the
+// look-back instead of being drained before it.
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // Per-tile compaction: the selection words of every (k, wave) are counted,
@@ -224,11 +242,10 @@ struct Tile {
     u64 excl[NCH][NW];
     u64 prefix[NCH];
     u64 agg[NCH];
-    unsigned tile;
 };
 
 // counts[ch][k] : per-lane value for row k (rows: 0/1 selection, Utf8: bytes)
-template <int BLOCK, int K, int NCH>
+template <int BLOCK, int K, int NCH, int R = 1, int SLEEP = 1, int SPREAD = 1>
 __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
                                              const unsigned (&cnt)[NCH][K], int lane, int wave) {
     constexpr int WAVES = BLOCK / 64;
@@ -237,10 +254,10 @@ __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>&
     for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const u64 s = wave_sum((u64)cnt[ch][k]);
+            const u64 s = ch == 0 ? (u64)__builtin_popcountll(__ballot(cnt[0][k] != 0)) : wave_sum((u64)cnt[ch][k]);
             if (lane == 0) T.cnt[ch][k * WAVES + wave] = s;
         }
-    __syncthreads();
+    lds_sync();
     if (wave == 0) {
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
@@ -249,7 +266,7 @@ __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>&
             if (lane < NW) T.excl[ch][lane] = incl - c;
             const u64 agg = __shfl(incl, NW - 1, 64);
             const u64 pre = (A.mode & 2) ? (ch == 0 ? (u64)tile * BLOCK * K : 0ull)
-                                         : lookback(A.status + (i64)ch * A.n_tiles, tile, agg, lane, A.err);
+                                         : lookback<R, SLEEP, SPREAD>(A.status + (i64)ch * A.n_tiles * SPREAD, tile, agg, lane, A.err);
             if (lane == 0) {
                 T.prefix[ch] = pre;
                 T.agg[ch] = agg;
@@ -257,7 +274,7 @@ __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>&
             }
         }
     }
-    __syncthreads();
+    lds_sync();
 }
 
 // Copy the selected rows of Utf8 input u into output o (rebased i32

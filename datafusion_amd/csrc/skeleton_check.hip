@@ -10,8 +10,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     constexpr int BLOCK = 512, K = 8, WAVES = BLOCK / 64, NCH = 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);
     __shared__ dfmi::Tile<BLOCK, K, NCH> T;
-    __shared__ unsigned s_tile;
-    const unsigned tile = dfmi::tile_index<BLOCK>(A, &s_tile);
+    const unsigned tile = blockIdx.x;
     const i64 base = (i64)tile * (BLOCK * K);
     const i64 rem = A.n_rows - base;
     u64 c0[K];
@@ -30,7 +29,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
         len0[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[0][row + 1] - A.offs[0][row]) : 0u;
         cnt[1][k] = len0[k];
     }
-    dfmi::tile_offsets<BLOCK, K, NCH>(A, T, tile, cnt, lane, wave);
+    dfmi::tile_offsets<BLOCK, K, NCH, 4, 2, 16>(A, T, tile, cnt, lane, wave);
     const i64 obase = (i64)T.prefix[0];
     unsigned dst[K];
     for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);
