@@ -114,6 +114,10 @@ EXPORTED = [
     "dfmi_context_destroy",
     "dfmi_context_set_stream",
     "dfmi_filter_project",
+    "dfmi_filter_project_host",
+    "dfmi_host_result_num_columns",
+    "dfmi_host_result_column",
+    "dfmi_host_result_free",
     "dfmi_last_timing",
     "dfmi_generate_column",  # include/dfmi_datasource.h
 ]
@@ -190,6 +194,16 @@ def lib() -> C.CDLL:
                                       C.POINTER(dfmi_batch), C.POINTER(dfmi_out_column), C.c_uint32,
                                       C.POINTER(dfmi_error)]
     L.dfmi_filter_project.restype = C.c_int32
+    L.dfmi_filter_project_host.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                           C.POINTER(dfmi_batch), C.c_uint32, C.POINTER(C.c_void_p),
+                                           C.POINTER(dfmi_error)]
+    L.dfmi_filter_project_host.restype = C.c_int32
+    L.dfmi_host_result_num_columns.argtypes = [C.c_void_p]
+    L.dfmi_host_result_num_columns.restype = C.c_int32
+    L.dfmi_host_result_column.argtypes = [C.c_void_p, C.c_int32, C.POINTER(dfmi_column)]
+    L.dfmi_host_result_column.restype = C.c_int32
+    L.dfmi_host_result_free.argtypes = [C.c_void_p]
+    L.dfmi_host_result_free.restype = None
     L.dfmi_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.dfmi_last_timing.restype = C.c_int32
     L.dfmi_generate_column.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64,

@@ -280,9 +280,16 @@ extern "C" int32_t dfmi_context_create(int32_t device, void* stream, dfmi_contex
     return DFMI_OK;
 }
 
+namespace dfmi {
+int ctx_device(const dfmi_context* c) { return c->device; }
+hipStream_t ctx_stream(const dfmi_context* c) { return c->stream; }
+void host_arena_release(const dfmi_context* c);
+}  // namespace dfmi
+
 extern "C" void dfmi_context_destroy(dfmi_context* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    dfmi::host_arena_release(c);
     if (c->ws) (void)hipFree(c->ws);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->host_hdr) (void)hipHostFree(c->host_hdr);

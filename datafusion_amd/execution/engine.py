@@ -149,3 +149,55 @@ class DeviceEngine:
             else:
                 result.append(Array(t, length, k["values"], k.get("validity") if nulls else None, None, nulls))
         return result
+
+    def filter_project_host(self, predicate, projections: Optional[Sequence], batch: RecordBatch,
+                            flags: int = 0) -> List[Array]:
+        """The same pull over a HOST batch through dfmi_filter_project_host:
+        the library stages the Arrow buffers into HBM and returns host
+        results (the path a Rust caller with arrow 0.12 buffers takes)."""
+        import numpy as np
+        from ..arrow import _bytes_tensor, _offsets_tensor
+        L = _abi.lib()
+        cols = batch.columns
+        if any(c.values.device.type != "cpu" for c in cols):
+            raise ValueError("filter_project_host takes a host batch")
+        projections = list(projections or [])
+        carr = (_abi.dfmi_column * max(1, len(cols)))()
+        for i, a in enumerate(cols):
+            carr[i] = column_struct(a)
+        cb = _abi.dfmi_batch()
+        cb.num_columns = len(cols)
+        cb.num_rows = batch.num_rows()
+        cb.columns = carr
+        progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
+        err = _abi.dfmi_error()
+        res = C.c_void_p()
+        L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        rc = L.dfmi_filter_project_host(self.ctx, predicate.handle if predicate is not None else None,
+                                        progs, len(projections), C.byref(cb), flags, C.byref(res), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        out = []
+        try:
+            for i in range(L.dfmi_host_result_num_columns(res)):
+                v = _abi.dfmi_column()
+                L.dfmi_host_result_column(res, i, C.byref(v))
+                t = DataType(v.type)
+                n = v.length
+                if t == DataType.Utf8:
+                    offs = np.ctypeslib.as_array(C.cast(v.offsets, C.POINTER(C.c_int32)), shape=(n + 1,)).copy()
+                    nb = int(offs[-1])
+                else:
+                    offs = None
+                    nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
+                vals = (np.ctypeslib.as_array(C.cast(v.values, C.POINTER(C.c_uint8)), shape=(nb,))
+                        if nb else np.zeros(0, np.uint8))
+                valid = None
+                if v.null_count and v.validity:
+                    valid = _bytes_tensor(np.ctypeslib.as_array(C.cast(v.validity, C.POINTER(C.c_uint8)),
+                                                            shape=((n + 7) // 8,)).copy())
+                out.append(Array(t, n, _bytes_tensor(vals.copy()), valid,
+                                 _offsets_tensor(offs, "cpu") if offs is not None else None, v.null_count))
+        finally:
+            L.dfmi_host_result_free(res)
+        return out

@@ -220,6 +220,28 @@ int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* predicate,
                             const dfmi_batch* input, dfmi_out_column* outputs,
                             uint32_t flags, dfmi_error* err);
 
+/* ---------------------------------------------------------------------------
+ * Host-buffer form, for callers whose batches live in host memory (the Rust
+ * reference's arrow 0.12 buffers from csv::Reader, csv_sql.rs:49): the same
+ * pull as dfmi_filter_project -- FilterRelation::next (filter.rs:46-72) +
+ * filter() (filter.rs:80-111) + ProjectRelation::next (projection.rs:45-66)
+ * -- but `input` holds HOST pointers. The library moves the buffers into HBM
+ * (pinned staging), runs the fused pass, and copies the exact-size results
+ * into host buffers it owns until dfmi_host_result_free. Passthrough columns
+ * (Arc clones, expression.rs:272-276) are returned as copies.
+ * ------------------------------------------------------------------------- */
+typedef struct dfmi_host_result dfmi_host_result;
+
+int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_program* predicate,
+                                 const dfmi_program* const* projections, int32_t num_projections,
+                                 const dfmi_batch* input, uint32_t flags,
+                                 dfmi_host_result** out, dfmi_error* err);
+int32_t dfmi_host_result_num_columns(const dfmi_host_result* result);
+/* Host view of result column i; buffers stay valid until the result is freed.
+ * `validity` is NULL when null_count == 0 (filtered outputs never have one). */
+int32_t dfmi_host_result_column(const dfmi_host_result* result, int32_t i, dfmi_column* view);
+void dfmi_host_result_free(dfmi_host_result* result);
+
 /* Device time in milliseconds of the last dfmi_filter_project's kernels
  * (HIP events on the context stream), and the dominant kernel's share. */
 int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main_kernel_ms);

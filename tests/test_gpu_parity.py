@@ -55,21 +55,31 @@ def run_both(schema, batch, pred, projs, flags=0):
         ref = oracle_filter_project(schema, batch, pred, projs, flags)
     except ExecutionError as e:
         ref_err = e
+    host_err = host = None
     try:
         p = compile_scalar_expr(None, pred, schema, flags) if pred is not None else None
         cp = [compile_scalar_expr(None, e, schema, flags) for e in projs]
-        dev = engine().filter_project(p, cp, batch, flags)
         names = [c.get_name() for c in cp] if cp else [f.name for f in schema.fields]
+        try:
+            # host-buffer entry point (dfmi_filter_project_host): staged H2D + D2H
+            host = engine().filter_project_host(p, cp, batch, flags)
+        except ExecutionError as e:
+            host_err = e
+        dev = engine().filter_project(p, cp, batch, flags)
     except ExecutionError as e:
         dev_err = e
     if ref_err is not None or dev_err is not None:
         assert ref_err is not None and dev_err is not None, (ref_err, dev_err)
         assert (dev_err.kind, dev_err.message) == (ref_err.kind, ref_err.message)
+        if host_err is not None or host is not None:
+            assert host_err is not None and (host_err.kind, host_err.message) == (ref_err.kind, ref_err.message)
         return None
-    assert len(dev) == len(ref)
-    for i, ((rname, r), d) in enumerate(zip(ref, dev)):
+    assert host_err is None, host_err
+    assert len(dev) == len(ref) == len(host)
+    for i, ((rname, r), d, h) in enumerate(zip(ref, dev, host)):
         assert names[i] == rname
         assert_same(d.cpu(), r, "%s col %d" % (rname, i))
+        assert_same(h, r, "host path: %s col %d" % (rname, i))
     return dev, ref
 
 

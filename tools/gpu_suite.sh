@@ -1,10 +1,12 @@
 #!/bin/bash
-# GPU parity suite + smoke + short bench with the query-compiled kernels
+# GPU parity suite + smoke + short bench (one gpurun call).
+# usage: tools/gpu_suite.sh [tag]
 set -o pipefail
+TAG=${1:-suite}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest12.log 2>&1
-rc=$?; tail -5 gpurun_out/pytest12.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke12.log 2>&1 || { cat gpurun_out/smoke12.log; exit 1; }
-cat gpurun_out/smoke12.log
-timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/bench12.json 2> gpurun_out/bench12.err || { tail gpurun_out/bench12.err; exit 1; }
-cat gpurun_out/bench12.json
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; tail -5 gpurun_out/pytest_$TAG.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { cat gpurun_out/smoke_$TAG.log; exit 1; }
+cat gpurun_out/smoke_$TAG.log
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
