@@ -33,6 +33,7 @@ using namespace dfmi;
 static constexpr size_t kHdrTicket = 0;
 static constexpr size_t kHdrErr = 8;
 static constexpr size_t kHdrTotals = 16;
+static constexpr size_t kHdrStats = 256;  // look-back statistics (DFMI_DEBUG_MODE bit 4)
 static constexpr size_t kHdrAlloc = 512;
 
 struct dfmi_context {
@@ -244,6 +245,8 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
     if (const char* e = getenv("DFMI_LOOKBACK_R")) X.R = std::max(1, std::min(16, atoi(e)));
     if (const char* e = getenv("DFMI_LOOKBACK_SLEEP")) X.sleep = std::max(0, std::min(127, atoi(e)));
     if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;  // diagnostics only
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 64)
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
@@ -395,6 +398,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             A.err = (unsigned long long*)(ctx->ws + kHdrErr);
             A.totals = (unsigned long long*)(ctx->ws + kHdrTotals);
             A.status = (unsigned long long*)(ctx->ws + kHdrAlloc);
+            A.stats = (unsigned long long*)(ctx->ws + kHdrStats);
             A.mode = 0;
             if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
             const unsigned grid = (unsigned)n_tiles;  // one block per tile
@@ -415,6 +419,12 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 dev_key = ~ew;
                 dev_kind = (int)(dev_key & 15);
                 dev_key &= ~15ull;
+            }
+            if (A.mode & 4) {
+                uint64_t st3[3];
+                memcpy(st3, ctx->host_hdr + kHdrStats, sizeof st3);
+                fprintf(stderr, "dfmi look-back: tiles %lld polls %llu sleeps %llu wait %.3f ms (summed over tiles)\n",
+                        (long long)n_tiles, (unsigned long long)st3[0], (unsigned long long)st3[1], st3[2] * 1e-5);
             }
             float m1 = 0, m2 = 0;
             (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);

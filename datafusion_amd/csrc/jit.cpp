@@ -63,6 +63,7 @@ struct Gen {
     std::ostringstream o;
     int tmp = 0;
     bool filtered_cols = false;  // projection after a Selection: columns all-valid
+    std::string sfx;             // name suffix of the register set being evaluated
 
     Gen(const Plan& p, Launch& x) : P(p), X(x) {}
 
@@ -88,7 +89,7 @@ struct Gen {
     // column value for the current row k (inside a per-k loop)
     Val col(const IrNode& n) {
         const int s = X.slot_of_col(n.col);
-        const std::string id = std::to_string(s);
+        const std::string id = std::to_string(s) + sfx;
         Val r;
         if (n.type == DFMI_TYPE_BOOLEAN) {
             r.v = "(((bw" + id + "[k] >> lane) & 1) != 0)";
@@ -291,9 +292,10 @@ static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Lau
                 std::string g = guard ? std::string(guard) : "";
                 if (!full) g = g.empty() ? "(" + base + " + k * BLOCK + tid < A.n_rows)"
                                          : "(" + base + " + k * BLOCK + tid < A.n_rows) && " + g;
+                const std::string ld = (X.nt & 1) ? "__builtin_nontemporal_load(p_ + k * BLOCK)" : "p_[k * BLOCK]";
                 o << "    { const u64* p_ = (const u64*)A.col[" << s << "] + " << base << " + tid;\n"
                   << "#pragma unroll\n      for (int k = 0; k < K; ++k) c" << id << "[k] = "
-                  << (g.empty() ? "p_[k * BLOCK];" : "(" + g + ") ? p_[k * BLOCK] : 0ull;") << " }\n";
+                  << (g.empty() ? ld + ";" : "(" + g + ") ? " + ld + " : 0ull;") << " }\n";
             }
             if (valid_words && X.col_nullable(col)) {
                 o << "#pragma unroll\n    for (int k = 0; k < K; ++k) vw" << id << "[k] = dfmi::bitmap_word(A.valid[" << s
@@ -315,16 +317,13 @@ std::string generate(const Plan& P, Launch& X) {
     if (P.pred) {
         const int nch = 1 + (int)X.utf8_outs.size();
         o << "  constexpr int NCH = " << nch << ";\n";
-        o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
-        // one tile per block in dispatch order (in order per XCD, so every
-        // tile a block waits on in the look-back is running or done)
-        o << "  const unsigned t = blockIdx.x;\n";
-        emit_decls(o, X.pred_slots, X, "", true);
-        emit_decls(o, X.proj_slots, X, "", false);
-        emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
-        {
-            o << "  const i64 base = (i64)t * (BLOCK * K);\n";
-            // predicate per row
+        const std::string tparams = std::to_string(X.R) + ", " + std::to_string(X.sleep) + ", " +
+                                    std::to_string(X.spread) + ", " + std::to_string(X.window);
+        // One tile: predicate, projection-only loads, scan + look-back,
+        // compacted stores; `cur` names the tile's register set.
+        auto tile_body = [&](const std::string& cur, const std::string& T) {
+            o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
+            g.sfx = cur;
             g.filtered_cols = false;
             o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
             o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
@@ -333,7 +332,7 @@ std::string generate(const Plan& P, Launch& X) {
                 o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
             o << "  }\n";
             // projection-only columns, loaded only where selected
-            emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
             // compaction offsets (rows + Utf8 bytes)
             o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
               << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
@@ -344,10 +343,12 @@ std::string generate(const Plan& P, Launch& X) {
                   << "    len" << j << "[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[" << u << "][row + 1] - A.offs["
                   << u << "][row]) : 0u;\n    cnt[" << (j + 1) << "][k] = len" << j << "[k];\n  }\n";
             }
-            o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << X.R << ", " << X.sleep << ", " << X.spread
-              << ">(A, T, t, cnt, lane, wave);\n";
-            o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
-              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
+            {
+                o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << tparams << ">(A, " << T << ", t, cnt, lane, wave);\n";
+            }
+            o << "  const i64 obase = (i64)" << T << ".prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
+              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)" << T
+              << ".excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
             // projections over the selected rows (filtered batch: no validity)
             g.filtered_cols = true;
             o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
@@ -367,21 +368,36 @@ std::string generate(const Plan& P, Launch& X) {
                 }
                 if (os.out_type == DFMI_TYPE_BOOLEAN)
                     o << "    ((u8*)A.out[" << oi << "] + obase)[d] = (" << v.v << ") ? 1 : 0;\n";
+                else if (X.nt & 2)
+                    o << "    __builtin_nontemporal_store((u64)(" << v.v << "), (u64*)A.out[" << oi << "] + obase + d);\n";
                 else
                     o << "    ((u64*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
             }
             o << "  }\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
-                o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << X.utf8_outs[j].second << ", "
-                  << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";
+                o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << X.utf8_outs[j].second
+                  << ", " << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";
             }
             if (!X.utf8_outs.empty()) {
                 o << "  if (tid == 0 && t == (unsigned)A.n_tiles - 1) {\n";
                 for (size_t j = 0; j < X.utf8_outs.size(); ++j)
-                    o << "    A.out_offs[" << X.utf8_outs[j].first << "][T.prefix[0] + T.agg[0]] = (int)(T.prefix["
-                      << (j + 1) << "] + T.agg[" << (j + 1) << "]);\n";
+                    o << "    A.out_offs[" << X.utf8_outs[j].first << "][" << T << ".prefix[0] + " << T
+                      << ".agg[0]] = (int)(" << T << ".prefix[" << (j + 1) << "] + " << T << ".agg[" << (j + 1)
+                      << "]);\n";
                 o << "  }\n";
             }
+            o << "  }\n";
+            g.sfx.clear();
+        };
+        {
+            // one tile per block in dispatch order (in order per XCD, so every
+            // tile a block waits on in the look-back is running or done)
+            o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
+            o << "  const unsigned t = blockIdx.x;\n";
+            emit_decls(o, X.pred_slots, X, "", true);
+            emit_decls(o, X.proj_slots, X, "", false);
+            emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
+            tile_body("", "T");
         }
     } else {
         // projection only: dense rows, ballot-packed validity / Boolean bitmaps

@@ -39,6 +39,11 @@ struct Launch {
     // between polls, one status word per `spread` words (16 = one per 128-byte
     // line: polling blocks then do not contend on shared lines)
     int R = 1, sleep = 32, spread = 16;
+    // predecessors read per poll, one lane each: 8 measured best at s=0.5
+    // (64 cost ~9% of the C2 kernel in polling traffic)
+    int window = 8;
+    // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores
+    int nt = 0;
     const dfmi_batch* in = nullptr;
     std::vector<int> num_cols;   // arg slot -> input column (numeric and Boolean)
     std::vector<int> pred_slots; // slots the predicate reads (loaded for every row)

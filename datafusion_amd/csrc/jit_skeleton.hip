@@ -47,6 +47,7 @@ struct Args {
     unsigned* ticket;                  // spare counter (zeroed per launch)
     u64* err;                          // max(~key) error word
     u64* totals;                       // [0..8) channel totals, [8..24) null counts
+    u64* stats;                        // look-back statistics (mode bit 4): polls, sleeps, tiles
 };
 
 enum ErrKind : unsigned { ERRK_DIV_ZERO = 1, ERRK_DIV_OVERFLOW = 2, ERRK_LOOKBACK_TIMEOUT = 3, ERRK_CAPACITY = 4 };
@@ -166,22 +167,32 @@ __device__ __forceinline__ u64 ld_status(u64* p) {
 // traffic off the data path (measured, DESIGN.md "Look-back").
 // The spin is bounded in wall time: a tile that could never resolve reports
 // a timeout instead of hanging the device.
-template <int R, int SLEEP, int SPREAD>
-__device__ u64 lookback(u64* st, unsigned tile, u64 agg, int lane, u64* err) {
-    if (tile == 0) {
-        if (lane == 0) st_status(st, FLAG_P | agg);
-        return 0;
-    }
-    if (lane == 0) st_status(st + (i64)tile * SPREAD, FLAG_A | agg);
+// Publish the tile aggregate (tile 0: its inclusive prefix) -- lane 0 only.
+template <int SPREAD>
+__device__ __forceinline__ void lb_publish(u64* st, unsigned tile, u64 agg, int lane) {
+    if (lane == 0) st_status(st + (i64)tile * SPREAD, (tile == 0 ? FLAG_P : FLAG_A) | agg);
+}
+
+// Resolve the exclusive prefix of a tile whose aggregate is published: read
+// R windows of 64 predecessor status words (one per lane per window, all R
+// loads in flight together) per round trip, summing aggregates until an
+// inclusive prefix is found; publish our own inclusive prefix.
+template <int R, int SLEEP, int SPREAD, int W = 64>
+__device__ u64 lb_resolve(u64* st, unsigned tile, u64 agg, int lane, u64* err, u64* stats = nullptr) {
+    static_assert(W >= 1 && W <= 64, "window of 1..64 predecessors per wave load");
+    if (tile == 0) return 0;
     u64 excl = 0;
     i64 j = (i64)tile - 1;  // highest predecessor not yet accounted for
     const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    unsigned polls = 0, sleeps = 0;
     while (true) {
+        ++polls;
         u64 w[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const i64 idx = j - lane - 64 * r;
-            w[r] = idx >= 0 ? ld_status(st + idx * SPREAD) : FLAG_P;
+            const i64 idx = j - lane - W * r;
+            // lanes past the window read nothing and stand for a zero aggregate
+            w[r] = lane >= W ? FLAG_A : (idx >= 0 ? ld_status(st + idx * SPREAD) : FLAG_P);
         }
         bool done = false, stall = false;
 #pragma unroll
@@ -205,7 +216,7 @@ __device__ u64 lookback(u64* st, unsigned tile, u64 agg, int lane, u64* err) {
                 break;
             }
             excl += wave_sum(w[r] & VAL_MASK);
-            j -= 64;
+            j -= W;
         }
         if (done) break;
         if (stall) {
@@ -214,10 +225,28 @@ __device__ u64 lookback(u64* st, unsigned tile, u64 agg, int lane, u64* err) {
                 break;
             }
             __builtin_amdgcn_s_sleep(SLEEP);
+            ++sleeps;
         }
     }
     if (lane == 0) st_status(st + (i64)tile * SPREAD, FLAG_P | (excl + agg));
+    if (stats && lane == 0) {
+        atomicAdd(stats, (u64)polls);
+        atomicAdd(stats + 1, (u64)sleeps);
+        atomicAdd(stats + 2, __builtin_amdgcn_s_memrealtime() - t0);
+    }
     return excl;
+}
+
+// Single-pass decoupled look-back (one wave): publish, then resolve. Status
+// words are SPREAD words apart: with one word per 128-byte line the hundreds
+// of polling waves do not serialise on a few shared lines, and s_sleep(SLEEP)
+// between polls keeps the polling traffic off the data path (measured,
+// DESIGN.md "Look-back"). The spin is bounded in wall time: a tile that could
+// never resolve reports a timeout instead of hanging the device.
+template <int R, int SLEEP, int SPREAD>
+__device__ u64 lookback(u64* st, unsigned tile, u64 agg, int lane, u64* err) {
+    lb_publish<SPREAD>(st, tile, agg, lane);
+    return lb_resolve<R, SLEEP, SPREAD>(st, tile, agg, lane, err);
 }
 
 // Workgroup barrier ordering LDS only. __syncthreads() also waits for every
@@ -245,9 +274,11 @@ struct Tile {
 };
 
 // counts[ch][k] : per-lane value for row k (rows: 0/1 selection, Utf8: bytes)
-template <int BLOCK, int K, int NCH, int R = 1, int SLEEP = 1, int SPREAD = 1>
-__device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
-                                             const unsigned (&cnt)[NCH][K], int lane, int wave) {
+// First half of the tile step: per-(k, wave) counts, the one-wave scan of the
+// tile's words and the publication of the tile aggregate (no waiting).
+template <int BLOCK, int K, int NCH, int SPREAD = 1>
+__device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
+                                                  const unsigned (&cnt)[NCH][K], int lane, int wave) {
     constexpr int WAVES = BLOCK / 64;
     constexpr int NW = K * WAVES;
 #pragma unroll
@@ -265,15 +296,39 @@ __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>&
             const u64 incl = wave_incl_scan(c, lane);
             if (lane < NW) T.excl[ch][lane] = incl - c;
             const u64 agg = __shfl(incl, NW - 1, 64);
+            if (!(A.mode & 2)) lb_publish<SPREAD>(A.status + (i64)ch * A.n_tiles * SPREAD, tile, agg, lane);
+            if (lane == 0) T.agg[ch] = agg;
+        }
+    }
+}
+
+// Second half: wave 0 resolves the tile's global offsets into T.prefix; a
+// block barrier (lds_sync) must follow before other waves read them.
+template <int BLOCK, int K, int NCH, int R = 1, int SLEEP = 1, int SPREAD = 1, int W = 64>
+__device__ __forceinline__ void tile_resolve(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile, int lane,
+                                             int wave) {
+    if (wave == 0) {
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const u64 agg = T.agg[ch];
             const u64 pre = (A.mode & 2) ? (ch == 0 ? (u64)tile * BLOCK * K : 0ull)
-                                         : lookback<R, SLEEP, SPREAD>(A.status + (i64)ch * A.n_tiles * SPREAD, tile, agg, lane, A.err);
+                                         : lb_resolve<R, SLEEP, SPREAD, W>(A.status + (i64)ch * A.n_tiles * SPREAD,
+                                                                           tile, agg, lane, A.err,
+                                                                           (A.mode & 4) ? A.stats : nullptr);
             if (lane == 0) {
                 T.prefix[ch] = pre;
-                T.agg[ch] = agg;
                 if (tile == (unsigned)A.n_tiles - 1) A.totals[ch] = pre + agg;
             }
         }
     }
+}
+
+// Both halves back to back: the tile's output offsets in T.
+template <int BLOCK, int K, int NCH, int R = 1, int SLEEP = 1, int SPREAD = 1, int W = 64>
+__device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
+                                             const unsigned (&cnt)[NCH][K], int lane, int wave) {
+    tile_scan_publish<BLOCK, K, NCH, SPREAD>(A, T, tile, cnt, lane, wave);
+    tile_resolve<BLOCK, K, NCH, R, SLEEP, SPREAD, W>(A, T, tile, lane, wave);
     lds_sync();
 }
 

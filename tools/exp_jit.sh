@@ -10,6 +10,6 @@ if [ "$1" = "--parity" ]; then
 fi
 for spec in "$@"; do
   name=${spec%%:*}; envs=${spec#*:}
-  env ${envs//,/ } timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/exp_$name.json 2> gpurun_out/exp_$name.err || { tail -3 gpurun_out/exp_$name.err; exit 1; }
+  env ${envs//,/ } timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu --extra '' > gpurun_out/exp_$name.json 2> gpurun_out/exp_$name.err || { tail -3 gpurun_out/exp_$name.err; exit 1; }
   python -c "import json,sys; d=json.load(open('gpurun_out/exp_$name.json')); print('$name', ' '.join('%s:%.3f'%(k,v['kernel_ms']) for k,v in d['sweep'].items()))"
 done
