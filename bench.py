@@ -192,6 +192,136 @@ def q6_line(eng, dev, rank, world, steps, warmup, dist, rows):
                          "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_row": round(bpr, 3)}}
 
 
+C3_ROWS = 500_000_000
+C3_BATCHES = 4  # i32 Utf8 offsets cap one batch's bytes at 2 GiB (arrow BinaryArray)
+
+
+def _utf8_dictionary(seed, words=1000, max_len=24):
+    """'w<i>' padded with lowercase letters to a length drawn from [len, max_len]."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(words):
+        w = b"w%d" % i
+        ln = int(rng.integers(len(w), max_len + 1))
+        out.append(w + bytes(rng.integers(97, 123, ln - len(w)).astype(np.uint8)))
+    return out
+
+
+def _c3_batch(dev, g, n, dict_bytes, dict_off, dict_len):
+    """One C3 batch on the device: v Float64 with ~10% nulls, s Utf8 drawn from
+    the dictionary (non-null)."""
+    from datafusion_amd.arrow import Array
+    v = torch.rand(n, device=dev, dtype=torch.float64, generator=g)
+    valid = torch.rand(n, device=dev, generator=g) >= 0.10
+    pad = (-n) % 64
+    vb = torch.cat([valid, torch.zeros(pad, dtype=torch.bool, device=dev)]).view(-1, 8).to(torch.uint8)
+    vbits = (vb << torch.arange(8, device=dev, dtype=torch.uint8)).sum(1, dtype=torch.uint8)
+    nulls = int(n - valid.sum().item())
+    idx = torch.randint(0, len(dict_len), (n,), device=dev, generator=g)
+    lens = dict_len[idx]
+    offs64 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs64[1:])
+    total = int(offs64[-1].item())
+    assert total < 2 ** 31
+    data = torch.empty(total, dtype=torch.uint8, device=dev)
+    step = 1 << 24
+    for r0 in range(0, n, step):  # bytes of rows [r0, r1) in bounded-memory chunks
+        r1 = min(n, r0 + step)
+        li = lens[r0:r1]
+        row = torch.repeat_interleave(torch.arange(r0, r1, device=dev), li)
+        within = torch.arange(row.numel(), device=dev) - (offs64[row] - offs64[r0])
+        data[offs64[r0]:offs64[r1]] = dict_bytes[dict_off[idx[row]] + within]
+    s = Array(DataType.Utf8, n, data, None, offs64.to(torch.int32), 0)
+    va = Array(DataType.Float64, n, v.view(torch.uint8), vbits, None, nulls)
+    return [s, va], total
+
+
+def c3_line(eng, dev, rank, world, steps, warmup, dist):
+    """C3 (BASELINE.json configs[2]): 5e8 rows = 4 batches of 1.25e8 rows, a
+    nullable Float64 v and a Utf8 s. Two queries, each one launch per batch:
+      eq:  SELECT s, v WHERE s = <word 17> (Utf8 equality, DFMI_FLAG_EXT_UTF8_COMPARE)
+      lt:  SELECT s, v WHERE v < 0.5     (nullable predicate, Utf8 offset/byte gather)
+    Parity of both query shapes: tests/test_gpu_parity.py::test_utf8_gather_and_equality."""
+    from datafusion_amd._abi import DFMI_FLAG_EXT_UTF8_COMPARE
+    from datafusion_amd.execution.engine import column_struct
+    from datafusion_amd.logicalplan import Utf8
+    words = _utf8_dictionary(SEED)
+    w17 = words[17].decode()  # one dictionary word: selectivity ~1/1000
+    dict_bytes = torch.tensor(np.frombuffer(b"".join(words), dtype=np.uint8), device=dev)
+    dict_len = torch.tensor([len(w) for w in words], dtype=torch.int64, device=dev)
+    dict_off = torch.cumsum(dict_len, 0) - dict_len
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + 1000 + rank)
+    nb = C3_ROWS // C3_BATCHES
+    batches, nbytes = [], 0
+    for _ in range(C3_BATCHES):
+        b, t = _c3_batch(dev, g, nb, dict_bytes, dict_off, dict_len)
+        batches.append(b)
+        nbytes += t
+    torch.cuda.empty_cache()
+    schema = Schema([Field("s", DataType.Utf8, False), Field("v", DataType.Float64, True)])
+    out_s_off = torch.zeros(nb + 16, dtype=torch.int32, device=dev)
+    out_s_data = torch.empty(max(b[0].values.numel() for b in batches), dtype=torch.uint8, device=dev)
+    out_v = torch.empty(nb, dtype=torch.float64, device=dev)
+    L = _abi.lib()
+    queries = {
+        "eq": (BinaryExpr(Column(0), Operator.Eq, Literal(Utf8(w17))), DFMI_FLAG_EXT_UTF8_COMPARE),
+        "lt": (BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5))), 0),
+    }
+    res = {}
+    for qn, (pe, flags) in queries.items():
+        pred = compile_scalar_expr(None, pe, schema, flags)
+        projs = [compile_scalar_expr(None, Column(0), schema, flags), compile_scalar_expr(None, Column(1), schema, flags)]
+        progs = (C.c_void_p * 2)(*[p.handle.value for p in projs])
+        calls = []
+        for b in batches:
+            carr = (_abi.dfmi_column * 2)(column_struct(b[0]), column_struct(b[1]))
+            cb = _abi.dfmi_batch(2, 0, nb, carr)
+            outs = (_abi.dfmi_out_column * 2)()
+            outs[0].offsets = out_s_off.data_ptr()
+            outs[0].data = out_s_data.data_ptr()
+            outs[0].data_capacity = out_s_data.numel()
+            outs[1].values = out_v.data_ptr()
+            calls.append((carr, cb, outs))
+        err = _abi.dfmi_error()
+        acc = {"sel": 0, "sel_bytes": 0, "kms": 0.0}
+
+        def step():
+            acc["sel"] = acc["sel_bytes"] = 0
+            acc["kms"] = 0.0
+            for carr, cb, outs in calls:
+                rc = L.dfmi_filter_project(eng.ctx, pred.handle, progs, 2, C.byref(cb), outs, flags, C.byref(err))
+                if rc != 0:
+                    raise RuntimeError(err.message.decode())
+                acc["sel"] += outs[0].length
+                acc["sel_bytes"] += outs[0].data_length
+                acc["kms"] += eng.last_timing()[1]
+            return acc["sel"]
+
+        kms_all = []
+
+        def timed():
+            r = step()
+            kms_all.append(acc["kms"])
+            return r
+
+        el, _, selected = timed_steps(timed, steps, warmup, dist, eng, dev)
+        kms = float(np.mean(kms_all[warmup:]))
+        n = C3_ROWS
+        s = selected / n
+        # SURVEY §8(d): v 8 B + validity 1/8 B, s offsets 4 B + its bytes; out s*(8 + 4) + selected bytes
+        alg = n * (8.0 + 0.125 + 4.0) + nbytes + selected * 12.0 + acc["sel_bytes"]
+        ach = alg / (kms * 1e-3) / 1e9
+        res[qn] = {"query": "SELECT s, v WHERE " + ("s = '%s'" % w17 if qn == "eq" else "v < 0.5"),
+                   "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3,
+                   "kernel_ms": round(kms, 4), "selectivity": round(s, 5), "selected": selected,
+                   "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(ach / HBM_PEAK_GBS, 4),
+                                "algorithmic_bytes_per_row": round(alg / n, 3)}}
+    return {"workload": "C3: 5e8 rows per GPU (4 batches of 1.25e8), nullable Float64 v (10%% nulls) + "
+                        "Utf8 s (1000-word dictionary, avg %.2f B)" % (nbytes / C3_ROWS), **res}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,6 +372,8 @@ def main():
     for name in [x for x in args.extra.split(",") if x]:
         if name == "c4":
             extra["c4"] = q6_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS)
+        elif name == "c3":
+            extra["c3"] = c3_line(eng, dev, rank, world, args.steps, args.warmup, dist)
         else:
             raise SystemExit("unknown extra config %r" % name)
         torch.cuda.empty_cache()

@@ -25,6 +25,8 @@
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <tuple>
+#include <vector>
 #include <string>
 #include <vector>
 
@@ -64,6 +66,11 @@ struct Gen {
     int tmp = 0;
     bool filtered_cols = false;  // projection after a Selection: columns all-valid
     std::string sfx;             // name suffix of the register set being evaluated
+    // predicate loop of a filtered tile: Utf8 `col = literal` comparisons are
+    // evaluated tile-wide before the loop (utf8_eq_lit_tile); each entry is
+    // (array name, utf8 slot, string literal index)
+    bool tile_pre = false;
+    std::vector<std::tuple<std::string, int, int>> pre_eq;
 
     Gen(const Plan& p, Launch& x) : P(p), X(x) {}
 
@@ -147,8 +154,14 @@ struct Gen {
                 const int u = X.slot_of_utf8(C.col);
                 const int sl = strlit(S.str);
                 const std::string vu = filtered_cols ? "true" : "dfmi::utf8_valid(A, " + std::to_string(u) + ", row)";
-                o << "    const bool " << v << "_e = " << vu << " && dfmi::utf8_eq_lit(A, " << u << ", row, " << sl
-                  << ");\n";
+                if (tile_pre) {
+                    const std::string arr = "uq" + std::to_string(pre_eq.size()) + sfx;
+                    pre_eq.emplace_back(arr, u, sl);
+                    o << "    const bool " << v << "_e = " << vu << " && " << arr << "[k];\n";
+                } else {
+                    o << "    const bool " << v << "_e = " << vu << " && dfmi::utf8_eq_lit(A, " << u << ", row, " << sl
+                      << ");\n";
+                }
                 o << "    const bool " << v << " = " << (eq ? "" : "!") << v << "_e;\n";
             }
             return Val{v, "true"};
@@ -325,12 +338,25 @@ std::string generate(const Plan& P, Launch& X) {
             o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
             g.sfx = cur;
             g.filtered_cols = false;
+            const std::string head = o.str();
+            g.tile_pre = true;
+            g.pre_eq.clear();
             o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
             o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
             const Val r = g.emit(P.pred, P.pred->root, 0, "in");
             if (P.pred->type == DFMI_TYPE_BOOLEAN && !r.v.empty())
                 o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
             o << "  }\n";
+            g.tile_pre = false;
+            if (!g.pre_eq.empty()) {  // splice the tile-wide Utf8 compares in front of the loop
+                const std::string loop = o.str().substr(head.size());
+                std::ostringstream pre;
+                for (const auto& [arr, u, sl] : g.pre_eq)
+                    pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u
+                        << ", base, tid, " << sl << ", " << arr << ");\n";
+                o.str(head + pre.str() + loop);
+                o.seekp(0, std::ios_base::end);
+            }
             // projection-only columns, loaded only where selected
             emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
             // compaction offsets (rows + Utf8 bytes)
