@@ -330,7 +330,7 @@ def main():
     ap.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
     ap.add_argument("--sel", type=float, default=0.5, help="headline selectivity")
     ap.add_argument("--sweep", default="0.01,0.5,0.99", help="selectivities also reported (first=headline if set)")
-    ap.add_argument("--extra", default="c4", help="extra config lines (comma list: c4; empty = none)")
+    ap.add_argument("--extra", default="c4,c3", help="extra config lines (comma list: c4,c3; empty = none)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 

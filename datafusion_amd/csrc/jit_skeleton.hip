@@ -386,6 +386,45 @@ __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>&
     lds_sync();
 }
 
+// Copy L > 0 bytes from src to dst (any alignment) with aligned 4-byte
+// words: the output is assembled a word at a time from aligned source words
+// (v_alignbyte), interior output words are stored whole and only the two edge
+// words bytewise. Source words are clamped to the words holding src[0] and
+// src[L-1], so nothing outside them is read. 8 output words per chunk: all
+// of a chunk's loads are in flight before its stores (a byte-at-a-time
+// load->store loop pays one memory latency per byte).
+__device__ __forceinline__ void utf8_copy(const u8* src, u8* dst, unsigned L) {
+    const u64 sa = (u64)src, da = (u64)dst;
+    const u64 sw0 = sa & ~3ull, swl = (sa + L - 1) & ~3ull;
+    const u64 dw0 = da & ~3ull, dwe = (da + L + 3) & ~3ull;
+    for (u64 wb = dw0; wb < dwe; wb += 32) {
+        const i64 sb = (i64)sa + ((i64)wb - (i64)da);  // source address of output byte wb
+        const u64 sbw = (u64)sb & ~3ull;
+        const unsigned sh = (unsigned)sb & 3u;
+        unsigned sv[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            u64 a = sbw + 4ull * j;
+            a = a < sw0 ? sw0 : (a > swl ? swl : a);
+            sv[j] = *(const unsigned*)a;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u64 w = wb + 4ull * j;
+            if (w >= dwe) break;
+            const unsigned val = __builtin_amdgcn_alignbyte(sv[j + 1], sv[j], sh);
+            const i64 p = (i64)w - (i64)da;  // offset of the word's first byte in dst
+            if (p >= 0 && p + 4 <= (i64)L) {
+                *(unsigned*)w = val;
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (p + b >= 0 && p + b < (i64)L) ((u8*)w)[b] = (u8)(val >> (8 * b));
+            }
+        }
+    }
+}
+
 // Copy the selected rows of Utf8 input u into output o (rebased i32
 // offsets + bytes, filter.rs:94-105).
 template <int BLOCK, int K, int NCH>
@@ -406,20 +445,9 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
             report_err(A.err, 0, 0, ERRK_CAPACITY);
             continue;
         }
-        const u8* __restrict__ src = A.bytes[u] + A.offs[u][row];
-        u8* __restrict__ dd = A.out_data[o] + ob;
-        // 16-byte chunks: all of a chunk's loads are in flight before its
-        // stores (a byte-at-a-time load->store loop pays one memory latency
-        // per byte)
         const unsigned L = len[k];
-        for (unsigned i = 0; i < L; i += 16) {
-            u8 b[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) b[j] = i + j < L ? src[i + j] : (u8)0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (i + j < L) dd[i + j] = b[j];
-        }
+        if (L == 0) continue;
+        utf8_copy(A.bytes[u] + A.offs[u][row], A.out_data[o] + ob, L);
     }
 }
 
