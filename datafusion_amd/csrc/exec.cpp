@@ -252,6 +252,10 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
     const int64_t n_tiles = (n + tile_rows - 1) / tile_rows;
     if (n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
+    // a filtered batch with one Utf8 output packs rows and bytes into one
+    // 62-bit look-back word (31 + 31 bits, jit_skeleton.hip tile_scan_publish)
+    if (X.utf8_outs.size() == 1 && n >= (int64_t(1) << 31))
+        throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
 
     B.n_tiles = n_tiles;
 }

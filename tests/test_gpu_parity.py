@@ -293,6 +293,27 @@ def test_utf8_gather_and_equality():
         run_both(s, b, BinaryExpr(Column(0), op, Column(2)), [Column(2)], DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
+def test_utf8_many_tiles():
+    """Utf8 gather / equality over ~74 tiles: the packed rows+bytes look-back
+    word, aligned-word copies at every source/destination alignment, strings
+    longer than one 32-byte copy chunk, empty strings and nulls."""
+    n = 300_001
+    rng = np.random.default_rng(31)
+    words = [bytes(rng.integers(97, 123, int(rng.integers(0, 70))).astype(np.uint8)) for _ in range(300)]
+    words[7] = b"w7"
+    idx = rng.integers(0, len(words), n)
+    strs = [words[i] for i in idx]
+    sv = [None if rng.random() < 0.05 else x for x in strs]
+    s = Schema([Field("s", DataType.Utf8, True), Field("v", DataType.Float64, True)])
+    v = gen_unit_f64(5, 0, 0, n)
+    b = RecordBatch(s, [Array.from_strings(sv), Array.from_numpy(DataType.Float64, v, rng.random(n) >= 0.1)])
+    for k in (0.01, 0.3, 0.97):
+        run_both(s, b, BinaryExpr(Column(1), Operator.Lt, Literal(Float64(k))), [Column(0), Column(1)])
+    for w in ("w7", words[3].decode()):
+        run_both(s, b, BinaryExpr(Column(0), Operator.Eq, Literal(Utf8(w))), [Column(0), Column(1)],
+                 DFMI_FLAG_EXT_UTF8_COMPARE)
+
+
 def test_static_errors_match():
     s, batch = synth(1000)
     cases = [
