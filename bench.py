@@ -322,6 +322,52 @@ def c3_line(eng, dev, rank, world, steps, warmup, dist):
                         "Utf8 s (1000-word dictionary, avg %.2f B)" % (nbytes / C3_ROWS), **res}
 
 
+HOST_ROWS = 100_000_000
+
+
+def host_line(eng, steps, warmup):
+    """PCIe-inclusive rate: the C2 query at s=0.5 over a HOST
+    batch through dfmi_filter_project_host (pinned staging H2D, kernel, D2H of
+    the selected rows into library-owned host buffers). Never `value`."""
+    from datafusion_amd.arrow import Array, RecordBatch
+    from datafusion_amd.execution.engine import column_struct
+    from oracle_ffi import gen_unit_f64
+    n = HOST_ROWS
+    schema = Schema([Field(c, DataType.Float64, False) for c in "abc"])
+    b = RecordBatch(schema, [Array.from_numpy(DataType.Float64, gen_unit_f64(SEED, j, 0, n)) for j in range(3)])
+    pred_e, proj_e = query(0.5)
+    pred = compile_scalar_expr(None, pred_e, schema)
+    projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+    carr = (_abi.dfmi_column * 3)(*[column_struct(a) for a in b.columns])
+    cb = _abi.dfmi_batch(3, 0, n, carr)
+    progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
+    L = _abi.lib()
+    err = _abi.dfmi_error()
+
+    def step():
+        res = C.c_void_p()
+        rc = L.dfmi_filter_project_host(eng.ctx, pred.handle, progs, 3, C.byref(cb), 0, C.byref(res), C.byref(err))
+        if rc != 0:
+            raise RuntimeError(err.message.decode())
+        v = _abi.dfmi_column()
+        L.dfmi_host_result_column(res, 0, C.byref(v))
+        sel = v.length
+        L.dfmi_host_result_free(res)
+        return sel
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sel = step()
+    el = (time.perf_counter() - t0) / steps
+    moved = n * 24 + sel * 24
+    return {"workload": "C2 query, s=0.5, %d-row HOST batch (dfmi_filter_project_host)" % n,
+            "rows_per_s": n / el, "ms_per_step": el * 1e3, "selected": sel,
+            "pcie_gbs": round(moved / el / 1e9, 1), "bytes_moved_per_step": moved,
+            "note": "host->HBM staging + kernel + HBM->host of the selected rows; not the headline value"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -372,6 +418,9 @@ def main():
     for name in [x for x in args.extra.split(",") if x]:
         if name == "c4":
             extra["c4"] = q6_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS)
+        elif name == "host":
+            if world == 1:
+                extra["host"] = host_line(eng, min(args.steps, 3), 1)
         elif name == "c3":
             extra["c3"] = c3_line(eng, dev, rank, world, args.steps, args.warmup, dist)
         else:

@@ -241,6 +241,7 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
     X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
     if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
     if (const char* bb = getenv("DFMI_BLOCK")) X.BLOCK = atoi(bb);        // diagnostics only
+    if (const char* ww = getenv("DFMI_WAVES_PER_EU")) X.waves_per_eu = atoi(ww);  // diagnostics only
     // look-back / tile-order variants (diagnostics only)
     if (const char* e = getenv("DFMI_LOOKBACK_R")) X.R = std::max(1, std::min(16, atoi(e)));
     if (const char* e = getenv("DFMI_LOOKBACK_SLEEP")) X.sleep = std::max(0, std::min(127, atoi(e)));

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dfmi_program.h"
@@ -69,8 +70,10 @@ size_t values_bytes(const dfmi_column& c) {
 struct Arena {
     uint8_t* dev = nullptr;
     size_t dev_cap = 0, dev_used = 0;
-    uint8_t* pin = nullptr;
+    uint8_t* pin = nullptr;  // two staging chunks
     size_t pin_cap = 0;
+    hipEvent_t drained[2] = {nullptr, nullptr};
+    bool in_flight[2] = {false, false};
     void reserve(size_t need) {
         if (need <= dev_cap) return;
         if (dev) (void)hipFree(dev);
@@ -95,22 +98,75 @@ Arena& arena_of(const dfmi_context* c) {
     return *g_arenas.back().second;
 }
 
-// H2D of one host buffer through pinned staging (pageable hipMemcpy would be
-// staged by the runtime anyway; chunks keep the pinned footprint bounded).
+// Host copy split over a few threads: one core's memcpy (~10-20 GB/s) would
+// bound the staging below what PCIe Gen5 moves.
+void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n) {
+    constexpr size_t kMinPiece = (size_t)4 << 20;
+    const int nt = (int)std::min<size_t>(8, std::max<size_t>(1, n / kMinPiece));
+    if (nt == 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t piece = (n + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; ++i) {
+        const size_t o = i * piece;
+        if (o < n) th.emplace_back([=] { memcpy(dst + o, src + o, std::min(piece, n - o)); });
+    }
+    memcpy(dst, src, std::min(piece, n));
+    for (auto& t : th) t.join();
+}
+
+// H2D of one host buffer through two pinned staging chunks: the host fills
+// one chunk while the DMA engine drains the other (chunks keep the pinned
+// footprint bounded; pageable hipMemcpy would be staged by the runtime
+// anyway, serially).
 void h2d(Arena& A, hipStream_t st, void* dst, const void* src, size_t n) {
     if (!n) return;
-    const size_t chunk = (size_t)64 << 20;
+    constexpr size_t chunk = (size_t)64 << 20;
     if (!A.pin) {
-        HIP_TRY(hipHostMalloc((void**)&A.pin, chunk, hipHostMallocDefault));
-        A.pin_cap = chunk;
+        HIP_TRY(hipHostMalloc((void**)&A.pin, 2 * chunk, hipHostMallocDefault));
+        A.pin_cap = 2 * chunk;
+        for (auto& e : A.drained) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    for (size_t off = 0; off < n; off += chunk) {
+    int b = 0;
+    for (size_t off = 0; off < n; off += chunk, b ^= 1) {
         const size_t m = std::min(chunk, n - off);
-        HIP_TRY(hipStreamSynchronize(st));  // staging buffer free again
-        memcpy(A.pin, (const uint8_t*)src + off, m);
-        HIP_TRY(hipMemcpyAsync((uint8_t*)dst + off, A.pin, m, hipMemcpyHostToDevice, st));
+        uint8_t* buf = A.pin + b * chunk;
+        if (A.in_flight[b]) HIP_TRY(hipEventSynchronize(A.drained[b]));  // chunk b free again
+        par_memcpy(buf, (const uint8_t*)src + off, m);
+        HIP_TRY(hipMemcpyAsync((uint8_t*)dst + off, buf, m, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(A.drained[b], st));
+        A.in_flight[b] = true;
     }
     HIP_TRY(hipStreamSynchronize(st));
+    A.in_flight[0] = A.in_flight[1] = false;
+}
+
+// D2H of one device buffer through the same two pinned chunks: the DMA of
+// chunk i+1 overlaps the host copy-out of chunk i.
+void d2h(Arena& A, hipStream_t st, void* dst, const void* src, size_t n) {
+    if (!n) return;
+    constexpr size_t chunk = (size_t)64 << 20;
+    if (!A.pin) {
+        HIP_TRY(hipHostMalloc((void**)&A.pin, 2 * chunk, hipHostMallocDefault));
+        A.pin_cap = 2 * chunk;
+        for (auto& e : A.drained) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const size_t nchunks = (n + chunk - 1) / chunk;
+    auto issue = [&](size_t i) {
+        const size_t off = i * chunk, m = std::min(chunk, n - off);
+        HIP_TRY(hipMemcpyAsync(A.pin + (i & 1) * chunk, (const uint8_t*)src + off, m, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipEventRecord(A.drained[i & 1], st));
+    };
+    issue(0);
+    if (nchunks > 1) issue(1);
+    for (size_t i = 0; i < nchunks; ++i) {
+        const size_t off = i * chunk, m = std::min(chunk, n - off);
+        HIP_TRY(hipEventSynchronize(A.drained[i & 1]));
+        par_memcpy((uint8_t*)dst + off, A.pin + (i & 1) * chunk, m);
+        if (i + 2 < nchunks) issue(i + 2);
+    }
 }
 
 void set_err(dfmi_error* err, int32_t code, const std::string& m) {
@@ -128,6 +184,8 @@ void host_arena_release(const dfmi_context* c) {
         Arena* a = g_arenas[i].second;
         if (a->dev) (void)hipFree(a->dev);
         if (a->pin) (void)hipHostFree(a->pin);
+        for (auto e : a->drained)
+            if (e) (void)hipEventDestroy(e);
         delete a;
         g_arenas.erase(g_arenas.begin() + i);
         return;
@@ -255,12 +313,12 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
                 rc_.offsets.resize((size_t)L + 1);
                 HIP_TRY(hipMemcpyAsync(rc_.offsets.data(), r.offsets, (size_t)(L + 1) * 4, hipMemcpyDeviceToHost, st));
                 rc_.values.resize((size_t)r.data_length);
-                if (r.data_length)
-                    HIP_TRY(hipMemcpyAsync(rc_.values.data(), r.data, (size_t)r.data_length, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                d2h(A, st, rc_.values.data(), r.data, (size_t)r.data_length);
             } else {
                 const size_t vb = r.type == DFMI_TYPE_BOOLEAN ? (size_t)(L + 7) / 8 : (size_t)L * width_of(r.type);
                 rc_.values.resize(vb);
-                if (vb) HIP_TRY(hipMemcpyAsync(rc_.values.data(), r.values, vb, hipMemcpyDeviceToHost, st));
+                d2h(A, st, rc_.values.data(), r.values, vb);
             }
             if (r.null_count > 0) {
                 rc_.validity.resize((size_t)(L + 7) / 8);

@@ -324,7 +324,9 @@ std::string generate(const Plan& P, Launch& X) {
     std::ostringstream& o = g.o;
     const int K = X.K, BLOCK = X.BLOCK;
     o << "\n// ---- generated query kernel ----\n";
-    o << "extern \"C\" __global__ __launch_bounds__(" << BLOCK << ") void dfmi_query(const dfmi::Args A) {\n";
+    o << "extern \"C\" __global__ __launch_bounds__(" << BLOCK << ")";
+    if (X.waves_per_eu > 0) o << " __attribute__((amdgpu_waves_per_eu(" << X.waves_per_eu << ")))";
+    o << " void dfmi_query(const dfmi::Args A) {\n";
     o << "  constexpr int BLOCK = " << BLOCK << ", K = " << K << ", WAVES = BLOCK / 64;\n";
     o << "  const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);\n";
     if (P.pred) {

@@ -35,6 +35,7 @@ struct Plan {
 // Slot tables + literal pools of one launch.
 struct Launch {
     int K = 8, BLOCK = 512;
+    int waves_per_eu = 0;  // >0: occupancy hint to the register allocator (diagnostics)
     // look-back: R windows of 64 status words per round trip, s_sleep(sleep)
     // between polls, one status word per `spread` words (16 = one per 128-byte
     // line: polling blocks then do not contend on shared lines)
