@@ -15,6 +15,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "dfmi_program.h"
@@ -34,11 +35,32 @@ int ctx_device(const dfmi_context* c);
 hipStream_t ctx_stream(const dfmi_context* c);
 }  // namespace dfmi
 
+// Allocator whose resize() leaves bytes uninitialised: result buffers are
+// overwritten by the D2H copy, and zero-filling GBs first costs as much as
+// the copy itself.
+template <class T>
+struct uninit_alloc : std::allocator<T> {
+    using std::allocator<T>::allocator;
+    template <class U>
+    struct rebind {
+        using other = uninit_alloc<U>;
+    };
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... Args>
+    void construct(U* p, Args&&... a) {
+        ::new ((void*)p) U(std::forward<Args>(a)...);
+    }
+};
+
 struct dfmi_host_result {
     struct Col {
         int32_t type = 0;
         int64_t length = 0, null_count = 0;
-        std::vector<uint8_t> values, validity;
+        std::vector<uint8_t, uninit_alloc<uint8_t>> values;
+        std::vector<uint8_t> validity;
         std::vector<int32_t> offsets;
     };
     std::vector<Col> cols;
