@@ -125,7 +125,9 @@ __device__ __noinline__ u64 sdiv64(u64 x, u64 y) {
     return (u64)(sx / sy);
 }
 
+// Rows past n_rows (the tail tile) read nothing: the callers mask them out.
 __device__ __forceinline__ bool utf8_eq_lit(const Args& A, int u, i64 row, int lit) {
+    if (row >= A.n_rows) return false;
     const int s = A.offs[u][row], e = A.offs[u][row + 1];
     const int len = A.str_len[lit];
     if (e - s != len) return false;
@@ -191,6 +193,7 @@ __device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, i64 base,
 }
 
 __device__ __forceinline__ bool utf8_eq_col(const Args& A, int u, int v, i64 row) {
+    if (row >= A.n_rows) return false;
     const int s0 = A.offs[u][row], e0 = A.offs[u][row + 1];
     const int s1 = A.offs[v][row], e1 = A.offs[v][row + 1];
     if (e0 - s0 != e1 - s1) return false;
@@ -201,7 +204,7 @@ __device__ __forceinline__ bool utf8_eq_col(const Args& A, int u, int v, i64 row
 
 __device__ __forceinline__ bool utf8_valid(const Args& A, int u, i64 row) {
     const u8* v = A.svalid[u];
-    return !v || ((v[row >> 3] >> (row & 7)) & 1);
+    return !v || row >= A.n_rows || ((v[row >> 3] >> (row & 7)) & 1);
 }
 
 __device__ __forceinline__ void st_status(u64* p, u64 v) {
