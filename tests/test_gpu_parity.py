@@ -314,6 +314,28 @@ def test_utf8_many_tiles():
                  DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
+def test_host_batch_many_staging_chunks():
+    """dfmi_filter_project_host over a batch larger than the two 64 MB pinned
+    staging chunks (H2D 20 chunks, D2H 10 per output): identical to the
+    HBM-resident path and to a numpy restatement of the selection."""
+    n = 30_000_000
+    schema = Schema([Field(c, DataType.Float64, False) for c in "abc"])
+    vals = [gen_unit_f64(7, j, 0, n) for j in range(3)]
+    b = RecordBatch(schema, [Array.from_numpy(DataType.Float64, v) for v in vals])
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.2))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.9))))
+    projs = [Column(0), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus, Column(2))]
+    p = compile_scalar_expr(None, pred, schema)
+    cp = [compile_scalar_expr(None, e, schema) for e in projs]
+    host = engine().filter_project_host(p, cp, b)
+    dev = engine().filter_project(p, cp, b)
+    sel = (vals[0] > 0.2) & (vals[1] < 0.9)
+    assert host[0].length == dev[0].length == int(sel.sum())
+    assert np.array_equal(host[0].numpy_values().view(np.uint64), vals[0][sel].view(np.uint64))
+    for h, d in zip(host, dev):
+        assert np.array_equal(h.numpy_values().view(np.uint64), d.numpy_values().view(np.uint64))
+
+
 def test_static_errors_match():
     s, batch = synth(1000)
     cases = [
