@@ -239,6 +239,10 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
     const size_t nload = X.num_cols.size();
     X.BLOCK = 512;
     X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
+    // a predicate over Utf8 columns only reads ~4 B/row of offsets: its tiles
+    // are latency-bound, and 4-wave blocks keep more of them resident
+    // (C3 equality 4.94 -> 4.53 ms)
+    if (pred && X.pred_slots.empty() && !X.utf8_cols.empty()) X.BLOCK = 256;
     if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
     if (const char* bb = getenv("DFMI_BLOCK")) X.BLOCK = atoi(bb);        // diagnostics only
     if (const char* ww = getenv("DFMI_WAVES_PER_EU")) X.waves_per_eu = atoi(ww);  // diagnostics only
