@@ -63,11 +63,9 @@ void set_err(dfmi_error* err, int32_t code, const std::string& m) {
         if (e_ != hipSuccess) throw Fail{DFMI_ERR_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)}; \
     } while (0)
 
-bool is8(int t) { return t == DFMI_TYPE_INT64 || t == DFMI_TYPE_FLOAT64; }
 bool gatherable(int t, uint32_t flags) {
     if (t == DFMI_TYPE_FLOAT64 || t == DFMI_TYPE_UTF8) return true;  // filter.rs:84,94
-    // extension: every fixed-width type (the device lowers the 8-byte ones and
-    // Boolean; others report NotImplemented)
+    // extension: every fixed-width type and Boolean
     if (flags & DFMI_FLAG_EXT_GATHER_ALL) return is_numeric_type(t) || t == DFMI_TYPE_BOOLEAN;
     return false;
 }
@@ -187,12 +185,9 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
             if (ct == DFMI_TYPE_UTF8) {
                 if (!oc.offsets || !oc.data) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 output buffers are NULL"};
                 os.kind = jit::OutSpec::UTF8;
-            } else if (is8(ct) || ct == DFMI_TYPE_BOOLEAN) {
+            } else {
                 if (!oc.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output values pointer is NULL"};
                 os.kind = jit::OutSpec::GATHER;
-            } else {
-                throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
-                           std::string("device path: gather of ") + type_debug(ct) + " columns"};
             }
             os.col = col;
             any_kernel_out = true;
@@ -223,7 +218,7 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
         for (const IrNode& nd : p->ir) {
             if (nd.kind != IR_COL) continue;
             if (nd.type == DFMI_TYPE_UTF8) reg_utf8(nd.col);
-            else if (is8(nd.type) || nd.type == DFMI_TYPE_BOOLEAN) reg_num(nd.col, phase);
+            else if (jit::type_width(nd.type) || nd.type == DFMI_TYPE_BOOLEAN) reg_num(nd.col, phase);
         }
     };
     if (pred) reg_prog(pred, X.pred_slots);
@@ -375,8 +370,9 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             for (size_t s = 0; s < X.num_cols.size(); ++s) {
                 const dfmi_column& c = in->columns[X.num_cols[s]];
                 if (!c.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
-                if (c.type != DFMI_TYPE_BOOLEAN && ((uintptr_t)c.values & 7))
-                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values must be 8-byte aligned"};
+                const int w = jit::type_width(c.type);
+                if (w && ((uintptr_t)c.values & (w - 1)))
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values must be aligned to their width"};
                 A.col[s] = c.values;
                 A.valid[s] = (c.validity && c.null_count > 0) ? c.validity : nullptr;
             }

@@ -49,14 +49,44 @@ const char* math_sym(int op) {
     return s[op - DFMI_OP_PLUS];
 }
 
-bool is8(int t) { return t == DFMI_TYPE_INT64 || t == DFMI_TYPE_FLOAT64; }
+bool is_float(int t) { return t == DFMI_TYPE_FLOAT32 || t == DFMI_TYPE_FLOAT64; }
+bool is_signed_int(int t) { return t >= DFMI_TYPE_INT8 && t <= DFMI_TYPE_INT64; }
+
+// Unsigned type integer math is done in (Rust's wrapping +, -, * on every
+// width; C++ signed overflow is undefined and u16 * u16 would promote to int).
+const char* math_type(int t) { return type_width(t) == 8 ? "u64" : "u32"; }
 
 struct Val {
-    std::string v;  // C++ expression / local: u64 raw bits (numeric) or bool
+    std::string v;  // C++ expression / local of the node's C++ type (ctype), or bool
     std::string n;  // validity expression ("true" when statically valid)
 };
 
 }  // namespace
+
+int type_width(int t) {
+    switch (t) {
+        case DFMI_TYPE_INT8: case DFMI_TYPE_UINT8: return 1;
+        case DFMI_TYPE_INT16: case DFMI_TYPE_UINT16: return 2;
+        case DFMI_TYPE_INT32: case DFMI_TYPE_UINT32: case DFMI_TYPE_FLOAT32: return 4;
+        case DFMI_TYPE_INT64: case DFMI_TYPE_UINT64: case DFMI_TYPE_FLOAT64: return 8;
+        default: return 0;
+    }
+}
+
+const char* ctype(int t) {
+    switch (t) {
+        case DFMI_TYPE_INT8: return "i8";
+        case DFMI_TYPE_INT16: return "i16";
+        case DFMI_TYPE_INT32: return "i32";
+        case DFMI_TYPE_INT64: return "i64";
+        case DFMI_TYPE_UINT8: return "u8";
+        case DFMI_TYPE_UINT16: return "u16";
+        case DFMI_TYPE_UINT32: return "u32";
+        case DFMI_TYPE_FLOAT32: return "float";
+        case DFMI_TYPE_FLOAT64: return "double";
+        default: return "u64";
+    }
+}
 
 // ------------------------------------------------------------- generator
 struct Gen {
@@ -107,21 +137,30 @@ struct Gen {
         return r;
     }
 
+    // Literal slot read as a value of type t (the slot holds the raw bits:
+    // Float32 in the low 32 bits, integers sign/zero-extended).
+    static std::string lit_value(int t, int slot) {
+        const std::string a = "A.lits[" + std::to_string(slot) + "]";
+        if (t == DFMI_TYPE_FLOAT64) return "__builtin_bit_cast(double, " + a + ")";
+        if (t == DFMI_TYPE_FLOAT32) return "__builtin_bit_cast(float, (u32)" + a + ")";
+        return "((" + std::string(ctype(t)) + ")" + a + ")";
+    }
+
     // Emit node i of program p; act = C++ bool expression "row is evaluated".
     Val emit(const dfmi_program* p, int i, int ord_base, const char* act) {
         const IrNode& n = p->ir[i];
         if (n.kind == IR_COL) {
             if (n.type == DFMI_TYPE_UTF8) return Val{"", "true"};  // only inside Utf8 compares
-            if (!is8(n.type) && n.type != DFMI_TYPE_BOOLEAN)
+            if (!type_width(n.type) && n.type != DFMI_TYPE_BOOLEAN)
                 throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
                            std::string("device path: ") + type_debug(n.type) + " column in an expression"};
             return col(n);
         }
         if (n.kind == IR_LIT) {
             if (n.type == DFMI_TYPE_UTF8) return Val{"", "true"};
-            if (!is8(n.type))
+            if (!type_width(n.type))
                 throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("device path: ") + type_debug(n.type) + " literal"};
-            return Val{"A.lits[" + std::to_string(lit(n.bits)) + "]", "true"};
+            return Val{lit_value(n.type, lit(n.bits)), "true"};
         }
         const int ord = ord_base + n.ordinal;
         if (n.rt_code) {
@@ -131,7 +170,8 @@ struct Gen {
                 emit(p, n.r, ord_base, act);
             } catch (const Fail&) {
             }
-            return n.type == DFMI_TYPE_BOOLEAN ? Val{"false", "true"} : Val{"0ull", "true"};
+            if (n.type == DFMI_TYPE_BOOLEAN) return Val{"false", "true"};
+            return Val{"((" + std::string(ctype(n.type)) + ")0)", "true"};
         }
         const int op = n.op;
         const IrNode& L = p->ir[n.l];
@@ -177,16 +217,20 @@ struct Gen {
               << b.v << ");\n";  // null -> zero value bit (append_null)
             return Val{v, nul ? v + "_n" : "true"};
         }
-        const bool f = L.type == DFMI_TYPE_FLOAT64;
+        // same-typed operands (anything else carries rt_code): compare / compute
+        // in the operand type -- iN/uN wrap, Float32 and Float64 round once per
+        // operator (-ffp-contract=off)
+        const int ty = L.type;
+        const bool f = is_float(ty);
+        const std::string ct = ctype(ty);
         const std::string v = t();
         if (op <= DFMI_OP_GT_EQ) {
-            const std::string x = f ? "dfmi::f64(" + a.v + ")" : "(i64)(" + a.v + ")";
-            const std::string y = f ? "dfmi::f64(" + b.v + ")" : "(i64)(" + b.v + ")";
+            const std::string cmp = "(" + a.v + ") " + cmp_sym(op) + " (" + b.v + ")";
             if (nul) {
-                o << "    const bool " << v << " = dfmi::cmp_opt<" << op << ">(" << a.n << ", " << b.n << ", " << x << " "
-                  << cmp_sym(op) << " " << y << ");\n";
+                o << "    const bool " << v << " = dfmi::cmp_opt<" << op << ">(" << a.n << ", " << b.n << ", " << cmp
+                  << ");\n";
             } else {
-                o << "    const bool " << v << " = " << x << " " << cmp_sym(op) << " " << y << ";\n";
+                o << "    const bool " << v << " = " << cmp << ";\n";
             }
             return Val{v, "true"};
         }
@@ -195,26 +239,25 @@ struct Gen {
         if (nul) o << "    const bool " << v << "_n = " << nn << ";\n";
         const std::string valid = nul ? v + "_n" : "true";
         if (op == DFMI_OP_DIVIDE) {
-            if (f) {
-                o << "    if ((" << act << ") && " << valid << " && dfmi::f64(" << b.v
-                  << ") == 0.0) dfmi::report_err(A.err, " << ord << ", row, dfmi::ERRK_DIV_ZERO);\n";
-                o << "    u64 " << v << " = dfmi::bits(dfmi::f64(" << a.v << ") / dfmi::f64(" << b.v << "));\n";
-            } else {
-                o << "    if ((" << act << ") && " << valid << ") {\n"
-                  << "      if ((" << b.v << ") == 0ull) dfmi::report_err(A.err, " << ord
-                  << ", row, dfmi::ERRK_DIV_ZERO);\n"
-                  << "      else if ((i64)(" << b.v << ") == -1 && (" << a.v
-                  << ") == 0x8000000000000000ull) dfmi::report_err(A.err, " << ord << ", row, dfmi::ERRK_DIV_OVERFLOW);\n"
-                  << "    }\n";
-                o << "    u64 " << v << " = dfmi::sdiv64(" << a.v << ", " << b.v << ");\n";
-            }
+            o << "    if ((" << act << ") && " << valid << ") {\n"
+              << "      if ((" << b.v << ") == (" << ct << ")0) dfmi::report_err(A.err, " << ord
+              << ", row, dfmi::ERRK_DIV_ZERO);\n";
+            if (is_signed_int(ty))
+                o << "      else if ((" << b.v << ") == (" << ct << ")-1 && (" << a.v << ") == dfmi::int_min<" << ct
+                  << ">()) dfmi::report_err(A.err, " << ord << ", row, dfmi::ERRK_DIV_OVERFLOW);\n";
+            o << "    }\n";
+            if (f)
+                o << "    " << ct << " " << v << " = (" << a.v << ") / (" << b.v << ");\n";
+            else
+                o << "    " << ct << " " << v << " = dfmi::idiv<" << ct << ">(" << a.v << ", " << b.v << ");\n";
         } else if (f) {
-            o << "    u64 " << v << " = dfmi::bits(dfmi::f64(" << a.v << ") " << math_sym(op) << " dfmi::f64(" << b.v
-              << "));\n";
+            o << "    " << ct << " " << v << " = (" << a.v << ") " << math_sym(op) << " (" << b.v << ");\n";
         } else {
-            o << "    u64 " << v << " = (" << a.v << ") " << math_sym(op) << " (" << b.v << ");\n";
+            const char* mt = math_type(ty);
+            o << "    " << ct << " " << v << " = (" << ct << ")((" << mt << ")(" << a.v << ") " << math_sym(op) << " ("
+              << mt << ")(" << b.v << "));\n";
         }
-        if (nul) o << "    if (!" << v << "_n) " << v << " = 0ull;\n";
+        if (nul) o << "    if (!" << v << "_n) " << v << " = (" << ct << ")0;\n";
         return Val{v, valid};
     }
 };
@@ -281,7 +324,11 @@ static void emit_decls(std::ostream& o, const std::vector<int>& slots, const Lau
                        bool valid_words) {
     for (int s : slots) {
         const int col = X.num_cols[s];
-        o << "  u64 " << (X.col_type(col) == DFMI_TYPE_BOOLEAN ? "bw" : "c") << s << sfx << "[K];\n";
+        const int ty = X.col_type(col);
+        if (ty == DFMI_TYPE_BOOLEAN)
+            o << "  u64 bw" << s << sfx << "[K];\n";
+        else
+            o << "  " << ctype(ty) << " c" << s << sfx << "[K];\n";
         if (valid_words && X.col_nullable(col)) o << "  u64 vw" << s << sfx << "[K];\n";
     }
 }
@@ -302,13 +349,15 @@ static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Lau
                   << "[k] = dfmi::bitmap_word((const u8*)A.col[" << s << "], (" << base
                   << " >> 6) + k * WAVES + wave, A.n_rows);\n";
             } else {
+                // 64 lanes x width bytes per wave load, contiguous in row order
                 std::string g = guard ? std::string(guard) : "";
                 if (!full) g = g.empty() ? "(" + base + " + k * BLOCK + tid < A.n_rows)"
                                          : "(" + base + " + k * BLOCK + tid < A.n_rows) && " + g;
+                const std::string ct = ctype(X.col_type(col));
                 const std::string ld = (X.nt & 1) ? "__builtin_nontemporal_load(p_ + k * BLOCK)" : "p_[k * BLOCK]";
-                o << "    { const u64* p_ = (const u64*)A.col[" << s << "] + " << base << " + tid;\n"
+                o << "    { const " << ct << "* p_ = (const " << ct << "*)A.col[" << s << "] + " << base << " + tid;\n"
                   << "#pragma unroll\n      for (int k = 0; k < K; ++k) c" << id << "[k] = "
-                  << (g.empty() ? ld + ";" : "(" + g + ") ? " + ld + " : 0ull;") << " }\n";
+                  << (g.empty() ? ld + ";" : "(" + g + ") ? " + ld + " : (" + ct + ")0;") << " }\n";
             }
             if (valid_words && X.col_nullable(col)) {
                 o << "#pragma unroll\n    for (int k = 0; k < K; ++k) vw" << id << "[k] = dfmi::bitmap_word(A.valid[" << s
@@ -394,12 +443,14 @@ std::string generate(const Plan& P, Launch& X) {
                 } else {
                     v = g.emit(os.prog, os.prog->root, os.ord_base, "true");
                 }
+                const std::string ct = ctype(os.out_type);
                 if (os.out_type == DFMI_TYPE_BOOLEAN)
                     o << "    ((u8*)A.out[" << oi << "] + obase)[d] = (" << v.v << ") ? 1 : 0;\n";
                 else if (X.nt & 2)
-                    o << "    __builtin_nontemporal_store((u64)(" << v.v << "), (u64*)A.out[" << oi << "] + obase + d);\n";
+                    o << "    __builtin_nontemporal_store((" << ct << ")(" << v.v << "), (" << ct << "*)A.out[" << oi
+                      << "] + obase + d);\n";
                 else
-                    o << "    ((u64*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
+                    o << "    ((" << ct << "*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
             }
             o << "  }\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
@@ -449,7 +500,7 @@ std::string generate(const Plan& P, Launch& X) {
                   << "      if (lane == 0 && w * 64 < A.n_rows) { ((u64*)A.out[" << oi << "])[w] = vb_;"
                   << " if (A.out_valid[" << oi << "]) ((u64*)A.out_valid[" << oi << "])[w] = nb_; } }\n";
             } else {
-                o << "    if (in) ((u64*)A.out[" << oi << "])[row] = " << v.v << ";\n";
+                o << "    if (in) ((" << ctype(os.out_type) << "*)A.out[" << oi << "])[row] = " << v.v << ";\n";
                 o << "    { const u64 nb_ = __ballot(in && (" << v.n << "));\n"
                   << "      nulls[" << oi << "] += __builtin_popcountll(__ballot(in && !(" << v.n << ")));\n"
                   << "      if (lane == 0 && w * 64 < A.n_rows && A.out_valid[" << oi << "]) ((u64*)A.out_valid[" << oi

@@ -73,6 +73,11 @@ struct Launch {
     }
 };
 
+// Bytes per value of a fixed-width dfmi_type (0 otherwise) and the C++ type
+// the generated code holds it in (i8 .. u64, float, double).
+int type_width(int t);
+const char* ctype(int t);
+
 // Generated source of the plan's kernel (skeleton + body); fills the literal pools.
 std::string generate(const Plan& P, Launch& X);
 // Compiled kernel for the plan (cached per source text and device).

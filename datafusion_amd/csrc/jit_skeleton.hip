@@ -16,6 +16,11 @@
 typedef unsigned long long u64;
 typedef long long i64;
 typedef unsigned char u8;
+typedef signed char i8;
+typedef short i16;
+typedef int i32;
+typedef unsigned short u16;
+typedef unsigned u32;
 
 namespace dfmi {
 
@@ -116,13 +121,22 @@ __device__ __forceinline__ bool cmp_opt(bool lv, bool rv, bool res) {
     else return lv;
 }
 
-// Rust `/` on i64 after arrow's zero check: wraps nothing, MIN / -1 panics
-// (reported by the caller), zero divisors never reach here when valid.
-__device__ __noinline__ u64 sdiv64(u64 x, u64 y) {
-    const i64 sx = (i64)x, sy = (i64)y;
-    if (sy == 0) return 0;
-    if (sy == -1) return 0ull - x;
-    return (u64)(sx / sy);
+// Rust `/` on iN / uN after arrow's zero check: truncating division; MIN / -1
+// panics and a zero divisor is DivideByZero (both reported by the caller, the
+// value here only has to be defined). Out of line: the 64-bit sequence is long.
+template <typename T>
+__device__ __noinline__ T idiv(T x, T y) {
+    if (y == (T)0) return (T)0;
+    if constexpr ((T)-1 < (T)0) {
+        if (y == (T)-1) return (T)(0ull - (u64)(i64)x);  // wrapping negation
+    }
+    return (T)(x / y);
+}
+
+// iN::MIN as a value of T (signed T only).
+template <typename T>
+__device__ __forceinline__ constexpr T int_min() {
+    return (T)((u64)1 << (8 * sizeof(T) - 1));
 }
 
 // Rows past n_rows (the tail tile) read nothing: the callers mask them out.

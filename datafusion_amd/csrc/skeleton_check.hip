@@ -1,6 +1,6 @@
 // Build-time check of jit_skeleton.hip: instantiates every skeleton template
 // with a representative generated body (one Float64 predicate, a gathered
-// column, a Utf8 gather), so a broken skeleton fails `make` rather than the
+// column, a Utf8 gather, integer division at several widths), so a broken skeleton fails `make` rather than the
 // first query compile on the GPU. Not linked into libdfmi.so.
 #include <hip/hip_runtime.h>
 
@@ -39,5 +39,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0) &&
                    dfmi::utf8_eq_col(A, 0, 1, base) && dfmi::utf8_valid(A, 0, base);
     if (b) dfmi::report_err(A.err, 1, base, dfmi::ERRK_DIV_ZERO);
-    if (tid == 0 && dfmi::bitmap_word(A.valid[0], 0, A.n_rows) == 7) A.totals[0] = dfmi::sdiv64(A.lits[1], A.lits[2]);
+    if (tid == 0 && dfmi::bitmap_word(A.valid[0], 0, A.n_rows) == 7)
+        A.totals[0] = (u64)dfmi::idiv<i64>((i64)A.lits[1], (i64)A.lits[2]) +
+                      (u64)dfmi::idiv<i8>((i8)A.lits[1], dfmi::int_min<i8>()) + dfmi::idiv<u16>((u16)A.lits[1], 3);
 }

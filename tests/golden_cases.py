@@ -17,7 +17,7 @@ from datafusion_amd._abi import DFMI_FLAG_EXT_GATHER_ALL
 from datafusion_amd.arrow import Field, Schema
 from datafusion_amd.execution.datasource import CsvDataSource
 from datafusion_amd.logicalplan import (BinaryExpr, Column, DataType, Float64, Int64, Literal, Operator,
-                                        binary_expr_coerced)
+                                        ScalarValue, binary_expr_coerced)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -57,19 +57,51 @@ def smoketest_points(section: int) -> List[tuple]:
     return out[section]
 
 
-def all_types_schema(f64_col: int = None, i64_col: int = None) -> Schema:
-    """all_types_flat.csv with every column Utf8 except the one under test
-    (so the reference's filter() can gather every column)."""
-    fields = []
-    for i in range(12):
-        t = DataType.Utf8
-        if i == f64_col:
-            t = DataType.Float64
-        if i == i64_col:
-            t = DataType.Int64
-        fields.append(Field("c%d" % i, t, False))
-    return Schema(fields)
+def all_types_schema(f64_col: int = None, i64_col: int = None, typed: dict = None) -> Schema:
+    """all_types_flat.csv with every column Utf8 except the ones under test
+    (so the reference's filter() can gather every column). ``typed`` maps a
+    column index to its real type (ALL_TYPES)."""
+    typed = dict(typed or {})
+    if f64_col is not None:
+        typed[f64_col] = DataType.Float64
+    if i64_col is not None:
+        typed[i64_col] = DataType.Int64
+    return Schema([Field("c%d" % i, typed.get(i, DataType.Utf8), False) for i in range(12)])
+
+
+# all_types_flat.csv column types (the original POC's all_types schema: the
+# values of every column fit exactly these types)
+ALL_TYPES = [DataType.Boolean, DataType.UInt8, DataType.UInt16, DataType.UInt32, DataType.UInt64, DataType.Int8,
+             DataType.Int16, DataType.Int32, DataType.Int64, DataType.Float32, DataType.Float64, DataType.Utf8]
+
+# Known answers from test/data/expected/ over all_types_flat.csv whose queries
+# were re-derived here (the POC's tests that produced them are not in the
+# reference tree; each query below reproduces its file row for row):
+# (file, column, operator, literal value) -> SELECT c<col> WHERE c<col> <op> <lit>,
+# the literal typed as the column (no cast).
+ALL_TYPES_NARROW = [
+    ("c_int8_positive.csv", 5, Operator.GtEq, 0), ("c_int8_negative.csv", 5, Operator.Lt, 0),
+    ("c_int8_range_exclusive.csv", 5, Operator.Gt, 100),
+    ("c_int16_positive.csv", 6, Operator.Gt, 0), ("c_int16_negative.csv", 6, Operator.Lt, 0),
+    ("c_int32_positive.csv", 7, Operator.Gt, 0), ("c_int32_negative.csv", 7, Operator.Lt, 0),
+    ("c_float32_high.csv", 9, Operator.Gt, 0.5), ("c_float32_low.csv", 9, Operator.Lt, 0.5),
+]
+
+
+def fixture_values(name: str, t: DataType) -> list:
+    """One-column expected file as Python values of type t."""
+    rows = expected_rows(name)
+    if t in (DataType.Float32, DataType.Float64):
+        return [float(np.float32(r[0])) if t == DataType.Float32 else float(r[0]) for r in rows]
+    return [int(r[0]) for r in rows]
 
 
 def lit_expr(schema, col, op, value):
     return binary_expr_coerced(Column(col), op, Literal(value), schema)
+
+
+def narrow_fixture_case(name, col, op, lit):
+    """(schema, predicate, projections) of an ALL_TYPES_NARROW entry."""
+    t = ALL_TYPES[col]
+    s = all_types_schema(typed={col: t})
+    return s, BinaryExpr(Column(col), op, Literal(ScalarValue(t, lit))), [Column(col)]

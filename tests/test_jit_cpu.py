@@ -127,6 +127,26 @@ def test_utf8_compare_extension_compiles():
     assert rc > 0, msg
 
 
+NARROW = [DataType.Int8, DataType.Int16, DataType.Int32, DataType.UInt8, DataType.UInt16, DataType.UInt32,
+          DataType.UInt64, DataType.Float32]
+
+
+@pytest.mark.parametrize("t", NARROW, ids=[t.name for t in NARROW])
+def test_narrow_type_kernels_compile(t):
+    """Every fixed-width type lowers to typed loads/compares/math/stores."""
+    from datafusion_amd.logicalplan import ScalarValue
+    sch = Schema([Field("x", t, True), Field("y", t, False), Field("z", DataType.Float64, False)])
+    lit = Literal(ScalarValue(t, 2.5 if t == DataType.Float32 else 3))
+    pred = BinaryExpr(BinaryExpr(BinaryExpr(Column(0), Operator.Divide, Column(1)), Operator.Lt, lit), Operator.Or,
+                      BinaryExpr(Column(0), Operator.GtEq, Column(1)))
+    projs = [Column(0), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Minus, lit), Column(2)]
+    rc, code, msg, src = jit_check(sch, pred, projs, _abi.DFMI_FLAG_EXT_GATHER_ALL, compile_=True)
+    assert rc > 0, msg
+    assert "%s c0[K]" % {DataType.Float32: "float"}.get(t, t.name.lower().replace("uint", "u").replace("int", "i")) in src
+    rc, code, msg, src = jit_check(sch, None, projs[1:] + [BinaryExpr(Column(0), Operator.Eq, lit)], compile_=True)
+    assert rc > 0, msg
+
+
 def _rand_expr(rng, depth, boolean=False):
     if boolean:
         if depth == 0 or rng.random() < 0.5:

@@ -9,8 +9,8 @@ from datafusion_amd.execution.error import ExecutionError
 from datafusion_amd.logicalplan import (BinaryExpr, Cast, Column, DataType, Float64, Int64, Literal, Operator,
                                         binary_expr_coerced)
 from datafusion_amd.sqlplanner import SqlToRel
-from golden_cases import (GOLDEN, CITIES, NUMERICS, all_types_schema, expected_rows, load_batch, lit_expr,
-                          smoketest_points)
+from golden_cases import (ALL_TYPES, ALL_TYPES_NARROW, GOLDEN, CITIES, NUMERICS, all_types_schema, expected_rows,
+                          fixture_values, load_batch, lit_expr, narrow_fixture_case, smoketest_points)
 from oracle_ffi import oracle_compile, oracle_filter_project
 
 
@@ -143,6 +143,22 @@ def test_numerics_float32(opname, op):
     exp = expected_rows("numerics_%s.csv" % opname)
     for r, e in enumerate(exp):
         assert got[r] == np.float32(e[3])
+
+
+@pytest.mark.parametrize("case", ALL_TYPES_NARROW, ids=[c[0] for c in ALL_TYPES_NARROW])
+def test_all_types_narrow(case):
+    """expected/c_int{8,16,32}_*.csv, c_float32_{high,low}.csv: comparisons of
+    Int8/Int16/Int32/Float32 columns of all_types_flat.csv (same-typed literal,
+    comparison_ops! expression.rs:174-203). Gathering them needs the
+    extension flag (filter.rs:106-110 rejects every type but Float64/Utf8)."""
+    name, col, op, lit = case
+    s, pred, projs = narrow_fixture_case(*case)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    with pytest.raises(ExecutionError) as e:
+        oracle_filter_project(s, batch, pred, projs)
+    assert e.value.message == "filter not supported for %r" % ALL_TYPES[col]
+    out = oracle_filter_project(s, batch, pred, projs, DFMI_FLAG_EXT_GATHER_ALL)
+    assert out[0][1].to_pylist() == fixture_values(name, ALL_TYPES[col])
 
 
 def test_projection_unit_test():
