@@ -28,6 +28,8 @@ DFMI_ERR_DEVICE = 10
 
 DFMI_FLAG_EXT_GATHER_ALL = 0x1
 DFMI_FLAG_EXT_UTF8_COMPARE = 0x2
+DFMI_FLAG_EXT_CAST = 0x4
+DFMI_FLAG_EXT_IS_NULL = 0x8
 
 STATUS_NAMES = {
     DFMI_ERR_EXECUTION: "ExecutionError",

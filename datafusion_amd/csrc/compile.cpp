@@ -235,6 +235,19 @@ int compile_node(const Builder& b, int t, const dfmi_schema& s, uint32_t flags, 
         case DFMI_EXPR_CAST: {  // expression.rs:277-325
             const int inner = kids[0];
             const dfmi_expr_node& in = b.nodes[b.trees[inner].node];
+            if ((flags & DFMI_FLAG_EXT_CAST) && in.kind != DFMI_EXPR_LITERAL) {
+                // extension: CAST of a column / expression (expression.rs:281-290)
+                const int c = compile_node(b, inner, s, flags, p);
+                const int from = p.ir[c].type;
+                if (!is_numeric_type(from) || !is_numeric_type(n.data_type))
+                    throw CompileError{DFMI_ERR_NOT_IMPLEMENTED, std::string("CAST from ") + type_debug(from) +
+                                                                     " to " + type_debug(n.data_type)};
+                ir.kind = IR_CAST;
+                ir.type = n.data_type;
+                ir.l = c;
+                ir.name = expr_debug(b, t);
+                break;
+            }
             if (in.kind == DFMI_EXPR_COLUMN) throw CompileError{DFMI_ERR_EXECUTION, "column reference"};
             if (in.kind == DFMI_EXPR_LITERAL) {
                 if (in.data_type == DFMI_TYPE_INT64) {
@@ -287,6 +300,16 @@ int compile_node(const Builder& b, int t, const dfmi_schema& s, uint32_t flags, 
             }
             break;
         }
+        case DFMI_EXPR_IS_NULL: case DFMI_EXPR_IS_NOT_NULL:
+            if (flags & DFMI_FLAG_EXT_IS_NULL) {  // extension: expression.rs:326-345
+                ir.kind = IR_ISNULL;
+                ir.op = n.kind == DFMI_EXPR_IS_NULL ? 0 : 1;
+                ir.type = DFMI_TYPE_BOOLEAN;
+                ir.l = compile_node(b, kids[0], s, flags, p);
+                ir.name = expr_debug(b, t);
+                break;
+            }
+            throw CompileError{DFMI_ERR_EXECUTION, "expression " + expr_debug(b, t)};
         default:
             throw CompileError{DFMI_ERR_EXECUTION, "expression " + expr_debug(b, t)};
     }

@@ -9,14 +9,17 @@
 
 namespace dfmi {
 
-enum IrKind { IR_COL = 1, IR_LIT = 2, IR_BIN = 3 };
+// IR_CAST (DFMI_FLAG_EXT_CAST): child l converted to `type` with the arrow
+// cast kernel's rules; IR_ISNULL (DFMI_FLAG_EXT_IS_NULL): op 0 = IS NULL,
+// 1 = IS NOT NULL of child l.
+enum IrKind { IR_COL = 1, IR_LIT = 2, IR_BIN = 3, IR_CAST = 4, IR_ISNULL = 5 };
 
 struct IrNode {
     int kind = 0;
     int type = 0;        // result dfmi_type
-    int op = 0;          // IR_BIN: dfmi_operator
+    int op = 0;          // IR_BIN: dfmi_operator; IR_ISNULL: 0 / 1
     int col = -1;        // IR_COL
-    int l = -1, r = -1;  // IR_BIN children (IR indices)
+    int l = -1, r = -1;  // IR_BIN children, IR_CAST / IR_ISNULL child (IR indices)
     uint64_t bits = 0;   // IR_LIT numeric payload (raw 64-bit, Float32 widened bits)
     std::string str;     // IR_LIT Utf8 payload
     std::string name;    // RuntimeExpr name of this sub-expression

@@ -198,6 +198,9 @@ void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int3
         os.kind = jit::OutSpec::EXPR;
         os.prog = p;
         os.ord_base = proj_base[o];
+        os.nullable = pred && jit::may_introduce_nulls(p);
+        if (os.nullable && !oc.validity)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output validity pointer is NULL (the projection can produce nulls)"};
         any_kernel_out = true;
     }
 
@@ -357,14 +360,20 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             }
             const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
             const size_t status_bytes = (size_t)n_chan * n_tiles * 8 * X.spread;
-            std::vector<int> bool_out;
-            for (int o = 0; o < nout; ++o)
-                if (pred && plan.outs[o].kind != jit::OutSpec::SKIP && plan.outs[o].kind != jit::OutSpec::UTF8 &&
-                    plan.outs[o].out_type == DFMI_TYPE_BOOLEAN)
-                    bool_out.push_back(o);
+            // filtered outputs written as one byte per row and packed into a
+            // bitmap after the kernel: Boolean values, and the validity of
+            // projections that can produce nulls (fallible CAST)
+            std::vector<int> bool_out, valid_out;
+            for (int o = 0; o < nout; ++o) {
+                if (!pred || plan.outs[o].kind == jit::OutSpec::SKIP || plan.outs[o].kind == jit::OutSpec::UTF8)
+                    continue;
+                if (plan.outs[o].out_type == DFMI_TYPE_BOOLEAN) bool_out.push_back(o);
+                if (plan.outs[o].nullable) valid_out.push_back(o);
+            }
+            const size_t row_bytes = (size_t)((n + 63) & ~63ll);
             ensure(ctx, &ctx->ws, &ctx->ws_bytes, kHdrAlloc + status_bytes);
-            if (!bool_out.empty())
-                ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, bool_out.size() * (size_t)((n + 63) & ~63ll));
+            if (!bool_out.empty() || !valid_out.empty())
+                ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, (bool_out.size() + valid_out.size()) * row_bytes);
             A.n_rows = n;
             A.n_tiles = (int)n_tiles;
             for (size_t s = 0; s < X.num_cols.size(); ++s) {
@@ -393,8 +402,10 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             }
             for (size_t i = 0; i < bool_out.size(); ++i) {
                 bool_dst[bool_out[i]] = (uint8_t*)outs[bool_out[i]].values;
-                A.out[bool_out[i]] = ctx->scratch + i * (size_t)((n + 63) & ~63ll);
+                A.out[bool_out[i]] = ctx->scratch + i * row_bytes;
             }
+            for (size_t i = 0; i < valid_out.size(); ++i)
+                A.out_valid[valid_out[i]] = ctx->scratch + (bool_out.size() + i) * row_bytes;
             memcpy(A.lits, X.args_lits, sizeof A.lits);
             memcpy(A.str_off, X.str_off, sizeof A.str_off);
             memcpy(A.str_len, X.str_len, sizeof A.str_len);
@@ -415,6 +426,8 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             HIP_TRY(hipEventRecord(ctx->ev1, st));
             for (int o = 0; o < nout; ++o)
                 if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
+            for (int o : valid_out)
+                HIP_TRY(launch_pack_bools(A.out_valid[o], outs[o].validity, A.totals, n, st));
             HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ctx->ws, kHdrAlloc, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipEventRecord(ctx->ev2, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -457,7 +470,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             dfmi_out_column& oc = outs[o];
             if (oc.passthrough_column >= 0) continue;
             oc.length = out_rows;
-            oc.null_count = pred ? 0 : (int64_t)totals[8 + o];
+            oc.null_count = (!pred || plan.outs[o].nullable) ? (int64_t)totals[8 + o] : 0;
             if (plan.outs[o].kind == jit::OutSpec::UTF8) {
                 oc.data_length = 0;
                 for (size_t j = 0; j < X.utf8_outs.size(); ++j)

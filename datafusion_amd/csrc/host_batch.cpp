@@ -266,7 +266,7 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
             } else {
                 need += align256(t == DFMI_TYPE_BOOLEAN ? bitmap_bytes(n) : (size_t)n * std::max(width_of(t), 1));
             }
-            if (!pred) need += align256(bitmap_bytes(n));
+            if (t != DFMI_TYPE_UTF8) need += align256(bitmap_bytes(n));
         }
         A.dev_used = 0;
         A.reserve(need);
@@ -305,7 +305,7 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
             } else {
                 oc[o].values = A.take(t == DFMI_TYPE_BOOLEAN ? bitmap_bytes(n) : (size_t)n * std::max(width_of(t), 1));
             }
-            if (!pred) oc[o].validity = A.take(bitmap_bytes(n));
+            if (t != DFMI_TYPE_UTF8) oc[o].validity = A.take(bitmap_bytes(n));
         }
 
         const int32_t rc = dfmi_filter_project(ctx, pred, projs, np, &db, oc.data(), flags, err);

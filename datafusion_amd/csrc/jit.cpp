@@ -52,6 +52,16 @@ const char* math_sym(int op) {
 bool is_float(int t) { return t == DFMI_TYPE_FLOAT32 || t == DFMI_TYPE_FLOAT64; }
 bool is_signed_int(int t) { return t >= DFMI_TYPE_INT8 && t <= DFMI_TYPE_INT64; }
 
+// Casts num::cast can never reject: int -> float, Float32 -> Float64, and an
+// integer into a type holding all of its values.
+bool cast_total(int from, int to) {
+    if (is_float(to)) return !is_float(from) || type_width(from) <= type_width(to);
+    if (is_float(from)) return false;
+    const int wf = type_width(from), wt = type_width(to);
+    if (is_signed_int(from) == is_signed_int(to)) return wt >= wf;
+    return !is_signed_int(from) && wt > wf;  // unsigned into a wider signed type
+}
+
 // Unsigned type integer math is done in (Rust's wrapping +, -, * on every
 // width; C++ signed overflow is undefined and u16 * u16 would promote to int).
 const char* math_type(int t) { return type_width(t) == 8 ? "u64" : "u32"; }
@@ -71,6 +81,12 @@ int type_width(int t) {
         case DFMI_TYPE_INT64: case DFMI_TYPE_UINT64: case DFMI_TYPE_FLOAT64: return 8;
         default: return 0;
     }
+}
+
+bool may_introduce_nulls(const dfmi_program* p) {
+    for (const IrNode& n : p->ir)
+        if (n.kind == IR_CAST && !cast_total(p->ir[n.l].type, n.type)) return true;
+    return false;
 }
 
 const char* ctype(int t) {
@@ -150,7 +166,10 @@ struct Gen {
     Val emit(const dfmi_program* p, int i, int ord_base, const char* act) {
         const IrNode& n = p->ir[i];
         if (n.kind == IR_COL) {
-            if (n.type == DFMI_TYPE_UTF8) return Val{"", "true"};  // only inside Utf8 compares
+            if (n.type == DFMI_TYPE_UTF8) {  // value only inside Utf8 compares; validity for IS NULL
+                if (filtered_cols || !X.col_nullable(n.col)) return Val{"", "true"};
+                return Val{"", "dfmi::utf8_valid(A, " + std::to_string(X.slot_of_utf8(n.col)) + ", row)"};
+            }
             if (!type_width(n.type) && n.type != DFMI_TYPE_BOOLEAN)
                 throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
                            std::string("device path: ") + type_debug(n.type) + " column in an expression"};
@@ -161,6 +180,29 @@ struct Gen {
             if (!type_width(n.type))
                 throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("device path: ") + type_debug(n.type) + " literal"};
             return Val{lit_value(n.type, lit(n.bits)), "true"};
+        }
+        if (n.kind == IR_ISNULL) {  // extension: the operand's validity, never null
+            const Val a = emit(p, n.l, ord_base, act);
+            if (a.n == "true") return Val{n.op == 0 ? "false" : "true", "true"};
+            const std::string v = t();
+            o << "    const bool " << v << " = " << (n.op == 0 ? "!" : "") << "(" << a.n << ");\n";
+            return Val{v, "true"};
+        }
+        if (n.kind == IR_CAST) {  // extension: arrow cast kernel, unfit values -> null
+            const Val a = emit(p, n.l, ord_base, act);
+            const int from = p->ir[n.l].type, to = n.type;
+            if (from == to) return a;
+            const std::string v = t();
+            o << "    " << ctype(to) << " " << v << ";\n";
+            if (cast_total(from, to)) {
+                o << "    (void)dfmi::num_cast<" << ctype(to) << ">(" << a.v << ", " << v << ");\n";
+                if (a.n != "true") o << "    if (!(" << a.n << ")) " << v << " = (" << ctype(to) << ")0;\n";
+                return Val{v, a.n};
+            }
+            o << "    const bool " << v << "_n = dfmi::num_cast<" << ctype(to) << ">(" << a.v << ", " << v << ")"
+              << (a.n != "true" ? " && (" + a.n + ")" : "") << ";\n";
+            o << "    if (!" << v << "_n) " << v << " = (" << ctype(to) << ")0;\n";
+            return Val{v, v + "_n"};
         }
         const int ord = ord_base + n.ordinal;
         if (n.rt_code) {
@@ -428,6 +470,8 @@ std::string generate(const Plan& P, Launch& X) {
               << ".excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
             // projections over the selected rows (filtered batch: no validity)
             g.filtered_cols = true;
+            for (size_t oi = 0; oi < P.outs.size(); ++oi)
+                if (P.outs[oi].nullable) o << "  unsigned nn" << oi << " = 0;\n";
             o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
               << "    const i64 row = base + k * BLOCK + tid;\n    const unsigned d = dst[k];\n";
             for (size_t oi = 0; oi < P.outs.size(); ++oi) {
@@ -444,6 +488,9 @@ std::string generate(const Plan& P, Launch& X) {
                     v = g.emit(os.prog, os.prog->root, os.ord_base, "true");
                 }
                 const std::string ct = ctype(os.out_type);
+                if (os.nullable)  // compacted validity as bytes (packed after the kernel)
+                    o << "    { const bool v_ = " << v.n << "; ((u8*)A.out_valid[" << oi << "] + obase)[d] = v_ ? 1 : 0;"
+                      << " nn" << oi << " += v_ ? 0u : 1u; }\n";
                 if (os.out_type == DFMI_TYPE_BOOLEAN)
                     o << "    ((u8*)A.out[" << oi << "] + obase)[d] = (" << v.v << ") ? 1 : 0;\n";
                 else if (X.nt & 2)
@@ -453,6 +500,10 @@ std::string generate(const Plan& P, Launch& X) {
                     o << "    ((" << ct << "*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
             }
             o << "  }\n";
+            for (size_t oi = 0; oi < P.outs.size(); ++oi)
+                if (P.outs[oi].nullable)
+                    o << "  { const u64 s_ = dfmi::wave_sum((u64)nn" << oi << "); if (lane == 0 && s_) atomicAdd(&A.totals[8 + "
+                      << oi << "], s_); }\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
                 o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << X.utf8_outs[j].second
                   << ", " << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";

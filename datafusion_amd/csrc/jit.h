@@ -25,6 +25,9 @@ struct OutSpec {
     const dfmi_program* prog = nullptr;  // EXPR
     int ord_base = 0;                  // evaluation-order base of prog's nodes
     int out_type = 0;
+    // EXPR after a Selection whose value can be null although the filtered
+    // batch has none (a CAST that rejects a value): validity bytes + count
+    bool nullable = false;
 };
 
 struct Plan {
@@ -77,6 +80,10 @@ struct Launch {
 // the generated code holds it in (i8 .. u64, float, double).
 int type_width(int t);
 const char* ctype(int t);
+
+// True when evaluating p over a batch without nulls can still produce a null
+// (a CAST num::cast can reject, DFMI_FLAG_EXT_CAST).
+bool may_introduce_nulls(const dfmi_program* p);
 
 // Generated source of the plan's kernel (skeleton + body); fills the literal pools.
 std::string generate(const Plan& P, Launch& X);

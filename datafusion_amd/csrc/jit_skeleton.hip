@@ -139,6 +139,50 @@ __device__ __forceinline__ constexpr T int_min() {
     return (T)((u64)1 << (8 * sizeof(T) - 1));
 }
 
+// CAST extension (DFMI_FLAG_EXT_CAST): the arrow 0.12 cast kernel's
+// num::cast::<From, To>(x) -- false (None -> a null) when x does not fit To:
+//   int -> int: x outside To's range; float -> int: NaN or trunc(x) outside
+//   the range; f64 -> f32: finite and outside [-FLT_MAX, FLT_MAX].
+// int -> float and widening float casts always succeed (`as`, round to nearest).
+template <typename To, typename From>
+__device__ __forceinline__ bool num_cast(From x, To& out) {
+    constexpr bool from_int = (From)0.5 == (From)0, to_int = (To)0.5 == (To)0;
+    constexpr bool from_signed = (From)-1 < (From)0, to_signed = (To)-1 < (To)0;
+    constexpr u64 tmax = ~0ull >> (64 - 8 * (int)sizeof(To) + (to_signed ? 1 : 0));
+    if constexpr (from_int && to_int) {
+        bool ok;
+        if constexpr (from_signed)
+            ok = x >= (From)0 ? (u64)x <= tmax : (to_signed && (i64)x >= -(i64)tmax - 1);
+        else
+            ok = (u64)x <= tmax;
+        out = (To)x;
+        return ok;
+    } else if constexpr (from_int) {
+        out = (To)x;
+        return true;
+    } else if constexpr (to_int) {
+        const double d = (double)x;
+        const double t = __builtin_trunc(d);
+        bool ok;
+        if constexpr (sizeof(To) == 8)
+            ok = to_signed ? (t >= -0x1p63 && t < 0x1p63) : (t >= 0.0 && t < 0x1p64);
+        else
+            ok = t >= (to_signed ? -(double)tmax - 1.0 : 0.0) && t <= (double)tmax;  // false for NaN
+        out = ok ? (To)t : (To)0;
+        return ok;
+    } else {
+        if constexpr (sizeof(From) > sizeof(To)) {
+            const double d = (double)x;
+            if (__builtin_isfinite(d) && (d < -0x1.fffffep127 || d > 0x1.fffffep127)) {
+                out = (To)0;
+                return false;
+            }
+        }
+        out = (To)x;
+        return true;
+    }
+}
+
 // Rows past n_rows (the tail tile) read nothing: the callers mask them out.
 __device__ __forceinline__ bool utf8_eq_lit(const Args& A, int u, i64 row, int lit) {
     if (row >= A.n_rows) return false;

@@ -124,7 +124,9 @@ class DeviceEngine:
             cap = 0
             if t == DataType.Utf8 and src_cols[o] is not None:
                 cap = cols[src_cols[o]].values.numel()
-            oc, keep = self._alloc_out(t, n, predicate is None, cap)
+            # validity: always without a predicate; after one, a projection
+            # with a fallible CAST can still produce nulls
+            oc, keep = self._alloc_out(t, n, t != DataType.Utf8, cap)
             outs[o] = oc
             keeps.append(keep)
 

@@ -156,6 +156,17 @@ typedef struct dfmi_expr_node {
                                            instead of "filter not supported for ..." */
 #define DFMI_FLAG_EXT_UTF8_COMPARE 0x2u /* Utf8 literals and Utf8 =/!= comparisons
                                            instead of "No support for literal type" */
+#define DFMI_FLAG_EXT_CAST         0x4u /* CAST(<numeric expression> AS <numeric type>)
+                                           instead of "column reference" / "CAST not
+                                           implemented for expression" (expression.rs:281-290,
+                                           321-324): arrow 0.12 cast kernel rules -- a null
+                                           stays null, a value the target type cannot hold
+                                           (num::cast -> None: out of range, NaN to an
+                                           integer) becomes null. Literal casts stay exactly
+                                           the reference's (Int64 -> Float64 only). */
+#define DFMI_FLAG_EXT_IS_NULL      0x8u /* IsNull / IsNotNull (expression.rs:326-345,
+                                           commented out in the reference): the operand's
+                                           validity as a non-null Boolean */
 
 /* Opaque compiled expression: the RuntimeExpr::Compiled of expression.rs:43-50. */
 typedef struct dfmi_program dfmi_program;
@@ -188,7 +199,10 @@ int32_t dfmi_context_set_stream(dfmi_context* ctx, void* hip_stream);
 
 /* Output column. The caller provides device buffers sized for the worst case:
  *   values:   num_rows * width bytes (Boolean: ceil(num_rows/8), 8-padded);
- *   validity: ceil(num_rows/8) bytes, 8-padded (only written without a predicate);
+ *   validity: ceil(num_rows/8) bytes, 8-padded; written when the result can
+ *             hold nulls (always without a predicate; after a Selection only
+ *             for a projection with a fallible CAST, DFMI_FLAG_EXT_CAST) --
+ *             null_count > 0 says it holds the result's validity;
  *   offsets:  (num_rows+1) int32 for Utf8;
  *   data:     Utf8 bytes, data_capacity >= input column's byte length.
  * The library fills the fields below the line. */

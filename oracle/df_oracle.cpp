@@ -460,6 +460,80 @@ ArrayRef bool_and_or(int op, const Array& l, const Array& r) {  // array_ops::{a
     return b.finish();
 }
 
+// ------------------------------------------ cast kernel (extension) ---
+// DFMI_FLAG_EXT_CAST: the arrow 0.12 cast kernel for primitive arrays
+// (compute::cast -> numeric_cast: a null stays null; each value goes through
+// num::cast::<From, To>, and None -- the value does not fit the target type --
+// appends a null). num-traits 0.2 NumCast rules restated:
+//   int -> int      Some iff the value is in To's range;
+//   int -> float    Some(x as To) (round to nearest even);
+//   float -> int    Some(trunc(x)) iff x is not NaN and trunc(x) is in range;
+//   f32 -> f64      Some (exact); f64 -> f32: None iff x is finite and outside
+//                   [f32::MIN, f32::MAX], else Some(x as f32).
+// Parity unpinned beyond the values the c_*_cast fixtures hold.
+template <typename From, typename To>
+bool num_cast(From x, To* out) {
+    if constexpr (std::is_integral<From>::value && std::is_integral<To>::value) {
+        using L = std::numeric_limits<To>;
+        bool ok;
+        if constexpr (std::is_signed<From>::value) {
+            ok = x >= 0 ? (uint64_t)x <= (uint64_t)L::max() : (std::is_signed<To>::value && (int64_t)x >= (int64_t)L::min());
+        } else {
+            ok = (uint64_t)x <= (uint64_t)L::max();
+        }
+        if (ok) *out = (To)x;
+        return ok;
+    } else if constexpr (std::is_integral<From>::value) {
+        *out = (To)x;
+        return true;
+    } else if constexpr (std::is_integral<To>::value) {
+        const double d = (double)x;
+        if (std::isnan(d)) return false;
+        const double t = std::trunc(d);
+        bool ok;
+        if constexpr (sizeof(To) == 8) {
+            ok = std::is_signed<To>::value ? (t >= -0x1p63 && t < 0x1p63) : (t >= 0.0 && t < 0x1p64);
+        } else {
+            ok = t >= (double)std::numeric_limits<To>::min() && t <= (double)std::numeric_limits<To>::max();
+        }
+        if (ok) *out = (To)t;
+        return ok;
+    } else {
+        if (sizeof(From) > sizeof(To) && std::isfinite((double)x) &&
+            ((double)x < -(double)std::numeric_limits<float>::max() || (double)x > (double)std::numeric_limits<float>::max()))
+            return false;
+        *out = (To)x;
+        return true;
+    }
+}
+
+ArrayRef cast_array(const Array& a, int to) {
+    ArrayRef out;
+    dispatch_numeric(a.type, [&](auto ftag) {
+        using F = decltype(ftag);
+        dispatch_numeric(to, [&](auto ttag) {
+            using T = decltype(ttag);
+            PrimBuilder<T> b(a.len);
+            for (int64_t i = 0; i < a.len; ++i) {
+                T v;
+                if (!a.is_null(i) && num_cast<F, T>(a.value<F>(i), &v))
+                    b.push(v);
+                else
+                    b.push_null();
+            }
+            out = b.finish(to);
+        });
+    });
+    return out;
+}
+
+// DFMI_FLAG_EXT_IS_NULL: Array::is_null / is_not_null -> non-null Boolean.
+ArrayRef is_null_array(const Array& a, bool want_null) {
+    BoolBuilder b(a.len);
+    for (int64_t i = 0; i < a.len; ++i) b.push(a.is_null(i) == want_null);
+    return b.finish();
+}
+
 // -------------------------------------------------- compiled closures ---
 using Fn = std::function<ArrayRef(const Batch&)>;
 struct Runtime {  // RuntimeExpr::Compiled {name, f, t}
@@ -555,6 +629,22 @@ Runtime compile(const Expr& e, const dfmi_schema& s, uint32_t flags) {
         }
         case DFMI_EXPR_CAST: {
             const Expr& inner = *e.kids[0];
+            if ((flags & DFMI_FLAG_EXT_CAST) && inner.n->kind != DFMI_EXPR_LITERAL) {
+                Runtime c = compile(inner, s, flags);
+                const int to = n->data_type;
+                if (!is_numeric(c.t) || !is_numeric(to))
+                    fail(DFMI_ERR_NOT_IMPLEMENTED,
+                         std::string("CAST from ") + type_name(c.t) + " to " + type_name(to));
+                Runtime r;
+                r.name = expr_debug(e);
+                r.t = to;
+                Fn cf = c.f;
+                if (c.t == to)  // cast(): the same type returns the array itself
+                    r.f = cf;
+                else
+                    r.f = [cf, to](const Batch& b) { return cast_array(*cf(b), to); };
+                return r;
+            }
             if (inner.n->kind == DFMI_EXPR_COLUMN) fail(DFMI_ERR_EXECUTION, "column reference");
             if (inner.n->kind == DFMI_EXPR_LITERAL) {
                 if (inner.n->data_type == DFMI_TYPE_INT64) {
@@ -628,6 +718,18 @@ Runtime compile(const Expr& e, const dfmi_schema& s, uint32_t flags) {
             }
             fail(DFMI_ERR_EXECUTION, std::string("operator: ") + op_name(op));
         }
+        case DFMI_EXPR_IS_NULL: case DFMI_EXPR_IS_NOT_NULL:
+            if (flags & DFMI_FLAG_EXT_IS_NULL) {
+                Runtime c = compile(*e.kids[0], s, flags);
+                Runtime r;
+                r.name = expr_debug(e);
+                r.t = DFMI_TYPE_BOOLEAN;
+                Fn cf = c.f;
+                const bool want_null = n->kind == DFMI_EXPR_IS_NULL;
+                r.f = [cf, want_null](const Batch& b) { return is_null_array(*cf(b), want_null); };
+                return r;
+            }
+            fail(DFMI_ERR_EXECUTION, "expression " + expr_debug(e));
         default:
             fail(DFMI_ERR_EXECUTION, "expression " + expr_debug(e));
     }

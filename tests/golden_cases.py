@@ -88,6 +88,60 @@ ALL_TYPES_NARROW = [
 ]
 
 
+# Known answers that need CAST(column) (DFMI_FLAG_EXT_CAST): the SQL planner
+# coerces `c5 < 0` (Int8 vs the Int64 literal) to CAST(#5 AS Int64) Lt Int64(0)
+# (sqlplanner.rs:273-278) and `c5 > c6` to CAST(#5 AS Int16) Gt #6, which the
+# reference cannot execute ("column reference", expression.rs:281-282).
+# The unsigned columns cannot be compared with an Int64 literal at all
+# (can_coerce_from(Int64, UInt8) is false, logicalplan.rs:553-602), so their
+# files are reproduced by an explicit projection CAST (all 256 rows).
+# (file, {column: type}, SQL over table t of all_types_flat.csv)
+ALL_TYPES_CAST = [
+    ("c_int8_cast.csv", (5,), "SELECT c5 FROM t WHERE c5 < 0"),
+    ("c_int16_cast.csv", (6,), "SELECT c6 FROM t WHERE c6 < 0"),
+    ("c_int32_cast.csv", (7,), "SELECT c7 FROM t WHERE c7 < 0"),
+    ("c_int64_cast.csv", (8,), "SELECT c8 FROM t WHERE c8 < 0"),
+    ("c_float32_cast.csv", (9,), "SELECT c9 FROM t WHERE c9 < 0.5"),
+    ("c_float64_cast.csv", (10,), "SELECT c10 FROM t WHERE c10 < 0.5"),
+    ("c_uint8_cast.csv", (1,), "SELECT CAST(c1 AS BIGINT) FROM t"),
+    ("c_uint16_cast.csv", (2,), "SELECT CAST(c2 AS BIGINT) FROM t"),
+    ("c_uint32_cast.csv", (3,), "SELECT CAST(c3 AS BIGINT) FROM t"),
+    ("c_uint64_cast.csv", (4,), "SELECT CAST(c4 AS BIGINT) FROM t"),
+    ("c_int8_col_gt.csv", (5, 6), "SELECT c5 FROM t WHERE c5 > c6"),
+    ("c_int8_col_gteq.csv", (5, 6), "SELECT c5 FROM t WHERE c5 >= c6"),
+    ("c_int8_col_lt.csv", (5, 6), "SELECT c5 FROM t WHERE c5 < c6"),
+    ("c_int8_col_lteq.csv", (5, 6), "SELECT c5 FROM t WHERE c5 <= c6"),
+    ("c_int8_col_eq.csv", (5, 6), "SELECT c5 FROM t WHERE c5 = c6"),
+    ("c_int8_col_noteq.csv", (5, 6), "SELECT c5 FROM t WHERE c5 != c6"),
+]
+
+# expected/is_null_csv.csv / is_not_null_csv.csv over null_test.csv
+# (DFMI_FLAG_EXT_IS_NULL; IsNull/IsNotNull are commented out in the reference).
+NULL_TEST = Schema([Field("c_int", DataType.Int64, False), Field("c_float", DataType.Float64, True),
+                    Field("c_string", DataType.Utf8, True), Field("c_bool", DataType.Boolean, False)])
+NULL_CASES = [("is_null_csv.csv", "SELECT c_int FROM null_test WHERE c_float IS NULL"),
+              ("is_not_null_csv.csv", "SELECT c_int FROM null_test WHERE c_float IS NOT NULL")]
+
+
+def sql_plan(sql: str, schema: Schema, table: str):
+    """(predicate, projections) the reference's SQL planner produces."""
+    from datafusion_amd.sqlplanner import SqlToRel
+
+    class _Ctx:
+        def table_schema(self, name):
+            return schema if name == table else None
+    p = SqlToRel(_Ctx()).sql_to_rel(sql)
+    pred = p.input.expr if type(p.input).__name__ == "Selection" else None
+    return pred, p.expr
+
+
+def cast_fixture_case(name, cols, sql):
+    """(schema, predicate, projections) of an ALL_TYPES_CAST entry."""
+    s = all_types_schema(typed={c: ALL_TYPES[c] for c in cols})
+    pred, projs = sql_plan(sql, s, "t")
+    return s, pred, projs
+
+
 def fixture_values(name: str, t: DataType) -> list:
     """One-column expected file as Python values of type t."""
     rows = expected_rows(name)

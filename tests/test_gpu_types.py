@@ -157,3 +157,76 @@ def test_all_columns_typed_on_gpu():
         lit = lit_of(t, 0.5 if t in (DataType.Float32, DataType.Float64) else 1)
         run_both(s, batch, BinaryExpr(Column(col), Operator.Gt, lit), [], GA)
         run_both(s, batch, None, [BinaryExpr(Column(col), Operator.Plus, lit), BinaryExpr(Column(col), Operator.LtEq, lit)])
+
+
+# ------------------------------------------------ CAST / IS NULL extensions
+from datafusion_amd._abi import DFMI_FLAG_EXT_CAST, DFMI_FLAG_EXT_IS_NULL  # noqa: E402
+from datafusion_amd.logicalplan import Cast, IsNotNull, IsNull  # noqa: E402
+from golden_cases import (ALL_TYPES_CAST, NULL_CASES, NULL_TEST, cast_fixture_case,  # noqa: E402
+                          sql_plan)
+
+EXT = GA | DFMI_FLAG_EXT_CAST | DFMI_FLAG_EXT_IS_NULL
+
+
+@pytest.mark.parametrize("case", ALL_TYPES_CAST, ids=[c[0] for c in ALL_TYPES_CAST])
+def test_all_types_cast_on_gpu(case):
+    """expected/c_*_cast.csv and c_int8_col_*.csv: planner-inserted CAST(column)."""
+    name, cols, sql = case
+    s, pred, projs = cast_fixture_case(*case)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    dev, _ = run_both(s, batch, pred, projs, EXT)
+    assert dev[0].cpu().to_pylist() == fixture_values(name, ALL_TYPES[cols[0]])
+    if "CAST(" in repr(pred) + repr(projs):
+        assert run_both(s, batch, pred, projs, GA) is None  # "column reference" without the flag
+
+
+@pytest.mark.parametrize("name,sql", NULL_CASES)
+def test_is_null_on_gpu(name, sql):
+    batch = load_batch(NULL_TEST, "null_test.csv", has_header=True)
+    pred, projs = sql_plan(sql, NULL_TEST, "null_test")
+    dev, _ = run_both(NULL_TEST, batch, pred, projs, EXT)
+    assert dev[0].cpu().to_pylist() == [int(r[0]) for r in expected_rows(name)]
+    assert run_both(NULL_TEST, batch, pred, projs, GA) is None  # "expression #1 IS NULL"
+
+
+@pytest.mark.parametrize("t", TYPES, ids=[t.name for t in TYPES])
+def test_cast_every_pair(t):
+    """CAST from t to every numeric type over the whole value range (edge
+    values, NaN/inf for floats, nulls): values that do not fit become nulls,
+    as a projection (dense kernel) and inside a predicate."""
+    s, b, _ = typed_table(t, 20_000, seed=int(t) * 13)
+    run_both(s, b, None, [Cast(Column(0), u) for u in TYPES], EXT)
+    for u in TYPES:
+        pred = BinaryExpr(Cast(Column(0), u), Operator.GtEq, Cast(Column(1), u))
+        run_both(s, b, pred, [Cast(Column(2), u), Column(0)], EXT)
+    # nested: CAST of arithmetic, arithmetic over casts
+    e = BinaryExpr(Cast(BinaryExpr(Column(0), Operator.Plus, Column(1)), DataType.Float64), Operator.Multiply,
+                   Cast(Column(2), DataType.Float64))
+    run_both(s, b, None, [e, Cast(Cast(Column(0), DataType.Int16), DataType.Float32)], EXT)
+
+
+def test_is_null_every_type():
+    """IS NULL / IS NOT NULL of columns of every type (incl. Utf8 and
+    Boolean) and of null-propagating expressions, as predicate and projection;
+    after a Selection the batch has no nulls (filter() drops validity)."""
+    rng = np.random.default_rng(5)
+    n = 30_000
+    cols, fields = [], []
+    for i, t in enumerate(TYPES):
+        cols.append(Array.from_numpy(t, typed_values(t, n, rng), rng.random(n) >= 0.25))
+        fields.append(Field("x%d" % i, t, True))
+    strs = [None if rng.random() < 0.2 else b"s%d" % (i % 97) for i in range(n)]
+    cols.append(Array.from_strings(strs))
+    fields.append(Field("s", DataType.Utf8, True))
+    cols.append(Array.from_numpy(DataType.Boolean, rng.random(n) < 0.5, rng.random(n) >= 0.3))
+    fields.append(Field("f", DataType.Boolean, True))
+    s = Schema(fields)
+    bt = RecordBatch(s, cols)
+    nc = len(fields)
+    run_both(s, bt, None, [IsNull(Column(i)) for i in range(nc)] + [IsNotNull(Column(0))], EXT)
+    for i in range(nc):
+        run_both(s, bt, IsNull(Column(i)), [Column(9), IsNull(Column(9))], EXT)
+        run_both(s, bt, IsNotNull(Column(i)), [Column(10), Column(3)], EXT)
+    e = BinaryExpr(Column(2), Operator.Multiply, Column(2))
+    run_both(s, bt, BinaryExpr(IsNull(e), Operator.Or, BinaryExpr(Column(9), Operator.Gt, Column(9))),
+             [IsNotNull(e), e], EXT)

@@ -201,3 +201,22 @@ def test_random_shapes_generate_and_sample_compiles():
             assert rc > 0, (msg, repr(pred), [repr(p) for p in projs])
             compiled += 1
     assert generated > 150 and compiled >= 10
+
+
+def test_cast_and_is_null_kernels_compile():
+    from datafusion_amd.logicalplan import IsNotNull, IsNull
+    types = [DataType.Int8, DataType.UInt16, DataType.Int32, DataType.UInt64, DataType.Float32, DataType.Float64]
+    sch = Schema([Field("x%d" % i, t, True) for i, t in enumerate(types)] + [Field("s", DataType.Utf8, True)])
+    fl = _abi.DFMI_FLAG_EXT_CAST | _abi.DFMI_FLAG_EXT_IS_NULL | _abi.DFMI_FLAG_EXT_GATHER_ALL
+    projs = [Cast(Column(i), u) for i in range(len(types)) for u in types[:2]]
+    rc, code, msg, src = jit_check(sch, None, projs[:12], fl, compile_=True)
+    assert rc > 0, msg
+    assert "num_cast" in src
+    pred = BinaryExpr(IsNull(Column(6)), Operator.Or,
+                      BinaryExpr(Cast(Column(4), DataType.Int64), Operator.Gt, Cast(Column(0), DataType.Int64)))
+    rc, code, msg, src = jit_check(sch, pred, [IsNotNull(Column(1)), Cast(Column(5), DataType.UInt8)], fl, compile_=True)
+    assert rc > 0, msg
+    # without the flags the reference's compile errors stand
+    with pytest.raises(ExecutionError) as e:
+        compile_scalar_expr(None, Cast(Column(0), DataType.Int64), sch)
+    assert e.value.message == "column reference"

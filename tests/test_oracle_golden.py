@@ -9,8 +9,10 @@ from datafusion_amd.execution.error import ExecutionError
 from datafusion_amd.logicalplan import (BinaryExpr, Cast, Column, DataType, Float64, Int64, Literal, Operator,
                                         binary_expr_coerced)
 from datafusion_amd.sqlplanner import SqlToRel
-from golden_cases import (ALL_TYPES, ALL_TYPES_NARROW, GOLDEN, CITIES, NUMERICS, all_types_schema, expected_rows,
-                          fixture_values, load_batch, lit_expr, narrow_fixture_case, smoketest_points)
+from golden_cases import (ALL_TYPES, ALL_TYPES_CAST, ALL_TYPES_NARROW, GOLDEN, CITIES, NULL_CASES, NULL_TEST,
+                          NUMERICS, all_types_schema, cast_fixture_case, expected_rows, fixture_values, load_batch,
+                          lit_expr, narrow_fixture_case, smoketest_points, sql_plan)
+from datafusion_amd._abi import DFMI_FLAG_EXT_CAST, DFMI_FLAG_EXT_IS_NULL
 from oracle_ffi import oracle_compile, oracle_filter_project
 
 
@@ -159,6 +161,63 @@ def test_all_types_narrow(case):
     assert e.value.message == "filter not supported for %r" % ALL_TYPES[col]
     out = oracle_filter_project(s, batch, pred, projs, DFMI_FLAG_EXT_GATHER_ALL)
     assert out[0][1].to_pylist() == fixture_values(name, ALL_TYPES[col])
+
+
+@pytest.mark.parametrize("case", ALL_TYPES_CAST, ids=[c[0] for c in ALL_TYPES_CAST])
+def test_all_types_cast_extension(case):
+    """expected/c_*_cast.csv, c_int8_col_*.csv: planner-inserted CAST(column)
+    nodes, executable only under DFMI_FLAG_EXT_CAST."""
+    name, cols, sql = case
+    s, pred, projs = cast_fixture_case(*case)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    fl = DFMI_FLAG_EXT_GATHER_ALL | DFMI_FLAG_EXT_CAST
+    if "CAST(" in repr(pred) + repr(projs):
+        with pytest.raises(ExecutionError) as e:
+            oracle_filter_project(s, batch, pred, projs, DFMI_FLAG_EXT_GATHER_ALL)
+        assert e.value.message == "column reference"
+    out = oracle_filter_project(s, batch, pred, projs, fl)
+    assert out[0][1].to_pylist() == fixture_values(name, ALL_TYPES[cols[0]])
+
+
+@pytest.mark.parametrize("name,sql", NULL_CASES)
+def test_is_null_extension(name, sql):
+    """expected/is_null_csv.csv, is_not_null_csv.csv over null_test.csv."""
+    batch = load_batch(NULL_TEST, "null_test.csv", has_header=True)
+    pred, projs = sql_plan(sql, NULL_TEST, "null_test")
+    with pytest.raises(ExecutionError) as e:
+        oracle_filter_project(NULL_TEST, batch, pred, projs, DFMI_FLAG_EXT_GATHER_ALL)
+    assert e.value.message.startswith("expression #1 IS")
+    out = oracle_filter_project(NULL_TEST, batch, pred, projs, DFMI_FLAG_EXT_GATHER_ALL | DFMI_FLAG_EXT_IS_NULL)
+    assert out[0][1].to_pylist() == [int(r[0]) for r in expected_rows(name)]
+
+
+def test_cast_rules():
+    """num::cast rules of the arrow cast kernel (parity unpinned beyond the
+    fixtures): out-of-range and NaN -> null, truncation toward zero."""
+    from datafusion_amd.arrow import Array, RecordBatch
+    from datafusion_amd.logicalplan import ScalarValue
+    f = np.array([1.9, -1.9, 127.5, 128.0, -128.9, -129.0, np.nan, np.inf, 3e38, 4e38, -0.5], dtype=np.float64)
+    S = Schema([Field("f", DataType.Float64, False)])
+    b = RecordBatch(S, [Array.from_numpy(DataType.Float64, f)])
+    fl = DFMI_FLAG_EXT_CAST
+    out = oracle_filter_project(S, b, None, [Cast(Column(0), DataType.Int8), Cast(Column(0), DataType.Float32),
+                                            Cast(Column(0), DataType.UInt8)], fl)
+    assert out[0][0] == "CAST(#0 AS Int8)"
+    assert out[0][1].to_pylist() == [1, -1, 127, None, -128, None, None, None, None, None, 0]
+    f32 = out[1][1].to_pylist()
+    assert f32[8] == float(np.float32(3e38)) and f32[9] is None and f32[7] == float("inf")
+    assert out[2][1].to_pylist() == [1, None, 127, 128, None, None, None, None, None, None, 0]
+    i = np.array([-1, 255, 256, -(1 << 63), (1 << 63) - 1], dtype=np.int64)
+    S2 = Schema([Field("i", DataType.Int64, False)])
+    b2 = RecordBatch(S2, [Array.from_numpy(DataType.Int64, i)])
+    out = oracle_filter_project(S2, b2, None, [Cast(Column(0), DataType.UInt8), Cast(Column(0), DataType.UInt64),
+                                              Cast(Column(0), DataType.Float32)], fl)
+    assert out[0][1].to_pylist() == [None, 255, None, None, None]
+    assert out[1][1].to_pylist() == [None, 255, 256, None, (1 << 63) - 1]
+    assert out[2][1].to_pylist()[3] == -2.0 ** 63
+    with pytest.raises(ExecutionError) as e:
+        oracle_filter_project(S2, b2, None, [Cast(Literal(ScalarValue(DataType.Int32, 1)), DataType.Int64)], fl)
+    assert e.value.kind == "NotImplemented"
 
 
 def test_projection_unit_test():
