@@ -121,6 +121,7 @@ EXPORTED = [
     "dfmi_host_result_column",
     "dfmi_host_result_free",
     "dfmi_last_timing",
+    "dfmi_last_compile_ms",
     "dfmi_generate_column",  # include/dfmi_datasource.h
 ]
 
@@ -208,6 +209,8 @@ def lib() -> C.CDLL:
     L.dfmi_host_result_free.restype = None
     L.dfmi_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.dfmi_last_timing.restype = C.c_int32
+    L.dfmi_last_compile_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    L.dfmi_last_compile_ms.restype = C.c_int32
     L.dfmi_generate_column.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_void_p, C.POINTER(dfmi_error)]
     L.dfmi_generate_column.restype = C.c_int32

@@ -7,6 +7,7 @@
 // errors the reference would raise only when the closure runs (comparison_ops,
 // math_ops, boolean_ops' unwrap panic) so execution reports them in the
 // reference's order.
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -354,6 +355,8 @@ extern "C" int32_t dfmi_compile_scalar_expr(const dfmi_expr_node* nodes, int32_t
         return DFMI_ERR_INVALID_ARGUMENT;
     }
     try {
+        static std::atomic<uint64_t> next_uid{1};
+        p->uid = next_uid.fetch_add(1);
         p->flags = flags;
         p->length = num_nodes;
         for (int i = 0; i < schema->num_fields; ++i) p->schema_types.push_back(schema->fields[i].type);

@@ -37,6 +37,7 @@ std::string rust_float(double v, bool f32, bool debug);
 }  // namespace dfmi
 
 struct dfmi_program {
+    uint64_t uid = 0;               // unique per compiled program (never reused): kernel cache key
     std::string name;
     int type = 0;
     uint32_t flags = 0;

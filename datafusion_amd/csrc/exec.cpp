@@ -29,7 +29,7 @@ hipError_t launch_pack_bools(const uint8_t* bytes, uint8_t* bits, const unsigned
 
 using namespace dfmi;
 
-// Workspace header layout (device, zeroed before every launch).
+// Workspace header layout (device, zero when a launch starts).
 static constexpr size_t kHdrTicket = 0;
 static constexpr size_t kHdrErr = 8;
 static constexpr size_t kHdrTotals = 16;
@@ -39,11 +39,20 @@ static constexpr size_t kHdrAlloc = 512;
 struct dfmi_context {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint8_t* ws = nullptr;       // header + look-back status
+    // Look-back workspace, double-buffered: [hdr 0 | hdr 1 | status 0 | status 1].
+    // Launch i uses pair (i & 1), which is zero on entry, and its blocks zero
+    // pair (i+1) & 1 -- what launch i-1 dirtied -- for launch i+1 (stream
+    // order makes launch i-1 complete first). No memset on the steady path.
+    uint8_t* ws = nullptr;
     size_t ws_bytes = 0;
+    size_t status_cap = 0;       // bytes per status buffer
+    int parity = 0;              // pair the next launch uses
+    size_t dirty[2] = {0, 0};    // status bytes [0, dirty[b]) of buffer b may be non-zero
+    bool ws_valid = false;       // the invariant above holds (else re-zero everything)
     uint8_t* scratch = nullptr;  // Boolean output bytes (filtered)
     size_t scratch_bytes = 0;
     uint8_t* host_hdr = nullptr; // pinned copy of the header
+    void* host_arena = nullptr;  // host_batch.cpp's staging arena (per context: no shared state)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_total_ms = 0, last_main_ms = 0, last_compile_ms = 0;
     bool timed = false;
@@ -106,8 +115,24 @@ struct Built {
     int64_t n_tiles = 0;
 };
 
+void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
+                     dfmi_out_column* outs, uint32_t flags, Built& B);
+
+// A device limit (NotImplemented) found while planning is reported only when
+// the plan raises none of the reference's own errors first: those come
+// earlier in its evaluation order (and stand for what it would report).
 void build_plan(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
                 dfmi_out_column* outs, uint32_t flags, Built& B) {
+    try {
+        build_plan_impl(pred, projs, np, in, outs, flags, B);
+    } catch (const Fail& f) {
+        if (f.code == DFMI_ERR_NOT_IMPLEMENTED && B.se.set) throw Fail{B.se.code, B.se.msg};
+        throw;
+    }
+}
+
+void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
+                     dfmi_out_column* outs, uint32_t flags, Built& B) {
     Err& se = B.se;
     jit::Plan& plan = B.plan;
     jit::Launch& X = B.X;
@@ -293,7 +318,8 @@ extern "C" int32_t dfmi_context_create(int32_t device, void* stream, dfmi_contex
 namespace dfmi {
 int ctx_device(const dfmi_context* c) { return c->device; }
 hipStream_t ctx_stream(const dfmi_context* c) { return c->stream; }
-void host_arena_release(const dfmi_context* c);
+void*& ctx_host_arena(dfmi_context* c) { return c->host_arena; }
+void host_arena_release(dfmi_context* c);
 }  // namespace dfmi
 
 extern "C" void dfmi_context_destroy(dfmi_context* c) {
@@ -322,6 +348,12 @@ extern "C" int32_t dfmi_last_timing(const dfmi_context* c, double* total_ms, dou
     return DFMI_OK;
 }
 
+extern "C" int32_t dfmi_last_compile_ms(const dfmi_context* c, double* compile_ms) {
+    if (!c || !compile_ms) return DFMI_ERR_INVALID_ARGUMENT;
+    *compile_ms = c->last_compile_ms;
+    return DFMI_OK;
+}
+
 extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pred,
                                        const dfmi_program* const* projs, int32_t np,
                                        const dfmi_batch* in, dfmi_out_column* outs, uint32_t flags,
@@ -345,6 +377,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         HIP_TRY(hipSetDevice(ctx->device));
         hipStream_t st = ctx->stream;
         ctx->timed = false;
+        ctx->last_compile_ms = 0;
         const bool launch = n > 0 && (pred || any_kernel_out);
         uint64_t dev_key = ~0ull;
         int dev_kind = 0;
@@ -371,7 +404,17 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 if (plan.outs[o].nullable) valid_out.push_back(o);
             }
             const size_t row_bytes = (size_t)((n + 63) & ~63ll);
-            ensure(ctx, &ctx->ws, &ctx->ws_bytes, kHdrAlloc + status_bytes);
+            if (!ctx->ws || status_bytes > ctx->status_cap) {
+                const size_t cap = (std::max(status_bytes, (size_t)1 << 20) + 255) & ~(size_t)255;
+                ensure(ctx, &ctx->ws, &ctx->ws_bytes, 2 * kHdrAlloc + 2 * cap);
+                ctx->status_cap = cap;
+                ctx->ws_valid = false;
+            }
+            if (!ctx->ws_valid) {  // first use, growth, or an interrupted call
+                HIP_TRY(hipMemsetAsync(ctx->ws, 0, 2 * kHdrAlloc + 2 * ctx->status_cap, st));
+                ctx->dirty[0] = ctx->dirty[1] = 0;
+                ctx->ws_valid = true;
+            }
             if (!bool_out.empty() || !valid_out.empty())
                 ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, (bool_out.size() + valid_out.size()) * row_bytes);
             A.n_rows = n;
@@ -410,25 +453,36 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             memcpy(A.str_off, X.str_off, sizeof A.str_off);
             memcpy(A.str_len, X.str_len, sizeof A.str_len);
             memcpy(A.str, X.str, sizeof A.str);
-            A.ticket = (unsigned*)(ctx->ws + kHdrTicket);
-            A.err = (unsigned long long*)(ctx->ws + kHdrErr);
-            A.totals = (unsigned long long*)(ctx->ws + kHdrTotals);
-            A.status = (unsigned long long*)(ctx->ws + kHdrAlloc);
-            A.stats = (unsigned long long*)(ctx->ws + kHdrStats);
+            const int par = ctx->parity;
+            uint8_t* hdr = ctx->ws + par * kHdrAlloc;
+            uint8_t* status = ctx->ws + 2 * kHdrAlloc + par * ctx->status_cap;
+            uint8_t* other_status = ctx->ws + 2 * kHdrAlloc + (1 - par) * ctx->status_cap;
+            A.ticket = (unsigned*)(hdr + kHdrTicket);
+            A.err = (unsigned long long*)(hdr + kHdrErr);
+            A.totals = (unsigned long long*)(hdr + kHdrTotals);
+            A.status = (unsigned long long*)status;
+            A.stats = (unsigned long long*)(hdr + kHdrStats);
+            A.clear_status = (unsigned long long*)other_status;
+            A.clear_words = (long long)(ctx->dirty[1 - par] / 8);
+            A.clear_hdr = (unsigned long long*)(ctx->ws + (1 - par) * kHdrAlloc);
             A.mode = 0;
             if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
             const unsigned grid = (unsigned)n_tiles;  // one block per tile
-            HIP_TRY(hipMemsetAsync(ctx->ws, 0, kHdrAlloc + status_bytes, st));
             HIP_TRY(hipEventRecord(ctx->ev0, st));
             size_t asz = sizeof A;
             void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+            ctx->ws_valid = false;  // until the launch is enqueued
             HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
+            ctx->dirty[par] = status_bytes;
+            ctx->dirty[1 - par] = 0;
+            ctx->parity = 1 - par;
+            ctx->ws_valid = true;
             HIP_TRY(hipEventRecord(ctx->ev1, st));
             for (int o = 0; o < nout; ++o)
                 if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
             for (int o : valid_out)
                 HIP_TRY(launch_pack_bools(A.out_valid[o], outs[o].validity, A.totals, n, st));
-            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ctx->ws, kHdrAlloc, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipEventRecord(ctx->ev2, st));
             HIP_TRY(hipStreamSynchronize(st));
             uint64_t ew;

@@ -33,6 +33,7 @@ using dfmi::Fail;
 namespace dfmi {
 int ctx_device(const dfmi_context* c);
 hipStream_t ctx_stream(const dfmi_context* c);
+void*& ctx_host_arena(dfmi_context* c);
 }  // namespace dfmi
 
 // Allocator whose resize() leaves bytes uninitialised: result buffers are
@@ -111,13 +112,12 @@ struct Arena {
     }
 };
 
-std::vector<std::pair<const dfmi_context*, Arena*>> g_arenas;
-
-Arena& arena_of(const dfmi_context* c) {
-    for (auto& a : g_arenas)
-        if (a.first == c) return *a.second;
-    g_arenas.push_back({c, new Arena()});
-    return *g_arenas.back().second;
+// The arena lives in the context (created on first use, freed with it), so
+// contexts driven from different host threads share nothing.
+Arena& arena_of(dfmi_context* c) {
+    void*& slot = dfmi::ctx_host_arena(c);
+    if (!slot) slot = new Arena();
+    return *(Arena*)slot;
 }
 
 // Host copy split over a few threads: one core's memcpy (~10-20 GB/s) would
@@ -200,18 +200,16 @@ void set_err(dfmi_error* err, int32_t code, const std::string& m) {
 }  // namespace
 
 namespace dfmi {
-void host_arena_release(const dfmi_context* c) {
-    for (size_t i = 0; i < g_arenas.size(); ++i) {
-        if (g_arenas[i].first != c) continue;
-        Arena* a = g_arenas[i].second;
-        if (a->dev) (void)hipFree(a->dev);
-        if (a->pin) (void)hipHostFree(a->pin);
-        for (auto e : a->drained)
-            if (e) (void)hipEventDestroy(e);
-        delete a;
-        g_arenas.erase(g_arenas.begin() + i);
-        return;
-    }
+void host_arena_release(dfmi_context* c) {
+    void*& slot = ctx_host_arena(c);
+    Arena* a = (Arena*)slot;
+    if (!a) return;
+    if (a->dev) (void)hipFree(a->dev);
+    if (a->pin) (void)hipHostFree(a->pin);
+    for (auto e : a->drained)
+        if (e) (void)hipEventDestroy(e);
+    delete a;
+    slot = nullptr;
 }
 }  // namespace dfmi
 

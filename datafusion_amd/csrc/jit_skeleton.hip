@@ -53,7 +53,23 @@ struct Args {
     u64* err;                          // max(~key) error word
     u64* totals;                       // [0..8) channel totals, [8..24) null counts
     u64* stats;                        // look-back statistics (mode bit 4): polls, sleeps, tiles
+    // The context's workspace is double-buffered: this launch uses one
+    // header + status array (zero on entry) and zeroes the other pair, which
+    // the previous launch used, for the next launch -- no memset per call.
+    u64* clear_status;                 // previous launch's status words ...
+    i64 clear_words;                   // ... [0, clear_words) to zero
+    u64* clear_hdr;                    // previous launch's 512-byte header
 };
+
+// This block's share of zeroing the previous launch's workspace.
+template <int BLOCK>
+__device__ __forceinline__ void clear_previous(const Args& A, unsigned block, int tid) {
+    const i64 per = (A.clear_words + A.n_tiles - 1) / A.n_tiles;
+    const i64 w0 = (i64)block * per;
+    const i64 w1 = w0 + per < A.clear_words ? w0 + per : A.clear_words;
+    for (i64 w = w0 + tid; w < w1; w += BLOCK) A.clear_status[w] = 0;
+    if (block == 0 && tid < 64) A.clear_hdr[tid] = 0;
+}
 
 enum ErrKind : unsigned { ERRK_DIV_ZERO = 1, ERRK_DIV_OVERFLOW = 2, ERRK_LOOKBACK_TIMEOUT = 3, ERRK_CAPACITY = 4 };
 
@@ -298,10 +314,12 @@ __device__ u64 lb_resolve(u64* st, unsigned tile, u64 agg, int lane, u64* err, u
     if (tile == 0) return 0;
     u64 excl = 0;
     i64 j = (i64)tile - 1;  // highest predecessor not yet accounted for
-    const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    const u64 t_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    u64 t0 = t_start;  // last progress: the timeout is time WITHOUT progress
     unsigned polls = 0, sleeps = 0;
     while (true) {
         ++polls;
+        const i64 j_before = j;
         u64 w[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -335,7 +353,12 @@ __device__ u64 lb_resolve(u64* st, unsigned tile, u64 agg, int lane, u64* err, u
         }
         if (done) break;
         if (stall) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+            const u64 now = __builtin_amdgcn_s_memrealtime();
+            if (j != j_before) {
+                t0 = now;  // predecessors resolved this round: progress
+            } else if (now - t0 > 200000000ull) {
+                // 2 s without a single predecessor resolving (a preempted or
+                // time-sliced GPU is far below this): report, do not hang
                 if (lane == 0) report_err(err, 0, 0, ERRK_LOOKBACK_TIMEOUT);
                 break;
             }
@@ -347,7 +370,7 @@ __device__ u64 lb_resolve(u64* st, unsigned tile, u64 agg, int lane, u64* err, u
     if (stats && lane == 0) {
         atomicAdd(stats, (u64)polls);
         atomicAdd(stats + 1, (u64)sleeps);
-        atomicAdd(stats + 2, __builtin_amdgcn_s_memrealtime() - t0);
+        atomicAdd(stats + 2, __builtin_amdgcn_s_memrealtime() - t_start);
     }
     return excl;
 }

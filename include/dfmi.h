@@ -260,6 +260,11 @@ void dfmi_host_result_free(dfmi_host_result* result);
  * (HIP events on the context stream), and the dominant kernel's share. */
 int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main_kernel_ms);
 
+/* hipRTC compile time in milliseconds of the last dfmi_filter_project call
+ * (0 when its query shape was already compiled: the kernel cache is keyed by
+ * the programs and the batch's column types / nullability). */
+int32_t dfmi_last_compile_ms(const dfmi_context* ctx, double* compile_ms);
+
 #ifdef __cplusplus
 }
 #endif
