@@ -275,7 +275,8 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
     if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;  // diagnostics only
-    if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 64)
+    if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) & 1;  // diagnostics only
+    if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 256)
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
     const int64_t n_tiles = (n + tile_rows - 1) / tile_rows;

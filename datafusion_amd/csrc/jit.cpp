@@ -442,14 +442,33 @@ std::string generate(const Plan& P, Launch& X) {
                 o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
             o << "  }\n";
             g.tile_pre = false;
-            if (!g.pre_eq.empty()) {  // splice the tile-wide Utf8 compares in front of the loop
-                const std::string loop = o.str().substr(head.size());
+            // Utf8 columns whose offsets are in registers (us<u> start, ux<u>
+            // next slice's first offset): the predicate's tile-wide compares and
+            // every Utf8 output (its byte count is needed before the look-back,
+            // so its offsets are loaded with the predicate columns -- one memory
+            // round trip before the tile publishes, not two). Spliced in front
+            // of the predicate loop.
+            std::vector<int> offs_loaded;
+            auto offs_name = [&](int u) { return std::to_string(u) + cur; };
+            {
                 std::ostringstream pre;
+                auto load_offs = [&](int u) {
+                    if (std::find(offs_loaded.begin(), offs_loaded.end(), u) != offs_loaded.end()) return;
+                    offs_loaded.push_back(u);
+                    pre << "  int us" << offs_name(u) << "[K], ux" << offs_name(u)
+                        << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u << ", base, lane, wave, ~0u, us"
+                        << offs_name(u) << ", ux" << offs_name(u) << ");\n";
+                };
+                for (const auto& pe : g.pre_eq) load_offs(std::get<1>(pe));
+                for (const auto& uo : X.utf8_outs) load_offs(uo.second);
                 for (const auto& [arr, u, sl] : g.pre_eq)
-                    pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u
-                        << ", base, tid, " << sl << ", " << arr << ");\n";
-                o.str(head + pre.str() + loop);
-                o.seekp(0, std::ios_base::end);
+                    pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u << ", " << sl
+                        << ", us" << offs_name(u) << ", ux" << offs_name(u) << ", lane, " << arr << ");\n";
+                if (!pre.str().empty()) {
+                    const std::string loop = o.str().substr(head.size());
+                    o.str(head + pre.str() + loop);
+                    o.seekp(0, std::ios_base::end);
+                }
             }
             // projection-only columns, loaded only where selected
             emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
@@ -458,10 +477,9 @@ std::string generate(const Plan& P, Launch& X) {
               << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
                 const int u = X.utf8_outs[j].second;
-                o << "  unsigned len" << j << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
-                  << "    const i64 row = base + k * BLOCK + tid;\n"
-                  << "    len" << j << "[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[" << u << "][row + 1] - A.offs["
-                  << u << "][row]) : 0u;\n    cnt[" << (j + 1) << "][k] = len" << j << "[k];\n  }\n";
+                o << "#pragma unroll\n  for (int k = 0; k < K; ++k) { const int e_ = dfmi::utf8_end(us" << offs_name(u)
+                  << "[k], ux" << offs_name(u) << "[k], lane); cnt[" << (j + 1) << "][k] = ((selm >> k) & 1) ? "
+                  << "(unsigned)(e_ - us" << offs_name(u) << "[k]) : 0u; }\n";
             }
             {
                 o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << tparams << ">(A, " << T << ", t, cnt, lane, wave);\n";
@@ -506,8 +524,15 @@ std::string generate(const Plan& P, Launch& X) {
                     o << "  { const u64 s_ = dfmi::wave_sum((u64)nn" << oi << "); if (lane == 0 && s_) atomicAdd(&A.totals[8 + "
                       << oi << "], s_); }\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
-                o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << X.utf8_outs[j].second
-                  << ", " << X.utf8_outs[j].first << ", base, selm, len" << j << ", dst, lane, wave);\n";
+                const int u = X.utf8_outs[j].second;
+                if (X.gather == 0)
+                    o << "  dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << u << ", "
+                      << X.utf8_outs[j].first << ", selm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
+                      << ", lane, wave);\n";
+                else
+                    o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << u << ", "
+                      << X.utf8_outs[j].first << ", selm, wm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
+                      << ", G[wave], lane, wave);\n";
             }
             if (!X.utf8_outs.empty()) {
                 o << "  if (tid == 0 && t == (unsigned)A.n_tiles - 1) {\n";
@@ -524,6 +549,7 @@ std::string generate(const Plan& P, Launch& X) {
             // one tile per block in dispatch order (in order per XCD, so every
             // tile a block waits on in the look-back is running or done)
             o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
+            if (!X.utf8_outs.empty() && X.gather) o << "  __shared__ dfmi::Utf8Stage G[WAVES];\n";
             o << "  const unsigned t = blockIdx.x;\n";
             emit_decls(o, X.pred_slots, X, "", true);
             emit_decls(o, X.proj_slots, X, "", false);
@@ -604,7 +630,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, os.out_type);
         put(k, (char)os.nullable);
     }
-    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt};
+    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -78,6 +78,18 @@ constexpr u64 FLAG_P = 2ull << 62;
 constexpr u64 VAL_MASK = (1ull << 62) - 1;
 
 __device__ __forceinline__ double f64(u64 x) { return __builtin_bit_cast(double, x); }
+
+// Pointer at a byte offset from `base`. Addresses are formed by pointer
+// arithmetic, never by integer -> pointer casts: the compiler then keeps
+// them in the global address space (global_* instructions, not flat_*).
+template <typename T, typename B>
+__device__ __forceinline__ T* at(B* base, i64 off) {
+    return (T*)((u8*)base + off);
+}
+template <typename T, typename B>
+__device__ __forceinline__ const T* at(const B* base, i64 off) {
+    return (const T*)((const u8*)base + off);
+}
 __device__ __forceinline__ u64 bits(double x) { return __builtin_bit_cast(u64, x); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -85,29 +97,52 @@ __device__ __forceinline__ unsigned lane_rank(u64 mask) {  // set bits below thi
     return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
 
-__device__ __forceinline__ u64 wave_sum(u64 v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ u64 wave_incl_scan(u64 v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const u64 t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+// Wave-wide scans on DPP lane moves (no LDS round trip): row_shr 1/2/4/8
+// within each row of 16 lanes, then row_bcast 15/31 carry the row totals
+// into the rows above. Every lane of the wave must be active. A source lane
+// outside the row / a disabled row contributes 0.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp32(unsigned v) {
+    return __builtin_amdgcn_update_dpp(0u, v, CTRL, ROWS, 0xf, false);
 }
 
 __device__ __forceinline__ unsigned wave_incl_scan32(unsigned v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    (void)lane;
+    v += dpp32<0x111, 0xf>(v);  // row_shr:1
+    v += dpp32<0x112, 0xf>(v);  // row_shr:2
+    v += dpp32<0x114, 0xf>(v);  // row_shr:4
+    v += dpp32<0x118, 0xf>(v);  // row_shr:8
+    v += dpp32<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp32<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
     return v;
 }
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ u64 dpp64(u64 v) {
+    const unsigned lo = dpp32<CTRL, ROWS>((unsigned)v), hi = dpp32<CTRL, ROWS>((unsigned)(v >> 32));
+    return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ u64 wave_incl_scan(u64 v, int lane) {
+    (void)lane;
+    v += dpp64<0x111, 0xf>(v);
+    v += dpp64<0x112, 0xf>(v);
+    v += dpp64<0x114, 0xf>(v);
+    v += dpp64<0x118, 0xf>(v);
+    v += dpp64<0x142, 0xa>(v);
+    v += dpp64<0x143, 0xc>(v);
+    return v;
+}
+
+// Sum over the wave (uniform result).
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+    const u64 t = wave_incl_scan(v, 0);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)t, 63), hi = __builtin_amdgcn_readlane((unsigned)(t >> 32), 63);
+    return ((u64)hi << 32) | lo;
+}
+
+// The value of the next lane (lane 63: 0).
+__device__ __forceinline__ int next_lane(int v) { return (int)dpp32<0x130, 0xf>((unsigned)v); }  // wave_shl:1
 
 // 64 bits of an LSB-first bitmap starting at row 64*w (w wave-uniform); the
 // tail word is assembled bytewise so nothing past the bitmap is read.
@@ -214,46 +249,70 @@ __device__ __forceinline__ bool utf8_eq_lit(const Args& A, int u, i64 row, int l
     return true;
 }
 
-// `utf8 column u = literal` for the K rows base + k*BLOCK + tid of a tile.
-// Per-row early-exit compares serialise one memory latency per k; here every
-// row's offsets, then the first min(len, 4) bytes of every equal-length
-// candidate, are in flight together, and only head matches (rare) compare
-// the rest. Rows past n_rows read nothing and compare false.
+// Offsets of Utf8 column u for the K rows of a tile (rows base + k*BLOCK +
+// 64*wave + lane): one coalesced load per row (its start, s[k]) plus one
+// wave-uniform load per 64-row slice (the next slice's first offset, nx[k]);
+// a row's end is its right neighbour's start (utf8_end). Rows past n_rows
+// read offs[n_rows] (inside the buffer) and come out empty. Slices whose bit
+// in `need` is clear (wave-uniform) load nothing.
 template <int BLOCK, int K>
-__device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, i64 base, int tid, int lit, bool (&res)[K]) {
-    const int len = A.str_len[lit];
-    const char* q = A.str + A.str_off[lit];
+__device__ __forceinline__ void utf8_offs_tile(const Args& A, int u, i64 base, int lane, int wave, unsigned need,
+                                               int (&s)[K], int (&nx)[K]) {
     const int* off = A.offs[u];
-    const u8* by = A.bytes[u];
-    int s[K], e[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const i64 row = base + (i64)k * BLOCK + tid;
-        const bool in = row < A.n_rows;
-        s[k] = in ? off[row] : 0;
-        e[k] = in ? off[row + 1] : -1;
+        s[k] = 0;
+        nx[k] = 0;
+        if (!((need >> k) & 1)) continue;
+        const i64 r0 = base + (i64)k * BLOCK + 64 * wave;
+        const i64 row = r0 + lane;
+        s[k] = off[row < A.n_rows ? row : A.n_rows];
+        nx[k] = off[r0 + 64 < A.n_rows ? r0 + 64 : A.n_rows];
     }
+}
+
+// End offset of this lane's row (all lanes active).
+__device__ __forceinline__ int utf8_end(int s, int nx, int lane) {
+    const int d = next_lane(s);
+    return lane == 63 ? nx : d;
+}
+
+// `utf8 column u = literal` for the K rows of a tile whose offsets are in
+// s / e. Every equal-length candidate's first min(len, 4) bytes are fetched
+// as the (at most two) aligned words holding them, all in flight together;
+// only head matches (rare) compare the rest. Only words holding bytes of the
+// candidate are read.
+template <int BLOCK, int K>
+__device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, int lit, const int (&s)[K], const int (&nx)[K],
+                                                 int lane, bool (&res)[K]) {
+    const int len = A.str_len[lit];
+    const char* q = A.str + A.str_off[lit];
+    const u8* by = A.bytes[u];
     const int hn = len < 4 ? len : 4;
+    const unsigned hm = hn == 4 ? ~0u : ((1u << (8 * hn)) - 1u);
     unsigned qh = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
         if (i < hn) qh |= (unsigned)(u8)q[i] << (8 * i);
     unsigned h[K];
+    int e[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) e[k] = utf8_end(s[k], nx[k], lane);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        unsigned w = ~qh;
-        if (e[k] - s[k] == len) {
+        unsigned w = qh;
+        if (e[k] - s[k] == len && hn > 0) {
             const u8* p = by + s[k];
-            w = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (i < hn) w |= (unsigned)p[i] << (8 * i);
+            const int mis = (int)((u64)p & 3u);
+            const unsigned w0 = *at<unsigned>(p, -mis);
+            const unsigned w1 = *at<unsigned>(p, ((mis + hn - 1) & ~3) - mis);  // the word of byte hn-1
+            w = __builtin_amdgcn_alignbyte(w1, w0, (unsigned)mis);
         }
         h[k] = w;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        bool eq = e[k] - s[k] == len && h[k] == qh;
+        bool eq = e[k] - s[k] == len && (h[k] & hm) == qh;
         if (eq) {
             const u8* p = by + s[k];
             for (int i = hn; i < len; ++i)
@@ -404,7 +463,7 @@ template <int BLOCK, int K, int NCH>
 struct Tile {
     static constexpr int WAVES = BLOCK / 64;
     static constexpr int NW = K * WAVES;  // 64-row words per tile
-    static_assert(NW <= 64, "one wave scans the tile's words");
+    static_assert(NW <= 256, "one wave scans the tile's words (up to 4 per lane)");
     u64 cnt[NCH][NW];
     u64 excl[NCH][NW];
     u64 prefix[NCH];
@@ -423,7 +482,9 @@ __device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, 
     for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const u64 s = ch == 0 ? (u64)__builtin_popcountll(__ballot(cnt[0][k] != 0)) : wave_sum((u64)cnt[ch][k]);
+            // Utf8 byte counts of one slice fit 32 bits (an array holds < 2^31 bytes)
+            const u64 s = ch == 0 ? (u64)__builtin_popcountll(__ballot(cnt[0][k] != 0))
+                                  : (u64)__builtin_amdgcn_readlane(wave_incl_scan32(cnt[ch][k], lane), 63);
             if (lane == 0) T.cnt[ch][k * WAVES + wave] = s;
         }
     lds_sync();
@@ -431,10 +492,24 @@ __device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, 
         u64 packed = 0;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
-            const u64 c = lane < NW ? T.cnt[ch][lane] : 0ull;
-            const u64 incl = wave_incl_scan(c, lane);
-            if (lane < NW) T.excl[ch][lane] = incl - c;
-            const u64 agg = __shfl(incl, NW - 1, 64);
+            constexpr int NPL = (NW + 63) / 64;  // words per lane, contiguous
+            u64 c[NPL], tot = 0;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int w = lane * NPL + i;
+                c[i] = w < NW ? T.cnt[ch][w] : 0ull;
+                tot += c[i];
+            }
+            const u64 incl = wave_incl_scan(tot, lane);
+            u64 ex = incl - tot;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int w = lane * NPL + i;
+                if (w < NW) T.excl[ch][w] = ex;
+                ex += c[i];
+            }
+            const u64 agg = ((u64)__builtin_amdgcn_readlane((unsigned)(incl >> 32), 63) << 32) |
+                            __builtin_amdgcn_readlane((unsigned)incl, 63);
             if constexpr (NCH == 2) {
                 packed |= agg << (31 * ch);
             } else {
@@ -504,60 +579,165 @@ __device__ __forceinline__ void tile_offsets(const Args& A, Tile<BLOCK, K, NCH>&
 // of a chunk's loads are in flight before its stores (a byte-at-a-time
 // load->store loop pays one memory latency per byte).
 __device__ __forceinline__ void utf8_copy(const u8* src, u8* dst, unsigned L) {
-    const u64 sa = (u64)src, da = (u64)dst;
-    const u64 sw0 = sa & ~3ull, swl = (sa + L - 1) & ~3ull;
-    const u64 dw0 = da & ~3ull, dwe = (da + L + 3) & ~3ull;
-    for (u64 wb = dw0; wb < dwe; wb += 32) {
-        const i64 sb = (i64)sa + ((i64)wb - (i64)da);  // source address of output byte wb
-        const u64 sbw = (u64)sb & ~3ull;
-        const unsigned sh = (unsigned)sb & 3u;
+    const int sm = (int)((u64)src & 3u), dm = (int)((u64)dst & 3u);
+    // byte offsets relative to src / dst
+    const i64 sw0 = -sm, swl = (i64)((sm + (int)L - 1) & ~3) - sm;  // first / last source word holding bytes
+    const i64 dwe = (i64)((dm + (int)L + 3) & ~3) - dm;             // end of the last output word
+    for (i64 wb = -dm; wb < dwe; wb += 32) {  // output word at dst + wb, source byte src + wb
+        const i64 sbw = ((wb + sm) & ~3ll) - sm;
+        const unsigned sh = (unsigned)((wb + sm) & 3);
         unsigned sv[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
-            u64 a = sbw + 4ull * j;
+            i64 a = sbw + 4 * j;
             a = a < sw0 ? sw0 : (a > swl ? swl : a);
-            sv[j] = *(const unsigned*)a;
+            sv[j] = *at<unsigned>(src, a);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const u64 w = wb + 4ull * j;
-            if (w >= dwe) break;
+            const i64 p = wb + 4 * j;  // offset of the word's first byte in dst
+            if (p >= dwe) break;
             const unsigned val = __builtin_amdgcn_alignbyte(sv[j + 1], sv[j], sh);
-            const i64 p = (i64)w - (i64)da;  // offset of the word's first byte in dst
             if (p >= 0 && p + 4 <= (i64)L) {
-                *(unsigned*)w = val;
+                *at<unsigned>(dst, p) = val;
             } else {
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    if (p + b >= 0 && p + b < (i64)L) ((u8*)w)[b] = (u8)(val >> (8 * b));
+                    if (p + b >= 0 && p + b < (i64)L) dst[p + b] = (u8)(val >> (8 * b));
             }
         }
     }
 }
 
-// Copy the selected rows of Utf8 input u into output o (rebased i32
-// offsets + bytes, filter.rs:94-105).
+// Per-lane Utf8 gather: each selected lane copies its own string with
+// utf8_copy (diagnostic variant, DFMI_UTF8_GATHER=0).
 template <int BLOCK, int K, int NCH>
-__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
-                                            i64 base, unsigned selm, const unsigned (&len)[K],
-                                            const unsigned (&dst)[K], int lane, int wave) {
+__device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+                                                 unsigned selm, const unsigned (&dst)[K], const int (&s)[K],
+                                                 const int (&nx)[K], int lane, int wave) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const unsigned incl = wave_incl_scan32(len[k], lane);
-        if (!((selm >> k) & 1)) continue;
-        const i64 row = base + (i64)k * BLOCK + threadIdx.x;
-        const u64 ob = bpre + T.excl[ch][k * WAVES + wave] + (incl - len[k]);
+        const bool sel = (selm >> k) & 1;
+        const int e = utf8_end(s[k], nx[k], lane);  // every lane (DPP)
+        const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
+        const unsigned incl = wave_incl_scan32(L, lane);
+        if (!sel) continue;
+        const u64 ob = bpre + T.excl[ch][k * WAVES + wave] + (incl - L);
         A.out_offs[o][obase + dst[k]] = (int)ob;
-        if ((i64)(ob + len[k]) > A.out_cap[o]) {
+        if ((i64)(ob + L) > A.out_cap[o]) {
             report_err(A.err, 0, 0, ERRK_CAPACITY);
             continue;
         }
-        const unsigned L = len[k];
         if (L == 0) continue;
-        utf8_copy(A.bytes[u] + A.offs[u][row], A.out_data[o] + ob, L);
+        utf8_copy(A.bytes[u] + s[k], A.out_data[o] + ob, L);
+    }
+}
+
+// LDS staging of one wave's Utf8 gather (per 64-row slice).
+constexpr int kStageChunks = 128;  // 16-byte source chunks: 2 KiB per wave
+struct Utf8Stage {
+    uint4 src[kStageChunks];      // the slice's source span, whole aligned 16-byte chunks
+    uint4 dst[kStageChunks + 1];  // its output bytes, at their output address modulo 4
+};
+
+// Orders this wave's LDS accesses (a wave's LDS operations execute in
+// order; this keeps the compiler from moving them across).
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// Bytes [lo, hi) of a word as a mask (0 <= lo < hi <= 4).
+__device__ __forceinline__ unsigned byte_mask(int lo, int hi) {
+    return (0xffffffffu >> (8 * (4 - hi))) & (0xffffffffu << (8 * lo));
+}
+
+// Copy the selected rows of Utf8 input u into output o (rebased i32
+// offsets + bytes, filter.rs:94-105), one 64-row slice at a time, the wave
+// cooperating. The slice's source span (first to last selected string) is
+// read with coalesced 16-byte loads into LDS; each selected lane ORs its
+// string, assembled into aligned words with v_alignbyte, into a zeroed LDS
+// image of the slice's output (strings that share an edge word merge
+// there); the wave then stores the image as coalesced aligned words --
+// bytewise only the two edge words the slice shares with its neighbours. A
+// span over 2 KiB (long strings) falls back to a per-lane copy. Source reads
+// are whole aligned 16-byte chunks holding span bytes.
+template <int BLOCK, int K, int NCH>
+__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+                                            unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
+                                            const int (&s)[K], const int (&nx)[K], Utf8Stage& G, int lane,
+                                            int wave) {
+    constexpr int WAVES = BLOCK / 64;
+    const u64 bpre = T.prefix[ch];
+    const i64 obase = (i64)T.prefix[0];
+    const u8* src = A.bytes[u];
+    u8* out = A.out_data[o];
+    const unsigned* gs = (const unsigned*)G.src;
+    unsigned* gd = (unsigned*)G.dst;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const u64 m = wm[k];
+        if (!m) continue;
+        const bool sel = (selm >> k) & 1;
+        const int e = utf8_end(s[k], nx[k], lane);
+        const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
+        const unsigned incl = wave_incl_scan32(L, lane);
+        const unsigned rel = incl - L;
+        const unsigned Ls = __builtin_amdgcn_readlane(incl, 63);
+        const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
+        if (sel) A.out_offs[o][obase + dst[k]] = (int)(ob0 + rel);
+        if ((i64)(ob0 + Ls) > A.out_cap[o]) {
+            if (lane == 0) report_err(A.err, 0, 0, ERRK_CAPACITY);
+            continue;
+        }
+        if (Ls == 0) continue;
+        const int fl = __builtin_ctzll(m), ll = 63 - __builtin_clzll(m);
+        const i64 s0 = __builtin_amdgcn_readlane(s[k], fl), s1 = __builtin_amdgcn_readlane(e, ll);  // s1 > s0
+        const i64 sm = (i64)((u64)src & 15u);
+        const i64 c0 = ((s0 + sm) & ~15ll) - sm;  // offset of the 16-byte chunk holding byte s0, from src
+        const int nch = (int)(((s1 - 1 - c0) >> 4)) + 1;
+        if (nch > kStageChunks) {
+            if (sel && L) utf8_copy(src + s[k], out + ob0 + rel, L);
+            continue;
+        }
+        const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
+        u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word holding the slice's first byte
+        const int nw = (sh + (int)Ls + 3) >> 2;
+        for (int c = lane; c < nch; c += 64) G.src[c] = *at<uint4>(src, c0 + 16 * c);
+        for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_fence();
+        if (L) {
+            // this string: source bytes [a, a + L) of G.src, output bytes [d, d + L) of G.dst
+            const int a = (int)(s[k] - c0);
+            const int d = sh + (int)rel;
+            const int wl = (d + (int)L - 1) >> 2;
+            for (int w = d >> 2; w <= wl; ++w) {
+                const int p = 4 * w - d;   // position of the word's first byte in the string (>= -3)
+                const int sb = a + p;      // ... in G.src (>= -3)
+                const int sw = sb >> 2;    // arithmetic shift: -1 at most
+                const unsigned lo = gs[sw < 0 ? 0 : sw], hi = gs[sw + 1];
+                const unsigned val = __builtin_amdgcn_alignbyte(hi, lo, (unsigned)sb & 3u);
+                const unsigned msk = byte_mask(p < 0 ? -p : 0, p + 4 > (int)L ? (int)L - p : 4);
+                __hip_atomic_fetch_or(gd + w, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+        }
+        wave_lds_fence();
+        for (int j = lane; j < nw; j += 64) {
+            const unsigned val = gd[j];
+            const int p = 4 * j - sh;  // output position of the word's first byte
+            if (p >= 0 && p + 4 <= (int)Ls) {
+                *at<unsigned>(w0, 4 * j) = val;
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (p + b >= 0 && p + b < (int)Ls) w0[4 * j + b] = (u8)(val >> (8 * b));
+            }
+        }
+        wave_lds_fence();
     }
 }
 

@@ -10,6 +10,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     constexpr int BLOCK = 512, K = 8, WAVES = BLOCK / 64, NCH = 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);
     __shared__ dfmi::Tile<BLOCK, K, NCH> T;
+    __shared__ dfmi::Utf8Stage G[WAVES];
     const unsigned tile = blockIdx.x;
     const i64 base = (i64)tile * (BLOCK * K);
     const i64 rem = A.n_rows - base;
@@ -20,14 +21,17 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
         const i64 row = base + k * BLOCK + tid;
         selm |= (unsigned)(row < A.n_rows && dfmi::f64(c0[k]) > dfmi::f64(A.lits[0])) << k;
     }
-    unsigned cnt[NCH][K], len0[K];
+    unsigned cnt[NCH][K];
     u64 wm[K];
+    int us[K], ue[K];
+    bool eq[K];
+    dfmi::utf8_offs_tile<BLOCK, K>(A, 0, base, lane, wave, ~0u, us, ue);
+    dfmi::utf8_eq_lit_tile<BLOCK, K>(A, 0, 0, us, ue, lane, eq);
     for (int k = 0; k < K; ++k) {
-        const i64 row = base + k * BLOCK + tid;
+        selm |= (unsigned)eq[k] << k;
         wm[k] = __ballot((selm >> k) & 1);
         cnt[0][k] = (selm >> k) & 1;
-        len0[k] = ((selm >> k) & 1) ? (unsigned)(A.offs[0][row + 1] - A.offs[0][row]) : 0u;
-        cnt[1][k] = len0[k];
+        cnt[1][k] = ((selm >> k) & 1) ? (unsigned)(dfmi::utf8_end(us[k], ue[k], lane) - us[k]) : 0u;
     }
     dfmi::tile_offsets<BLOCK, K, NCH, 4, 2, 16>(A, T, tile, cnt, lane, wave);
     const i64 obase = (i64)T.prefix[0];
@@ -35,7 +39,8 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);
     for (int k = 0; k < K; ++k)
         if ((selm >> k) & 1) ((u64*)A.out[0] + obase)[dst[k]] = c0[k];
-    dfmi::utf8_gather<BLOCK, K, NCH>(A, T, 1, 0, 1, base, selm, len0, dst, lane, wave);
+    dfmi::utf8_gather<BLOCK, K, NCH>(A, T, 1, 0, 1, selm, wm, dst, us, ue, G[wave], lane, wave);
+    dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, 1, 0, 1, selm, dst, us, ue, lane, wave);
     const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0) &&
                    dfmi::utf8_eq_col(A, 0, 1, base) && dfmi::utf8_valid(A, 0, base);
     if (b) dfmi::report_err(A.err, 1, base, dfmi::ERRK_DIV_ZERO);

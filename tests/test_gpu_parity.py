@@ -314,6 +314,37 @@ def test_utf8_many_tiles():
                  DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
+def test_utf8_multi_channel_many_tiles():
+    """Three Utf8 outputs (one look-back channel each, plus rows) over ~100
+    tiles: short dictionary words (LDS-staged slices), long strings (slices
+    whose source span exceeds the 2 KiB stage: per-lane copy), a string longer
+    than the stage itself, empty strings and nulls; equality predicates on a
+    nullable column with the offsets shared by predicate and gather."""
+    n = 400_003
+    rng = np.random.default_rng(77)
+    short = [bytes(rng.integers(97, 123, int(rng.integers(0, 25))).astype(np.uint8)) for _ in range(1000)]
+    short[17] = b"w17dizjxms"
+    longw = [bytes(rng.integers(32, 127, int(rng.integers(20, 300))).astype(np.uint8)) for _ in range(50)]
+    longw[3] = b"L" * 5000
+    s0 = [short[i] for i in rng.integers(0, len(short), n)]
+    s0v = [None if rng.random() < 0.07 else x for x in s0]
+    s1 = [longw[i] if rng.random() < 0.3 else short[j] for i, j in zip(rng.integers(0, len(longw), n),
+                                                                         rng.integers(0, len(short), n))]
+    s2 = [short[i] for i in rng.integers(0, len(short), n)]
+    v = gen_unit_f64(8, 0, 0, n)
+    s = Schema([Field("a", DataType.Utf8, True), Field("b", DataType.Utf8, False), Field("c", DataType.Utf8, False),
+                Field("v", DataType.Float64, True)])
+    b = RecordBatch(s, [Array.from_strings(s0v), Array.from_strings(s1), Array.from_strings(s2),
+                        Array.from_numpy(DataType.Float64, v, rng.random(n) >= 0.1)])
+    for k in (0.002, 0.5, 0.99):
+        run_both(s, b, BinaryExpr(Column(3), Operator.Lt, Literal(Float64(k))), [Column(0), Column(1), Column(2), Column(3)])
+    run_both(s, b, BinaryExpr(Column(3), Operator.Lt, Literal(Float64(0.6))), [Column(2), Column(0)])
+    for w, c in (("w17dizjxms", 0), (short[5].decode(), 2), ("", 0)):
+        run_both(s, b, BinaryExpr(Column(c), Operator.Eq, Literal(Utf8(w))), [Column(1), Column(0), Column(3)],
+                 DFMI_FLAG_EXT_UTF8_COMPARE)
+        run_both(s, b, BinaryExpr(Column(c), Operator.NotEq, Literal(Utf8(w))), [Column(c)], DFMI_FLAG_EXT_UTF8_COMPARE)
+
+
 def test_host_batch_many_staging_chunks():
     """dfmi_filter_project_host over a batch larger than the two 64 MB pinned
     staging chunks (H2D 20 chunks, D2H 10 per output): identical to the
