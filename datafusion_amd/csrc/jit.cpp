@@ -471,7 +471,7 @@ std::string generate(const Plan& P, Launch& X) {
                 }
             }
             // projection-only columns, loaded only where selected
-            emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
+            if (!X.late_proj) emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
             // compaction offsets (rows + Utf8 bytes)
             o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
               << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
@@ -484,6 +484,9 @@ std::string generate(const Plan& P, Launch& X) {
             {
                 o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << tparams << ">(A, " << T << ", t, cnt, lane, wave);\n";
             }
+            // byte-light predicates: projection-only columns after the look-back
+            // (fewer registers held across it; few rows are selected)
+            if (X.late_proj) emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
             o << "  const i64 obase = (i64)" << T << ".prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
               << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)" << T
               << ".excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
@@ -630,7 +633,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, os.out_type);
         put(k, (char)os.nullable);
     }
-    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather};
+    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather, X.late_proj};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -46,6 +46,7 @@ struct Launch {
     // predecessors read per poll, one lane each: 8 measured best at s=0.5
     // (64 cost ~9% of the C2 kernel in polling traffic)
     int window = 8;
+    int late_proj = 0;  // projection-only columns loaded after the look-back (byte-light predicates)
     int gather = 1;  // Utf8 gather: 1 = wave-cooperative LDS staging, 0 = per-lane copy (diagnostics)
     // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores
     int nt = 0;

@@ -264,10 +264,15 @@ __device__ __forceinline__ void utf8_offs_tile(const Args& A, int u, i64 base, i
         s[k] = 0;
         nx[k] = 0;
         if (!((need >> k) & 1)) continue;
-        const i64 r0 = base + (i64)k * BLOCK + 64 * wave;
-        const i64 row = r0 + lane;
-        s[k] = off[row < A.n_rows ? row : A.n_rows];
-        nx[k] = off[r0 + 64 < A.n_rows ? r0 + 64 : A.n_rows];
+        const i64 r0 = base + (i64)k * BLOCK + 64 * wave;  // wave-uniform
+        const int* o0 = off + r0;                           // (uniform base + lane offset addressing)
+        if (r0 + 64 <= A.n_rows) {
+            s[k] = o0[lane];
+            nx[k] = o0[64];
+        } else {
+            s[k] = off[r0 + lane < A.n_rows ? r0 + lane : A.n_rows];
+            nx[k] = off[A.n_rows];
+        }
     }
 }
 
@@ -290,6 +295,7 @@ __device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, int lit, 
     const u8* by = A.bytes[u];
     const int hn = len < 4 ? len : 4;
     const unsigned hm = hn == 4 ? ~0u : ((1u << (8 * hn)) - 1u);
+    const unsigned bmis = (unsigned)((u64)by & 3u);
     unsigned qh = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -302,11 +308,12 @@ __device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, int lit, 
     for (int k = 0; k < K; ++k) {
         unsigned w = qh;
         if (e[k] - s[k] == len && hn > 0) {
-            const u8* p = by + s[k];
-            const int mis = (int)((u64)p & 3u);
-            const unsigned w0 = *at<unsigned>(p, -mis);
-            const unsigned w1 = *at<unsigned>(p, ((mis + hn - 1) & ~3) - mis);  // the word of byte hn-1
-            w = __builtin_amdgcn_alignbyte(w1, w0, (unsigned)mis);
+            // 32-bit unsigned offsets from the uniform base (offsets are >= 0)
+            const unsigned sk = (unsigned)s[k];
+            const unsigned mis = (sk + bmis) & 3u;
+            const unsigned w0 = *at<unsigned>(by, sk - mis);
+            const unsigned w1 = *at<unsigned>(by, sk - mis + ((mis + (unsigned)hn - 1u) & ~3u));  // the word of byte hn-1
+            w = __builtin_amdgcn_alignbyte(w1, w0, mis);
         }
         h[k] = w;
     }
@@ -707,7 +714,8 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
         const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
         u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word holding the slice's first byte
         const int nw = (sh + (int)Ls + 3) >> 2;
-        for (int c = lane; c < nch; c += 64) G.src[c] = *at<uint4>(src, c0 + 16 * c);
+        const uint4* sp = at<uint4>(src, c0);  // wave-uniform
+        for (int c = lane; c < nch; c += 64) G.src[c] = sp[c];
         for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_fence();
         if (L) {
