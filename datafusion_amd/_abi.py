@@ -30,6 +30,13 @@ DFMI_FLAG_EXT_GATHER_ALL = 0x1
 DFMI_FLAG_EXT_UTF8_COMPARE = 0x2
 DFMI_FLAG_EXT_CAST = 0x4
 DFMI_FLAG_EXT_IS_NULL = 0x8
+DFMI_FLAG_EXT_AGGREGATE = 0x10
+
+# dfmi_agg_fn (AggregateType, expression.rs:33-40)
+DFMI_AGG_MIN = 0
+DFMI_AGG_MAX = 1
+DFMI_AGG_SUM = 2
+DFMI_AGG_COUNT = 3
 
 STATUS_NAMES = {
     DFMI_ERR_EXECUTION: "ExecutionError",
@@ -106,6 +113,10 @@ class dfmi_out_column(C.Structure):
     ]
 
 
+class dfmi_agg_value(C.Structure):
+    _fields_ = [("type", C.c_int32), ("is_null", C.c_int32), ("count", C.c_int64), ("bits", C.c_uint64)]
+
+
 # Every symbol include/dfmi.h declares (checked by the CPU test suite).
 EXPORTED = [
     "dfmi_compile_scalar_expr",
@@ -122,6 +133,17 @@ EXPORTED = [
     "dfmi_host_result_free",
     "dfmi_last_timing",
     "dfmi_last_compile_ms",
+    "dfmi_compile_aggregate",
+    "dfmi_aggregate_name",
+    "dfmi_aggregate_type",
+    "dfmi_aggregate_free",
+    "dfmi_agg_state_create",
+    "dfmi_aggregate_batch",
+    "dfmi_agg_state_finish",
+    "dfmi_agg_partial_bytes",
+    "dfmi_agg_state_partial",
+    "dfmi_agg_merge_partials",
+    "dfmi_agg_state_free",
     "dfmi_generate_column",  # include/dfmi_datasource.h
 ]
 
@@ -214,5 +236,29 @@ def lib() -> C.CDLL:
     L.dfmi_generate_column.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_void_p, C.POINTER(dfmi_error)]
     L.dfmi_generate_column.restype = C.c_int32
+    P = C.POINTER
+    L.dfmi_compile_aggregate.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_uint32, P(C.c_void_p), P(dfmi_error)]
+    L.dfmi_compile_aggregate.restype = C.c_int32
+    L.dfmi_aggregate_name.argtypes = [C.c_void_p]
+    L.dfmi_aggregate_name.restype = C.c_char_p
+    L.dfmi_aggregate_type.argtypes = [C.c_void_p]
+    L.dfmi_aggregate_type.restype = C.c_int32
+    L.dfmi_aggregate_free.argtypes = [C.c_void_p]
+    L.dfmi_aggregate_free.restype = None
+    L.dfmi_agg_state_create.argtypes = [C.c_void_p, P(C.c_void_p), C.c_int32, P(C.c_void_p), P(dfmi_error)]
+    L.dfmi_agg_state_create.restype = C.c_int32
+    L.dfmi_aggregate_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(dfmi_batch), C.c_uint32, P(dfmi_error)]
+    L.dfmi_aggregate_batch.restype = C.c_int32
+    L.dfmi_agg_state_finish.argtypes = [C.c_void_p, C.c_void_p, P(dfmi_agg_value), P(dfmi_error)]
+    L.dfmi_agg_state_finish.restype = C.c_int32
+    L.dfmi_agg_partial_bytes.argtypes = [C.c_void_p]
+    L.dfmi_agg_partial_bytes.restype = C.c_int64
+    L.dfmi_agg_state_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(dfmi_error)]
+    L.dfmi_agg_state_partial.restype = C.c_int32
+    L.dfmi_agg_merge_partials.argtypes = [P(C.c_void_p), C.c_int32, P(C.c_void_p), C.c_int32, P(dfmi_agg_value),
+                                          P(dfmi_error)]
+    L.dfmi_agg_merge_partials.restype = C.c_int32
+    L.dfmi_agg_state_free.argtypes = [C.c_void_p]
+    L.dfmi_agg_state_free.restype = None
     _LIB = L
     return L

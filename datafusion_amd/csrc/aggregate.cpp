@@ -1,0 +1,591 @@
+// Aggregate extension (DFMI_FLAG_EXT_AGGREGATE): host side of the fused
+// Selection + Aggregate pass with no GROUP BY.
+//
+// The reference plans `SELECT SUM(e), ... FROM t [WHERE p]` as
+// Aggregate(Selection?(TableScan)) (sqlplanner.rs:91-117), compiles each
+// AggregateFunction with compile_expr (expression.rs:81-116) and then stops:
+// ExecutionContext::execute has no Aggregate arm (context.rs:161
+// `unimplemented!()`). Here every input batch is one launch of a
+// query-compiled kernel (jit.cpp generate_agg): predicate, argument and
+// reduction fused, partials accumulated in device memory across batches; the
+// host merges the accumulator copies exactly and rounds once at the end.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "exec_internal.h"
+#include "jit_skeleton.hip"
+
+using namespace dfmi;
+using namespace dfmi::xi;
+
+struct dfmi_aggregate {
+    std::string name;  // as spelled in the SQL text (the Field name, sqlplanner.rs:385-389)
+    int fn = 0;        // dfmi_agg_fn
+    int ret_type = 0;
+    dfmi_program arg;  // compile_expr's compiled argument (a copy: same uid, same kernels)
+};
+
+struct dfmi_agg_state {
+    int device = 0;
+    std::vector<const dfmi_aggregate*> aggs;
+    uint64_t* acc = nullptr;  // [kAggCopies][n][kAggWords]
+    size_t acc_words = 0;
+    bool failed = false;      // a batch raised an error: the query has failed
+    dfmi_error failure{};
+};
+
+namespace {
+
+int agg_fn_of(const std::string& name) {
+    std::string l = name;
+    for (auto& c : l) c = (char)tolower((unsigned char)c);
+    if (l == "min") return DFMI_AGG_MIN;
+    if (l == "max") return DFMI_AGG_MAX;
+    if (l == "count") return DFMI_AGG_COUNT;
+    if (l == "sum") return DFMI_AGG_SUM;
+    return -1;
+}
+
+bool is_float_type(int t) { return t == DFMI_TYPE_FLOAT32 || t == DFMI_TYPE_FLOAT64; }
+
+// ---- exact merge of accumulator copies (host)
+// One aggregate's merged state: the layout of a device copy with the float
+// digits carry-normalised (every digit but the top in [0, 2^32)).
+struct Partial {
+    uint64_t count = 0, flags = 0, key = 0, isum = 0;
+    int64_t limbs[kAggLimbs] = {};
+};
+
+void merge_into(Partial& p, const uint64_t* w, bool is_min) {
+    p.count += w[0];
+    if ((w[1] & AGGF_VALUE)) {
+        if (!(p.flags & AGGF_VALUE)) p.key = w[2];
+        else p.key = is_min ? std::min(p.key, w[2]) : std::max(p.key, w[2]);
+    }
+    p.flags |= w[1];
+    p.isum += w[3];
+    for (int i = 0; i < kAggLimbs; ++i) p.limbs[i] += (int64_t)w[4 + i];
+}
+
+void normalize(Partial& p) {
+    for (int i = 0; i < kAggLimbs - 1; ++i) {
+        const int64_t c = p.limbs[i] >> 32;  // floor division by 2^32
+        p.limbs[i] -= c * 4294967296ll;
+        p.limbs[i + 1] += c;
+    }
+}
+
+// The exact sum (normalised digits, units of 2^-1074) rounded half-to-even
+// to a format of `prec` significand bits whose quantum is at least
+// 2^(qmin-1074); `zero` when the exact sum is 0. Result as a double (exact
+// for Float32 results).
+double round_exact(const Partial& p, int prec, int qmin, double overflow_limit, bool* zero) {
+    // magnitude digits (two's complement negation of the digit string)
+    int64_t d[kAggLimbs];
+    const bool neg = p.limbs[kAggLimbs - 1] < 0;
+    if (!neg) {
+        memcpy(d, p.limbs, sizeof d);
+    } else {
+        int64_t borrow = 0;
+        for (int i = 0; i < kAggLimbs; ++i) {
+            int64_t v = -p.limbs[i] - borrow;
+            borrow = 0;
+            if (i < kAggLimbs - 1 && v < 0) {
+                v += 4294967296ll;
+                borrow = 1;
+            }
+            d[i] = v;
+        }
+    }
+    int top = -1;
+    for (int i = kAggLimbs - 1; i >= 0; --i)
+        if (d[i]) {
+            top = i;
+            break;
+        }
+    *zero = top < 0;
+    if (top < 0) return 0.0;
+    auto bit = [&](int i) -> uint64_t { return i < 0 ? 0 : ((uint64_t)d[i >> 5] >> (i & 31)) & 1; };
+    int msb = 32 * top;  // highest set bit (digits < 2^32 after normalisation)
+    for (int b = 31; b >= 0; --b)
+        if (((uint64_t)d[top] >> b) & 1) {
+            msb = 32 * top + b;
+            break;
+        }
+    int q = std::max(msb - (prec - 1), qmin);
+    uint64_t mant = 0;
+    for (int i = msb; i >= q; --i) mant = (mant << 1) | bit(i);
+    const uint64_t rb = q >= 1 ? bit(q - 1) : 0;
+    bool sticky = false;
+    for (int i = q - 2; i >= 0 && !sticky; --i) sticky = bit(i);
+    if (rb && (sticky || (mant & 1))) {
+        ++mant;
+        if (mant >> prec) {
+            mant >>= 1;
+            ++q;
+        }
+    }
+    double v = std::ldexp((double)mant, q - 1074);
+    if (v >= overflow_limit) v = HUGE_VAL;
+    return neg ? -v : v;
+}
+
+uint64_t key_to_bits(uint64_t key, int t) {
+    switch (t) {
+        case DFMI_TYPE_FLOAT64: return (key >> 63) ? (key & ~(1ull << 63)) : ~key;
+        case DFMI_TYPE_FLOAT32: {
+            const uint32_t k = (uint32_t)key;
+            return (k >> 31) ? (uint64_t)(k & 0x7fffffffu) : (uint64_t)(uint32_t)~k;
+        }
+        case DFMI_TYPE_INT8: case DFMI_TYPE_INT16: case DFMI_TYPE_INT32: case DFMI_TYPE_INT64:
+            return key ^ (1ull << 63);  // the value sign-extended to 64 bits
+        default: return key;
+    }
+}
+
+uint64_t narrow_int(uint64_t v, int t) {
+    switch (t) {
+        case DFMI_TYPE_INT8: return (uint64_t)(int64_t)(int8_t)v;
+        case DFMI_TYPE_INT16: return (uint64_t)(int64_t)(int16_t)v;
+        case DFMI_TYPE_INT32: return (uint64_t)(int64_t)(int32_t)v;
+        case DFMI_TYPE_UINT8: return v & 0xffull;
+        case DFMI_TYPE_UINT16: return v & 0xffffull;
+        case DFMI_TYPE_UINT32: return v & 0xffffffffull;
+        default: return v;
+    }
+}
+
+dfmi_agg_value finish_one(const dfmi_aggregate& a, Partial p) {
+    normalize(p);
+    dfmi_agg_value r;
+    r.type = a.ret_type;
+    r.count = (int64_t)p.count;
+    r.is_null = 0;
+    r.bits = 0;
+    const int t = a.arg.type;
+    if (a.fn == DFMI_AGG_COUNT) {
+        r.bits = p.count;
+        return r;
+    }
+    if (p.count == 0) {
+        r.is_null = 1;
+        return r;
+    }
+    const bool f32 = t == DFMI_TYPE_FLOAT32;
+    const uint64_t qnan = f32 ? 0x7FC00000ull : 0x7FF8000000000000ull;
+    if (a.fn == DFMI_AGG_SUM) {
+        if (!is_float_type(t)) {
+            r.bits = narrow_int(p.isum, t);
+        } else if ((p.flags & AGGF_NAN) || ((p.flags & AGGF_PINF) && (p.flags & AGGF_NINF))) {
+            r.bits = qnan;
+        } else if (p.flags & (AGGF_PINF | AGGF_NINF)) {
+            const bool pos = p.flags & AGGF_PINF;
+            r.bits = f32 ? (pos ? 0x7F800000ull : 0xFF800000ull) : (pos ? 0x7FF0000000000000ull : 0xFFF0000000000000ull);
+        } else {
+            bool zero = false;
+            double v = f32 ? round_exact(p, 24, 925, 0x1p128, &zero) : round_exact(p, 53, 0, HUGE_VAL, &zero);
+            if (zero) v = (p.flags & AGGF_NONNEGZERO) ? 0.0 : -0.0;
+            if (f32) {
+                const float fv = (float)v;
+                uint32_t b;
+                memcpy(&b, &fv, 4);
+                r.bits = b;
+            } else {
+                memcpy(&r.bits, &v, 8);
+            }
+        }
+        return r;
+    }
+    // MIN / MAX
+    r.bits = (p.flags & AGGF_VALUE) ? key_to_bits(p.key, t) : qnan;
+    return r;
+}
+
+// Static errors, slots and tile shape of one aggregate batch (the filtered
+// form of exec.cpp's build_plan: FilterRelation::next, then each argument
+// over the filtered batch in aggregate order).
+struct AggBuilt {
+    Err se;
+    jit::Plan plan;
+    jit::Launch X;
+    int64_t n_tiles = 0;
+};
+
+void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in, uint32_t flags,
+                    AggBuilt& B) {
+    Err& se = B.se;
+    jit::Launch& X = B.X;
+    const int64_t n = in->num_rows;
+    const int ncols = in->num_columns;
+    auto check_schema = [&](const dfmi_program* p) {
+        if ((int)p->schema_types.size() != ncols)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch does not match the compiled schema"};
+        for (int i = 0; i < ncols; ++i)
+            if (p->schema_types[i] != in->columns[i].type)
+                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch column type does not match the schema"};
+    };
+    if (pred) check_schema(pred);
+    for (const dfmi_aggregate* a : st->aggs) check_schema(&a->arg);
+    for (int i = 0; i < ncols; ++i)
+        if (in->columns[i].length != n) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
+    const int P = pred ? pred->length : 0;
+    if (pred) {
+        for (const IrNode& nd : pred->ir)
+            if (nd.rt_code) se.offer((uint64_t)nd.ordinal << 44, nd.rt_code, nd.rt_msg);
+        if (pred->type != DFMI_TYPE_BOOLEAN)
+            se.offer((uint64_t)P << 44, DFMI_ERR_EXECUTION, "Filter expression did not evaluate to boolean");
+        for (int i = 0; i < ncols; ++i)
+            if (!gatherable(in->columns[i].type, flags)) {
+                se.offer((uint64_t)(P + 1) << 44, DFMI_ERR_EXECUTION,
+                         std::string("filter not supported for ") + type_debug(in->columns[i].type));
+                break;
+            }
+    }
+    int base = P + 2, nf = 0;
+    for (const dfmi_aggregate* a : st->aggs) {
+        for (const IrNode& nd : a->arg.ir)
+            if (nd.rt_code) se.offer((uint64_t)(base + nd.ordinal) << 44, nd.rt_code, nd.rt_msg);
+        jit::AggSpec s;
+        s.fn = a->fn;
+        s.prog = &a->arg;
+        s.ord_base = base;
+        s.arg_type = a->arg.type;
+        if (a->fn == DFMI_AGG_SUM && is_float_type(a->arg.type)) s.fslot = nf++;
+        B.plan.aggs.push_back(s);
+        base += a->arg.length;
+    }
+    if (base >= (1 << 19)) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: expressions too long"};
+    if (nf > 4) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 4 floating-point SUMs"};
+    B.plan.pred = pred;
+    X.in = in;
+    auto reg_num = [&](int col, std::vector<int>& phase) {
+        for (size_t i = 0; i < X.num_cols.size(); ++i)
+            if (X.num_cols[i] == col) return;
+        X.num_cols.push_back(col);
+        phase.push_back((int)X.num_cols.size() - 1);
+    };
+    auto reg_prog = [&](const dfmi_program* p, std::vector<int>& phase) {
+        for (const IrNode& nd : p->ir) {
+            if (nd.kind != IR_COL) continue;
+            if (nd.type == DFMI_TYPE_UTF8) {
+                bool have = false;
+                for (int c : X.utf8_cols) have |= c == nd.col;
+                if (!have) X.utf8_cols.push_back(nd.col);
+            } else if (jit::type_width(nd.type) || nd.type == DFMI_TYPE_BOOLEAN) {
+                reg_num(nd.col, phase);
+            }
+        }
+    };
+    if (pred) reg_prog(pred, X.pred_slots);
+    for (const dfmi_aggregate* a : st->aggs) reg_prog(&a->arg, X.proj_slots);
+    if ((int)X.num_cols.size() > kArgCols || X.utf8_cols.size() > (size_t)kArgUtf8)
+        throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many input columns"};
+    const size_t nload = X.num_cols.size();
+    X.BLOCK = 512;
+    X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
+    if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
+    if (X.K < 1 || X.K > 32) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
+    const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
+    B.n_tiles = (n + tile_rows - 1) / tile_rows;
+    if (B.n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
+}
+
+std::vector<Partial> merge_copies(const dfmi_agg_state* st, const std::vector<uint64_t>& h) {
+    const size_t n = st->aggs.size();
+    std::vector<Partial> parts(n);
+    for (size_t j = 0; j < n; ++j) {
+        const bool is_min = st->aggs[j]->fn == DFMI_AGG_MIN;
+        for (int c = 0; c < kAggCopies; ++c) merge_into(parts[j], &h[((size_t)c * n + j) * kAggWords], is_min);
+        normalize(parts[j]);
+    }
+    return parts;
+}
+
+std::vector<uint64_t> read_acc(dfmi_context* ctx, dfmi_agg_state* st) {
+    std::vector<uint64_t> h(st->acc_words);
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpyAsync(h.data(), st->acc, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return h;
+}
+
+}  // namespace
+
+extern "C" int32_t dfmi_compile_aggregate(const char* name, const dfmi_program* arg, int32_t return_type,
+                                          uint32_t flags, dfmi_aggregate** out, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!name || !arg || !out) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        // ExecutionContext::execute has no Aggregate arm (context.rs:161)
+        if (!(flags & DFMI_FLAG_EXT_AGGREGATE)) throw Fail{DFMI_ERR_PANIC, "not yet implemented"};
+        const int fn = agg_fn_of(name);  // compile_expr's match (expression.rs:100-106)
+        if (fn < 0) throw Fail{DFMI_ERR_PANIC, std::string("not yet implemented: Unsupported aggregate function '") + name + "'"};
+        const int want = fn == DFMI_AGG_COUNT ? DFMI_TYPE_UINT64 : arg->type;  // sqlplanner.rs:296-330
+        if (return_type != want) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "aggregate return type does not match the planner's"};
+        if (fn != DFMI_AGG_COUNT && !is_numeric_type(arg->type))
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("aggregate over ") + type_debug(arg->type)};
+        dfmi_aggregate* a = new (std::nothrow) dfmi_aggregate();
+        if (!a) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "out of memory"};
+        a->name = name;
+        a->fn = fn;
+        a->ret_type = return_type;
+        a->arg = *arg;
+        *out = a;
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" const char* dfmi_aggregate_name(const dfmi_aggregate* a) { return a ? a->name.c_str() : ""; }
+extern "C" int32_t dfmi_aggregate_type(const dfmi_aggregate* a) { return a ? a->ret_type : 0; }
+extern "C" void dfmi_aggregate_free(dfmi_aggregate* a) { delete a; }
+
+extern "C" int32_t dfmi_agg_state_create(dfmi_context* ctx, const dfmi_aggregate* const* aggs, int32_t n,
+                                         dfmi_agg_state** out, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    dfmi_agg_state* st = nullptr;
+    try {
+        if (!ctx || !out || n <= 0 || !aggs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        if (n > 16) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 16 aggregates"};
+        st = new dfmi_agg_state();
+        st->device = ctx->device;
+        for (int j = 0; j < n; ++j) {
+            if (!aggs[j]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL aggregate"};
+            st->aggs.push_back(aggs[j]);
+        }
+        st->acc_words = (size_t)kAggCopies * n * kAggWords;
+        std::vector<uint64_t> init(st->acc_words, 0);
+        for (int c = 0; c < kAggCopies; ++c)
+            for (int j = 0; j < n; ++j)
+                if (aggs[j]->fn == DFMI_AGG_MIN) init[((size_t)c * n + j) * kAggWords + 2] = ~0ull;
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipMalloc((void**)&st->acc, st->acc_words * 8));
+        HIP_TRY(hipMemcpyAsync(st->acc, init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        *out = st;
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        if (st) {
+            if (st->acc) (void)hipFree(st->acc);
+            delete st;
+        }
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" void dfmi_agg_state_free(dfmi_agg_state* st) {
+    if (!st) return;
+    if (st->acc) {
+        (void)hipSetDevice(st->device);
+        (void)hipFree(st->acc);
+    }
+    delete st;
+}
+
+extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_program* pred,
+                                        const dfmi_batch* in, uint32_t flags, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st || !in || (in->num_columns > 0 && !in->columns))
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return st->failure.code;
+        }
+        AggBuilt B;
+        try {
+            build_agg_plan(st, pred, in, flags, B);
+        } catch (const Fail& f) {
+            if (f.code == DFMI_ERR_NOT_IMPLEMENTED && B.se.set) throw Fail{B.se.code, B.se.msg};
+            throw;
+        }
+        Err& se = B.se;
+        const int64_t n = in->num_rows;
+        HIP_TRY(hipSetDevice(ctx->device));
+        hipStream_t stream = ctx->stream;
+        ctx->timed = false;
+        ctx->last_compile_ms = 0;
+        uint64_t dev_key = ~0ull;
+        int dev_kind = 0;
+        if (n > 0) {
+            hipFunction_t fn;
+            try {
+                fn = jit::get_kernel(ctx->device, B.plan, B.X, &ctx->last_compile_ms);
+            } catch (const Fail& f) {
+                if (se.set) throw Fail{se.code, se.msg};
+                throw;
+            }
+            jit::Launch& X = B.X;
+            Args A;
+            memset(&A, 0, sizeof A);
+            A.n_rows = n;
+            A.n_tiles = (int)B.n_tiles;
+            for (size_t s = 0; s < X.num_cols.size(); ++s) {
+                const dfmi_column& c = in->columns[X.num_cols[s]];
+                if (!c.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
+                const int w = jit::type_width(c.type);
+                if (w && ((uintptr_t)c.values & (w - 1)))
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values must be aligned to their width"};
+                A.col[s] = c.values;
+                A.valid[s] = (c.validity && c.null_count > 0) ? c.validity : nullptr;
+            }
+            for (size_t u = 0; u < X.utf8_cols.size(); ++u) {
+                const dfmi_column& c = in->columns[X.utf8_cols[u]];
+                if (!c.values || !c.offsets) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 column buffers are NULL"};
+                A.offs[u] = c.offsets;
+                A.bytes[u] = (const u8*)c.values;
+                A.svalid[u] = (c.validity && c.null_count > 0) ? c.validity : nullptr;
+            }
+            memcpy(A.lits, X.args_lits, sizeof A.lits);
+            memcpy(A.str_off, X.str_off, sizeof A.str_off);
+            memcpy(A.str_len, X.str_len, sizeof A.str_len);
+            memcpy(A.str, X.str, sizeof A.str);
+            const WsLease ws = ws_acquire(ctx, 0, stream);
+            A.err = (unsigned long long*)(ws.hdr + kHdrErr);
+            A.totals = (unsigned long long*)(ws.hdr + kHdrTotals);
+            A.ticket = (unsigned*)(ws.hdr + kHdrTicket);
+            A.stats = (unsigned long long*)(ws.hdr + kHdrStats);
+            A.clear_status = (unsigned long long*)ws.clear_status;
+            A.clear_words = ws.clear_words;
+            A.clear_hdr = (unsigned long long*)ws.clear_hdr;
+            A.agg = (unsigned long long*)st->acc;
+            HIP_TRY(hipEventRecord(ctx->ev0, stream));
+            size_t asz = sizeof A;
+            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+            HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)B.n_tiles, 1, 1, X.BLOCK, 1, 1, 0, stream, nullptr, cfg));
+            ws_commit(ctx, ws);
+            HIP_TRY(hipEventRecord(ctx->ev1, stream));
+            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, ws.hdr, kHdrAlloc, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipEventRecord(ctx->ev2, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            uint64_t ew;
+            memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
+            if (ew) {
+                dev_key = ~ew;
+                dev_kind = (int)(dev_key & 15);
+                dev_key &= ~15ull;
+            }
+            float m1 = 0, m2 = 0;
+            (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
+            (void)hipEventElapsedTime(&m2, ctx->ev0, ctx->ev2);
+            ctx->last_main_ms = m1;
+            ctx->last_total_ms = m2;
+            ctx->timed = true;
+        }
+        Fail fail{DFMI_OK, ""};
+        if (dev_kind && (!se.set || dev_key < se.key))
+            fail = dev_kind == ERRK_DIV_ZERO ? Fail{DFMI_ERR_DIVIDE_BY_ZERO, "DivideByZero"}
+                                             : Fail{DFMI_ERR_PANIC, "attempt to divide with overflow"};
+        else if (se.set)
+            fail = Fail{se.code, se.msg};
+        if (fail.code != DFMI_OK) {
+            // the query has failed (the state holds partial sums of this batch)
+            st->failed = true;
+            set_err(&st->failure, fail.code, fail.msg);
+            throw fail;
+        }
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_state_finish(dfmi_context* ctx, dfmi_agg_state* st, dfmi_agg_value* out,
+                                         dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st || !out) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return st->failure.code;
+        }
+        const std::vector<Partial> parts = merge_copies(st, read_acc(ctx, st));
+        for (size_t j = 0; j < st->aggs.size(); ++j) out[j] = finish_one(*st->aggs[j], parts[j]);
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int64_t dfmi_agg_partial_bytes(const dfmi_agg_state* st) {
+    return st ? (int64_t)(st->aggs.size() * sizeof(Partial)) : 0;
+}
+
+extern "C" int32_t dfmi_agg_state_partial(dfmi_context* ctx, dfmi_agg_state* st, void* host_out, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st || !host_out) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return st->failure.code;
+        }
+        const std::vector<Partial> parts = merge_copies(st, read_acc(ctx, st));
+        memcpy(host_out, parts.data(), parts.size() * sizeof(Partial));
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, int32_t n, const void* const* partials,
+                                           int32_t nparts, dfmi_agg_value* out, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!aggs || n <= 0 || !partials || nparts <= 0 || !out) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        for (int j = 0; j < n; ++j) {
+            Partial m;
+            const bool is_min = aggs[j]->fn == DFMI_AGG_MIN;
+            for (int r = 0; r < nparts; ++r) {
+                Partial p;
+                memcpy(&p, (const uint8_t*)partials[r] + (size_t)j * sizeof(Partial), sizeof p);
+                uint64_t w[kAggWords];
+                w[0] = p.count;
+                w[1] = p.flags;
+                w[2] = p.key;
+                w[3] = p.isum;
+                for (int i = 0; i < kAggLimbs; ++i) w[4 + i] = (uint64_t)p.limbs[i];
+                merge_into(m, w, is_min);
+            }
+            out[j] = finish_one(*aggs[j], m);
+        }
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+// Internal test hook (not part of the C ABI, not declared in include/): the
+// aggregate kernel a dfmi_aggregate_batch call would launch, generated and
+// (compile != 0) compiled with hipRTC -- no device needed (tests/test_aggregate_cpu.py).
+extern "C" int64_t dfmi_internal_agg_jit_check(const dfmi_program* pred, const dfmi_aggregate* const* aggs, int32_t n,
+                                               const dfmi_batch* in, uint32_t flags, int32_t compile, char* buf,
+                                               int64_t cap, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!in || !aggs || n <= 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        dfmi_agg_state st;
+        for (int j = 0; j < n; ++j) st.aggs.push_back(aggs[j]);
+        AggBuilt B;
+        build_agg_plan(&st, pred, in, flags, B);
+        const std::string src = jit::generate(B.plan, B.X);
+        if (compile) (void)jit::compile_code(src, nullptr);
+        if (buf && cap > 0) snprintf(buf, (size_t)cap, "%s", src.c_str());
+        return (int64_t)src.size();
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return -(int64_t)f.code;
+    }
+}

@@ -29,81 +29,11 @@ hipError_t launch_pack_bools(const uint8_t* bytes, uint8_t* bits, const unsigned
 
 using namespace dfmi;
 
-// Workspace header layout (device, zero when a launch starts).
-static constexpr size_t kHdrTicket = 0;
-static constexpr size_t kHdrErr = 8;
-static constexpr size_t kHdrTotals = 16;
-static constexpr size_t kHdrStats = 256;  // look-back statistics (DFMI_DEBUG_MODE bit 4)
-static constexpr size_t kHdrAlloc = 512;
+#include "exec_internal.h"
 
-struct dfmi_context {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    // Look-back workspace, double-buffered: [hdr 0 | hdr 1 | status 0 | status 1].
-    // Launch i uses pair (i & 1), which is zero on entry, and its blocks zero
-    // pair (i+1) & 1 -- what launch i-1 dirtied -- for launch i+1 (stream
-    // order makes launch i-1 complete first). No memset on the steady path.
-    uint8_t* ws = nullptr;
-    size_t ws_bytes = 0;
-    size_t status_cap = 0;       // bytes per status buffer
-    int parity = 0;              // pair the next launch uses
-    size_t dirty[2] = {0, 0};    // status bytes [0, dirty[b]) of buffer b may be non-zero
-    bool ws_valid = false;       // the invariant above holds (else re-zero everything)
-    uint8_t* scratch = nullptr;  // Boolean output bytes (filtered)
-    size_t scratch_bytes = 0;
-    uint8_t* host_hdr = nullptr; // pinned copy of the header
-    void* host_arena = nullptr;  // host_batch.cpp's staging arena (per context: no shared state)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-    double last_total_ms = 0, last_main_ms = 0, last_compile_ms = 0;
-    bool timed = false;
-};
+using namespace dfmi::xi;
 
 namespace {
-
-void set_err(dfmi_error* err, int32_t code, const std::string& m) {
-    if (!err) return;
-    err->code = code;
-    snprintf(err->message, sizeof err->message, "%s", m.c_str());
-}
-
-#define HIP_TRY(x)                                                                         \
-    do {                                                                                   \
-        hipError_t e_ = (x);                                                               \
-        if (e_ != hipSuccess) throw Fail{DFMI_ERR_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)}; \
-    } while (0)
-
-bool gatherable(int t, uint32_t flags) {
-    if (t == DFMI_TYPE_FLOAT64 || t == DFMI_TYPE_UTF8) return true;  // filter.rs:84,94
-    // extension: every fixed-width type and Boolean
-    if (flags & DFMI_FLAG_EXT_GATHER_ALL) return is_numeric_type(t) || t == DFMI_TYPE_BOOLEAN;
-    return false;
-}
-
-// A candidate error: the reference raises the one with the smallest ordinal.
-struct Err {
-    bool set = false;
-    uint64_t key = ~0ull;  // ordinal << 44 | row << 4
-    int32_t code = 0;
-    std::string msg;
-    void offer(uint64_t k, int32_t c, const std::string& m) {
-        if (!set || k < key) {
-            set = true;
-            key = k;
-            code = c;
-            msg = m;
-        }
-    }
-};
-
-void ensure(dfmi_context* ctx, uint8_t** buf, size_t* have, size_t need) {
-    if (*have >= need) return;
-    if (*buf) HIP_TRY(hipFree(*buf));
-    *buf = nullptr;
-    *have = 0;
-    size_t cap = std::max(need, (size_t)1 << 20);
-    HIP_TRY(hipMalloc(buf, cap));
-    *have = cap;
-}
 
 // Everything about one call that does not need the device: static errors,
 // output metadata, the jit plan and the column slot tables.
@@ -413,17 +343,6 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 if (plan.outs[o].nullable) valid_out.push_back(o);
             }
             const size_t row_bytes = (size_t)((n + 63) & ~63ll);
-            if (!ctx->ws || status_bytes > ctx->status_cap) {
-                const size_t cap = (std::max(status_bytes, (size_t)1 << 20) + 255) & ~(size_t)255;
-                ensure(ctx, &ctx->ws, &ctx->ws_bytes, 2 * kHdrAlloc + 2 * cap);
-                ctx->status_cap = cap;
-                ctx->ws_valid = false;
-            }
-            if (!ctx->ws_valid) {  // first use, growth, or an interrupted call
-                HIP_TRY(hipMemsetAsync(ctx->ws, 0, 2 * kHdrAlloc + 2 * ctx->status_cap, st));
-                ctx->dirty[0] = ctx->dirty[1] = 0;
-                ctx->ws_valid = true;
-            }
             if (!bool_out.empty() || !valid_out.empty())
                 ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, (bool_out.size() + valid_out.size()) * row_bytes);
             A.n_rows = n;
@@ -462,30 +381,24 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             memcpy(A.str_off, X.str_off, sizeof A.str_off);
             memcpy(A.str_len, X.str_len, sizeof A.str_len);
             memcpy(A.str, X.str, sizeof A.str);
-            const int par = ctx->parity;
-            uint8_t* hdr = ctx->ws + par * kHdrAlloc;
-            uint8_t* status = ctx->ws + 2 * kHdrAlloc + par * ctx->status_cap;
-            uint8_t* other_status = ctx->ws + 2 * kHdrAlloc + (1 - par) * ctx->status_cap;
+            const WsLease ws = ws_acquire(ctx, status_bytes, st);
+            uint8_t* hdr = ws.hdr;
             A.ticket = (unsigned*)(hdr + kHdrTicket);
             A.err = (unsigned long long*)(hdr + kHdrErr);
             A.totals = (unsigned long long*)(hdr + kHdrTotals);
-            A.status = (unsigned long long*)status;
+            A.status = (unsigned long long*)ws.status;
             A.stats = (unsigned long long*)(hdr + kHdrStats);
-            A.clear_status = (unsigned long long*)other_status;
-            A.clear_words = (long long)(ctx->dirty[1 - par] / 8);
-            A.clear_hdr = (unsigned long long*)(ctx->ws + (1 - par) * kHdrAlloc);
+            A.clear_status = (unsigned long long*)ws.clear_status;
+            A.clear_words = ws.clear_words;
+            A.clear_hdr = (unsigned long long*)ws.clear_hdr;
             A.mode = 0;
             if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
             const unsigned grid = (unsigned)n_tiles;  // one block per tile
             HIP_TRY(hipEventRecord(ctx->ev0, st));
             size_t asz = sizeof A;
             void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
-            ctx->ws_valid = false;  // until the launch is enqueued
             HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
-            ctx->dirty[par] = status_bytes;
-            ctx->dirty[1 - par] = 0;
-            ctx->parity = 1 - par;
-            ctx->ws_valid = true;
+            ws_commit(ctx, ws);
             HIP_TRY(hipEventRecord(ctx->ev1, st));
             for (int o = 0; o < nout; ++o)
                 if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));

@@ -410,6 +410,124 @@ static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Lau
     o << "  }\n";
 }
 
+// The predicate of a filtered tile: `unsigned selm` (bit k = row base + k*BLOCK
+// + tid selected, mask.value(i)); Utf8 columns' offsets (us<u> / ux<u>) are
+// loaded tile-wide in front of the predicate loop -- the predicate's `col =
+// literal` compares and the columns in `extra_offs` (Utf8 outputs: their byte
+// counts are needed before the look-back, so they share the first memory
+// round trip). Returns the Utf8 slots whose offsets are in registers.
+static std::vector<int> emit_predicate(Gen& g, std::ostringstream& o, const Plan& P, Launch& X, const std::string& cur,
+                                       const std::vector<int>& extra_offs) {
+    const std::string head = o.str();
+    g.tile_pre = true;
+    g.pre_eq.clear();
+    o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
+    o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
+    const Val r = g.emit(P.pred, P.pred->root, 0, "in");
+    if (P.pred->type == DFMI_TYPE_BOOLEAN && !r.v.empty())
+        o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
+    o << "  }\n";
+    g.tile_pre = false;
+    std::vector<int> offs_loaded;
+    auto offs_name = [&](int u) { return std::to_string(u) + cur; };
+    std::ostringstream pre;
+    auto load_offs = [&](int u) {
+        if (std::find(offs_loaded.begin(), offs_loaded.end(), u) != offs_loaded.end()) return;
+        offs_loaded.push_back(u);
+        pre << "  int us" << offs_name(u) << "[K], ux" << offs_name(u)
+            << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u << ", base, lane, wave, ~0u, us" << offs_name(u)
+            << ", ux" << offs_name(u) << ");\n";
+    };
+    for (const auto& pe : g.pre_eq) load_offs(std::get<1>(pe));
+    for (int u : extra_offs) load_offs(u);
+    for (const auto& [arr, u, sl] : g.pre_eq)
+        pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u << ", " << sl << ", us"
+            << offs_name(u) << ", ux" << offs_name(u) << ", lane, " << arr << ");\n";
+    if (!pre.str().empty()) {  // splice in front of the predicate loop
+        const std::string loop = o.str().substr(head.size());
+        o.str(head + pre.str() + loop);
+        o.seekp(0, std::ios_base::end);
+    }
+    return offs_loaded;
+}
+
+// Fused Selection + Aggregate kernel (DFMI_FLAG_EXT_AGGREGATE): one block per
+// tile, no compaction and no look-back -- the selected rows' argument values
+// are reduced in registers, the block's partial goes to a global accumulator
+// copy (jit_skeleton.hip "aggregate extension").
+static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X) {
+    const int NA = (int)P.aggs.size();
+    int NF = 0;
+    for (const AggSpec& a : P.aggs) NF += a.fslot >= 0;
+    o << "  constexpr int NA = " << NA << ", NF = " << NF << ";\n";
+    o << "  __shared__ dfmi::AggLds<NA, NF> S;\n  const unsigned char is_min[NA] = {";
+    for (int j = 0; j < NA; ++j) o << (j ? ", " : "") << (P.aggs[j].fn == DFMI_AGG_MIN ? 1 : 0);
+    o << "};\n  const int fslot[NF > 0 ? NF : 1] = {";
+    {
+        bool any = false;
+        for (int j = 0; j < NA; ++j)
+            if (P.aggs[j].fslot >= 0) {
+                o << (any ? ", " : "") << j;
+                any = true;
+            }
+        if (!any) o << "0";
+    }
+    o << "};\n";
+    o << "  if (wave == 0) dfmi::agg_lds_init<NA, NF>(S, is_min, lane);\n";
+    o << "  const unsigned t = blockIdx.x;\n";
+    emit_decls(o, X.pred_slots, X, "", true);
+    emit_decls(o, X.proj_slots, X, "", !P.pred);
+    emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
+    o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
+    if (P.pred) {
+        g.filtered_cols = false;
+        emit_predicate(g, o, P, X, "", {});
+        // argument-only columns, loaded only where selected
+        emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+    } else {
+        o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) selm |= (unsigned)(base + k * BLOCK "
+             "+ tid < A.n_rows) << k;\n";
+        emit_loads(o, X.proj_slots, X, "", "base", nullptr, true);
+    }
+    // arguments over the filtered batch (no validity) or the batch itself
+    g.filtered_cols = P.pred != nullptr;
+    for (int j = 0; j < NA; ++j)
+        o << "  unsigned acnt" << j << " = 0, afl" << j << " = 0;\n  u64 asum" << j << " = 0, akey" << j << " = "
+          << (P.aggs[j].fn == DFMI_AGG_MIN ? "~0ull" : "0ull") << ";\n";
+    o << "  dfmi::lds_sync();\n";
+    o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+      << "    const i64 row = base + k * BLOCK + tid;\n    const bool sel = (selm >> k) & 1;\n";
+    for (int j = 0; j < NA; ++j) {
+        const AggSpec& a = P.aggs[j];
+        const Val v = g.emit(a.prog, a.prog->root, a.ord_base, "sel");
+        const std::string ok = "ok" + std::to_string(j) + "_";
+        o << "    { const bool " << ok << " = sel && (" << v.n << ");\n";
+        o << "      acnt" << j << " += " << ok << " ? 1u : 0u;\n";
+        if (a.fn == DFMI_AGG_SUM && a.fslot < 0) {
+            o << "      asum" << j << " += " << ok << " ? (u64)(" << (is_signed_int(a.arg_type) ? "i64" : "u64") << ")("
+              << v.v << ") : 0ull;\n";
+        } else if (a.fn == DFMI_AGG_SUM) {
+            o << "      afl" << j << " |= " << ok << " ? dfmi::agg_sum_flags(" << v.v << ") : 0u;\n"
+              << "      const bool fin_ = " << ok << " && (dfmi::agg_sum_flags(" << v.v << ") == dfmi::AGGF_NONNEGZERO) && ("
+              << v.v << ") != 0;\n"
+              << "      dfmi::fsum_add(S.limbs[" << a.fslot << "], &S.dlo[" << a.fslot << "], &S.dhi[" << a.fslot
+              << "], (double)(" << v.v << "), fin_, lane);\n";
+        } else if (a.fn == DFMI_AGG_MIN || a.fn == DFMI_AGG_MAX) {
+            const char* cmp = a.fn == DFMI_AGG_MIN ? "<" : ">";
+            o << "      const bool nan_ = dfmi::agg_isnan(" << v.v << ");\n"
+              << "      afl" << j << " |= " << ok << " ? (nan_ ? (unsigned)dfmi::AGGF_NAN : (unsigned)dfmi::AGGF_VALUE) : 0u;\n"
+              << "      if (" << ok << " && !nan_) { const u64 k_ = dfmi::agg_key(" << v.v << "); if (k_ " << cmp << " akey" << j
+              << ") akey" << j << " = k_; }\n";
+        }
+        o << "    }\n";
+    }
+    o << "  }\n";
+    for (int j = 0; j < NA; ++j)
+        o << "  dfmi::agg_wave_flush<NA, NF>(S, " << j << ", acnt" << j << ", asum" << j << ", akey" << j << ", "
+          << (P.aggs[j].fn == DFMI_AGG_MIN ? "true" : "false") << ", afl" << j << ", lane);\n";
+    o << "  dfmi::lds_sync();\n  dfmi::agg_block_flush<NA, NF>(A, S, fslot, is_min, tid);\n  }\n";
+}
+
 std::string generate(const Plan& P, Launch& X) {
     Gen g(P, X);
     std::ostringstream& o = g.o;
@@ -421,7 +539,9 @@ std::string generate(const Plan& P, Launch& X) {
     o << "  constexpr int BLOCK = " << BLOCK << ", K = " << K << ", WAVES = BLOCK / 64;\n";
     o << "  const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);\n";
     o << "  dfmi::clear_previous<BLOCK>(A, blockIdx.x, tid);\n";
-    if (P.pred) {
+    if (!P.aggs.empty()) {
+        generate_agg(g, o, P, X);
+    } else if (P.pred) {
         const int nch = 1 + (int)X.utf8_outs.size();
         o << "  constexpr int NCH = " << nch << ";\n";
         const std::string tparams = std::to_string(X.R) + ", " + std::to_string(X.sleep) + ", " +
@@ -432,44 +552,10 @@ std::string generate(const Plan& P, Launch& X) {
             o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
             g.sfx = cur;
             g.filtered_cols = false;
-            const std::string head = o.str();
-            g.tile_pre = true;
-            g.pre_eq.clear();
-            o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n";
-            o << "    const i64 row = base + k * BLOCK + tid;\n    const bool in = row < A.n_rows;\n";
-            const Val r = g.emit(P.pred, P.pred->root, 0, "in");
-            if (P.pred->type == DFMI_TYPE_BOOLEAN && !r.v.empty())
-                o << "    selm |= (unsigned)(in && (" << r.v << ")) << k;\n";  // mask.value(i)
-            o << "  }\n";
-            g.tile_pre = false;
-            // Utf8 columns whose offsets are in registers (us<u> start, ux<u>
-            // next slice's first offset): the predicate's tile-wide compares and
-            // every Utf8 output (its byte count is needed before the look-back,
-            // so its offsets are loaded with the predicate columns -- one memory
-            // round trip before the tile publishes, not two). Spliced in front
-            // of the predicate loop.
-            std::vector<int> offs_loaded;
+            std::vector<int> utf8_out_cols;
+            for (const auto& uo : X.utf8_outs) utf8_out_cols.push_back(uo.second);
+            const std::vector<int> offs_loaded = emit_predicate(g, o, P, X, cur, utf8_out_cols);
             auto offs_name = [&](int u) { return std::to_string(u) + cur; };
-            {
-                std::ostringstream pre;
-                auto load_offs = [&](int u) {
-                    if (std::find(offs_loaded.begin(), offs_loaded.end(), u) != offs_loaded.end()) return;
-                    offs_loaded.push_back(u);
-                    pre << "  int us" << offs_name(u) << "[K], ux" << offs_name(u)
-                        << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u << ", base, lane, wave, ~0u, us"
-                        << offs_name(u) << ", ux" << offs_name(u) << ");\n";
-                };
-                for (const auto& pe : g.pre_eq) load_offs(std::get<1>(pe));
-                for (const auto& uo : X.utf8_outs) load_offs(uo.second);
-                for (const auto& [arr, u, sl] : g.pre_eq)
-                    pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u << ", " << sl
-                        << ", us" << offs_name(u) << ", ux" << offs_name(u) << ", lane, " << arr << ");\n";
-                if (!pre.str().empty()) {
-                    const std::string loop = o.str().substr(head.size());
-                    o.str(head + pre.str() + loop);
-                    o.seekp(0, std::ios_base::end);
-                }
-            }
             // projection-only columns, loaded only where selected
             if (!X.late_proj) emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
             // compaction offsets (rows + Utf8 bytes)
@@ -625,6 +711,12 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
     k.reserve(256);
     put(k, device);
     put(k, P.pred ? P.pred->uid : 0ull);
+    for (const AggSpec& a : P.aggs) {
+        put(k, a.fn);
+        put(k, a.prog ? a.prog->uid : 0ull);
+        put(k, a.ord_base);
+        put(k, a.fslot);
+    }
     for (const OutSpec& os : P.outs) {
         put(k, (int)os.kind);
         put(k, os.col);

@@ -30,9 +30,19 @@ struct OutSpec {
     bool nullable = false;
 };
 
+// One aggregate of the aggregate kernel (DFMI_FLAG_EXT_AGGREGATE).
+struct AggSpec {
+    int fn = 0;                          // dfmi_agg_fn
+    const dfmi_program* prog = nullptr;  // argument
+    int ord_base = 0;                    // evaluation-order base of prog's nodes
+    int arg_type = 0;
+    int fslot = -1;                      // >= 0: exact float sum, its LDS digit block
+};
+
 struct Plan {
     const dfmi_program* pred = nullptr;  // nullptr: projection only (dense kernel)
     std::vector<OutSpec> outs;
+    std::vector<AggSpec> aggs;           // non-empty: the aggregate kernel (outs unused)
 };
 
 // Slot tables + literal pools of one launch.

@@ -59,6 +59,7 @@ struct Args {
     u64* clear_status;                 // previous launch's status words ...
     i64 clear_words;                   // ... [0, clear_words) to zero
     u64* clear_hdr;                    // previous launch's 512-byte header
+    u64* agg;                          // aggregate extension: [copies][aggs][kAggWords] accumulators
 };
 
 // This block's share of zeroing the previous launch's workspace.
@@ -746,6 +747,197 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
             }
         }
         wave_lds_fence();
+    }
+}
+
+// ------------------------------------------------ aggregate extension
+// Fused Selection + Aggregate (no GROUP BY): every block reduces its tile's
+// selected rows in registers / LDS and adds the block's partial into one of
+// kAggCopies global accumulator copies (blockIdx % copies: atomics spread
+// over many addresses); the host merges the copies exactly (aggregate.cpp).
+// Accumulator words per aggregate: [0] non-null count, [1] flags, [2] MIN/MAX
+// key, [3] wrapping integer sum, [4..] exact float sum digits.
+constexpr int kAggCopies = 64;
+constexpr int kAggLimbs = 68;                // 32-bit digits of the exact sum in units of 2^-1074, + carries
+constexpr int kAggWords = 4 + kAggLimbs;
+enum AggFlag : unsigned { AGGF_NAN = 1, AGGF_PINF = 2, AGGF_NINF = 4, AGGF_NONNEGZERO = 8, AGGF_VALUE = 16 };
+
+// Order-preserving key of a MIN/MAX value (-0.0 below +0.0; NaN never keyed).
+template <typename T>
+__device__ __forceinline__ u64 agg_key(T v) {
+    if constexpr (__is_same(T, float)) {
+        const unsigned b = __builtin_bit_cast(unsigned, v);
+        return (b >> 31) ? (u64)(~b) : (u64)(b | 0x80000000u);
+    } else if constexpr (__is_same(T, double)) {
+        const u64 b = __builtin_bit_cast(u64, v);
+        return (b >> 63) ? ~b : (b | (1ull << 63));
+    } else if constexpr ((T)-1 < (T)0) {
+        return (u64)(i64)v ^ (1ull << 63);
+    } else {
+        return (u64)v;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ bool agg_isnan(T v) {
+    if constexpr ((T)0.5 != (T)0) return v != v;
+    else return false;
+}
+
+// Flag bits of one SUM input value (floats): NaN, +inf, -inf, "not -0.0".
+template <typename T>
+__device__ __forceinline__ unsigned agg_sum_flags(T v) {
+    if constexpr ((T)0.5 != (T)0) {
+        if (v != v) return AGGF_NAN;
+        if (__builtin_isinf(v)) return v > 0 ? AGGF_PINF : AGGF_NINF;
+        return (v == 0 && __builtin_signbit(v)) ? 0u : AGGF_NONNEGZERO;
+    } else {
+        return 0u;
+    }
+}
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp32_id(unsigned v, unsigned id) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, ROWS, 0xf, false);
+}
+
+// Wave-wide min / max of u64 (uniform result; all lanes active).
+template <bool MIN>
+__device__ __forceinline__ u64 wave_minmax(u64 v) {
+    const unsigned id = MIN ? ~0u : 0u;
+#define DFMI_MM_STEP(C, R)                                                                  \
+    {                                                                                       \
+        const u64 o = ((u64)dpp32_id<C, R>((unsigned)(v >> 32), id) << 32) |                \
+                      dpp32_id<C, R>((unsigned)v, id);                                      \
+        v = MIN ? (o < v ? o : v) : (o > v ? o : v);                                        \
+    }
+    DFMI_MM_STEP(0x111, 0xf) DFMI_MM_STEP(0x112, 0xf) DFMI_MM_STEP(0x114, 0xf)
+    DFMI_MM_STEP(0x118, 0xf) DFMI_MM_STEP(0x142, 0xa) DFMI_MM_STEP(0x143, 0xc)
+#undef DFMI_MM_STEP
+    return ((u64)__builtin_amdgcn_readlane((unsigned)(v >> 32), 63) << 32) | __builtin_amdgcn_readlane((unsigned)v, 63);
+}
+
+// Block-level (LDS) state of NA aggregates, NF of them exact float sums.
+template <int NA, int NF>
+struct AggLds {
+    u64 count[NA];
+    u64 isum[NA];
+    u64 key[NA];
+    unsigned flags[NA];
+    long long limbs[NF > 0 ? NF : 1][kAggLimbs];
+    int dlo[NF > 0 ? NF : 1], dhi[NF > 0 ? NF : 1];
+};
+
+template <int NA, int NF>
+__device__ __forceinline__ void agg_lds_init(AggLds<NA, NF>& S, const unsigned char (&is_min)[NA > 0 ? NA : 1], int tid) {
+    for (int i = tid; i < NA; i += 64) {
+        S.count[i] = 0;
+        S.isum[i] = 0;
+        S.key[i] = is_min[i] ? ~0ull : 0ull;
+        S.flags[i] = 0;
+    }
+    for (int i = tid; i < NF * kAggLimbs; i += 64) (&S.limbs[0][0])[i] = 0;
+    for (int i = tid; i < NF; i += 64) {
+        S.dlo[i] = 0x7fffffff;
+        S.dhi[i] = -1;
+    }
+}
+
+// Exact float sum: this wave's `ok` values (finite, non-zero) added into the
+// block's 32-bit-digit accumulator. A double is m * 2^(b-1074) (m < 2^53,
+// b = biased exponent - 1, subnormals b = 0): digits d = b/32 .. d+2 receive
+// the three 32-bit pieces of m << (b % 32), signed. When every value of the
+// wave falls on the same digit (the common case) the wave sums the pieces
+// first and one lane adds three words; otherwise each lane adds its own.
+__device__ __forceinline__ void fsum_add(long long* limbs, int* dlo, int* dhi, double v, bool ok, int lane) {
+    const u64 vm = __ballot(ok);
+    if (!vm) return;
+    const u64 b = __builtin_bit_cast(u64, v);
+    const int e = (int)((b >> 52) & 0x7ff);
+    const u64 m = (b & ((1ull << 52) - 1)) | (e ? (1ull << 52) : 0ull);
+    const int pos = (e ? e : 1) - 1;
+    const int d = pos >> 5, sh = pos & 31;
+    const u64 x0 = (m & 0xffffffffull) << sh, x1 = (m >> 32) << sh;
+    long long c0 = (long long)(x0 & 0xffffffffull);
+    long long c1 = (long long)((x0 >> 32) + (x1 & 0xffffffffull));
+    long long c2 = (long long)(x1 >> 32);
+    if (b >> 63) {
+        c0 = -c0;
+        c1 = -c1;
+        c2 = -c2;
+    }
+    if (!ok) c0 = c1 = c2 = 0;
+    const int d0 = __builtin_amdgcn_readlane(d, __builtin_ctzll(vm));
+    if (!__ballot(ok && d != d0)) {
+        const u64 s0 = wave_sum((u64)c0), s1 = wave_sum((u64)c1), s2 = wave_sum((u64)c2);
+        if (lane == 0) {
+            atomicAdd((unsigned long long*)&limbs[d0], (unsigned long long)s0);
+            atomicAdd((unsigned long long*)&limbs[d0 + 1], (unsigned long long)s1);
+            atomicAdd((unsigned long long*)&limbs[d0 + 2], (unsigned long long)s2);
+            atomicMin(dlo, d0);
+            atomicMax(dhi, d0 + 2);
+        }
+    } else if (ok) {
+        atomicAdd((unsigned long long*)&limbs[d], (unsigned long long)c0);
+        atomicAdd((unsigned long long*)&limbs[d + 1], (unsigned long long)c1);
+        atomicAdd((unsigned long long*)&limbs[d + 2], (unsigned long long)c2);
+        atomicMin(dlo, d);
+        atomicMax(dhi, d + 2);
+    }
+}
+
+// One wave's per-lane partials of aggregate j into the block state.
+template <int NA, int NF>
+__device__ __forceinline__ void agg_wave_flush(AggLds<NA, NF>& S, int j, unsigned cnt, u64 isum, u64 key, bool is_min,
+                                               unsigned flags, int lane) {
+    const u64 c = wave_sum((u64)cnt), s = wave_sum(isum);
+    const u64 k = is_min ? wave_minmax<true>(key) : wave_minmax<false>(key);
+    unsigned f = 0;
+#pragma unroll
+    for (int bit = 0; bit < 5; ++bit) f |= __ballot((flags >> bit) & 1) ? (1u << bit) : 0u;
+    if (lane == 0) {
+        if (c) atomicAdd((unsigned long long*)&S.count[j], (unsigned long long)c);
+        if (s) atomicAdd((unsigned long long*)&S.isum[j], (unsigned long long)s);
+        if (is_min) atomicMin((unsigned long long*)&S.key[j], (unsigned long long)k);
+        else atomicMax((unsigned long long*)&S.key[j], (unsigned long long)k);
+        if (f) atomicOr(&S.flags[j], f);
+    }
+}
+
+// The block's state into global copy blockIdx % kAggCopies (after a block
+// barrier). The float digits are carry-normalised first (every digit but the
+// top one in [0, 2^32)), so a global digit absorbs 2^31 block partials.
+template <int NA, int NF>
+__device__ __forceinline__ void agg_block_flush(const Args& A, AggLds<NA, NF>& S, const int (&fslot)[NF > 0 ? NF : 1],
+                                                const unsigned char (&is_min)[NA > 0 ? NA : 1], int tid) {
+    u64* base = A.agg + (u64)(blockIdx.x % kAggCopies) * NA * kAggWords;
+    if (tid < NA) {
+        u64* w = base + tid * kAggWords;
+        if (S.count[tid]) atomicAdd((unsigned long long*)&w[0], (unsigned long long)S.count[tid]);
+        if (S.flags[tid]) atomicOr((unsigned long long*)&w[1], (unsigned long long)S.flags[tid]);
+        if (S.flags[tid] & AGGF_VALUE) {
+            if (is_min[tid]) atomicMin((unsigned long long*)&w[2], (unsigned long long)S.key[tid]);
+            else atomicMax((unsigned long long*)&w[2], (unsigned long long)S.key[tid]);
+        }
+        if (S.isum[tid]) atomicAdd((unsigned long long*)&w[3], (unsigned long long)S.isum[tid]);
+    }
+    if constexpr (NF > 0) {
+        if (tid >= 64 && tid < 64 + NF) {  // one lane per float sum, in another wave
+            const int f = tid - 64;
+            const int lo = S.dlo[f], hi = S.dhi[f];
+            if (hi >= 0) {
+                long long* L = S.limbs[f];
+                const int top = hi + 2 < kAggLimbs - 1 ? hi + 2 : kAggLimbs - 1;
+                for (int i = lo; i < top; ++i) {
+                    const long long c = L[i] >> 32;  // arithmetic: floor division by 2^32
+                    L[i] -= c * 4294967296ll;
+                    L[i + 1] += c;
+                }
+                u64* w = base + fslot[f] * kAggWords + 4;
+                for (int i = lo; i <= top; ++i)
+                    if (L[i]) atomicAdd((unsigned long long*)&w[i], (unsigned long long)L[i]);
+            }
+        }
     }
 }
 

@@ -8,7 +8,8 @@ from typing import Dict
 from ..arrow import Field, Schema
 from ..logicalplan import Column, Expr, PlanError, expr_to_field_name_type
 from .error import ExecutionError
-from .expression import compile_scalar_expr
+from .aggregate import AggregateRelation
+from .expression import compile_expr, compile_scalar_expr
 from .filter import FilterRelation
 from .projection import ProjectRelation
 from .relation import DataSourceRelation, Relation
@@ -30,6 +31,16 @@ class Projection:
     def __init__(self, expr, input, schema: Schema = None):
         self.expr = list(expr)
         self.input = input
+        self.schema = schema
+
+
+class Aggregate:
+    """LogicalPlan::Aggregate { input, group_expr, aggr_expr, schema } (logicalplan.rs:324-329)."""
+
+    def __init__(self, input, group_expr, aggr_expr, schema: Schema = None):
+        self.input = input
+        self.group_expr = list(group_expr)
+        self.aggr_expr = list(aggr_expr)
         self.schema = schema
 
 
@@ -79,4 +90,25 @@ class ExecutionContext:
             project_schema = Schema(fields)
             compiled = [compile_scalar_expr(self, e, input_schema, self.flags) for e in plan.expr]
             return ProjectRelation(input_rel, compiled, project_schema, self.device, self.flags)
+        if isinstance(plan, Aggregate):
+            return self._execute_aggregate(plan)
         raise ExecutionError("NotImplemented", "unimplemented!() plan %r" % type(plan).__name__)
+
+    def _execute_aggregate(self, plan: "Aggregate") -> Relation:
+        """The Aggregate arm the reference lacks (context.rs:161 unimplemented!()),
+        under DFMI_FLAG_EXT_AGGREGATE: the input's Selection fuses into the pass."""
+        from .. import _abi
+        if not (self.flags & _abi.DFMI_FLAG_EXT_AGGREGATE):
+            raise ExecutionError("panic", "not yet implemented")
+        if plan.group_expr:
+            raise ExecutionError("NotImplemented", "GROUP BY on the device path")
+        inp, pred = plan.input, None
+        if isinstance(inp, Selection):
+            source = self.execute(inp.input)
+            pred = compile_scalar_expr(self, inp.expr, source.schema(), self.flags)
+        else:
+            source = self.execute(inp)
+        input_schema = source.schema()
+        aggs = [compile_expr(self, e, input_schema, self.flags) for e in plan.aggr_expr]
+        schema = Schema([Field(e.name, e.return_type, True) for e in plan.aggr_expr])  # sqlplanner.rs:385-389
+        return AggregateRelation(source, pred, aggs, schema, self.device, self.flags)

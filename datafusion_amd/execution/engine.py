@@ -203,3 +203,89 @@ class DeviceEngine:
         finally:
             L.dfmi_host_result_free(res)
         return out
+
+    # ---- aggregate extension (DFMI_FLAG_EXT_AGGREGATE)
+    def _batch_struct(self, batch: RecordBatch):
+        cols = batch.columns
+        carr = (_abi.dfmi_column * max(1, len(cols)))()
+        for i, a in enumerate(cols):
+            carr[i] = column_struct(a)
+        cb = _abi.dfmi_batch()
+        cb.num_columns = len(cols)
+        cb.num_rows = batch.num_rows()
+        cb.columns = carr
+        return cb, carr
+
+    def agg_state(self, aggs: Sequence) -> "AggState":
+        """Device accumulators for one Aggregate plan (dfmi_agg_state_create)."""
+        return AggState(self, aggs)
+
+
+class AggState:
+    """dfmi_agg_state: accumulates batches of one Aggregate plan on one GPU."""
+
+    def __init__(self, eng: DeviceEngine, aggs: Sequence):
+        self.eng = eng
+        self.aggs = list(aggs)
+        L = _abi.lib()
+        arr = (C.c_void_p * len(self.aggs))(*[a.handle.value for a in self.aggs])
+        out = C.c_void_p()
+        err = _abi.dfmi_error()
+        rc = L.dfmi_agg_state_create(eng.ctx, arr, len(self.aggs), C.byref(out), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        self.handle = out
+
+    def add(self, predicate, batch: RecordBatch, flags: int = 0) -> None:
+        """One batch of the aggregate's input (fused Selection when predicate is given)."""
+        eng = self.eng
+        batch = eng.to_device(batch)
+        cb, keep = eng._batch_struct(batch)
+        err = _abi.dfmi_error()
+        L = _abi.lib()
+        L.dfmi_context_set_stream(eng.ctx, C.c_void_p(torch.cuda.current_stream(eng.device).cuda_stream))
+        rc = L.dfmi_aggregate_batch(eng.ctx, self.handle, predicate.handle if predicate is not None else None,
+                                    C.byref(cb), flags, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+
+    def finish(self) -> List[_abi.dfmi_agg_value]:
+        out = (_abi.dfmi_agg_value * len(self.aggs))()
+        err = _abi.dfmi_error()
+        rc = _abi.lib().dfmi_agg_state_finish(self.eng.ctx, self.handle, out, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        return list(out)
+
+    def partial(self) -> bytes:
+        """The exact partial state (for merging shards: dfmi_agg_merge_partials)."""
+        L = _abi.lib()
+        nb = L.dfmi_agg_partial_bytes(self.handle)
+        buf = C.create_string_buffer(nb)
+        err = _abi.dfmi_error()
+        rc = L.dfmi_agg_state_partial(self.eng.ctx, self.handle, buf, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        return buf.raw
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _abi.lib().dfmi_agg_state_free(h)
+            except Exception:
+                pass
+            self.handle = C.c_void_p(0)
+
+
+def merge_agg_partials(aggs: Sequence, partials: Sequence[bytes]) -> List[_abi.dfmi_agg_value]:
+    """Final values from every shard's exact partial state (host merge)."""
+    arr = (C.c_void_p * len(aggs))(*[a.handle.value for a in aggs])
+    bufs = [C.create_string_buffer(p, len(p)) for p in partials]
+    parr = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+    out = (_abi.dfmi_agg_value * len(aggs))()
+    err = _abi.dfmi_error()
+    rc = _abi.lib().dfmi_agg_merge_partials(arr, len(aggs), parr, len(bufs), out, C.byref(err))
+    if rc != _abi.DFMI_OK:
+        raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+    return list(out)

@@ -66,8 +66,55 @@ def compile_scalar_expr(ctx, expr: Expr, input_schema: Schema, flags: int = None
     return RuntimeExpr(expr, out.value, input_schema, flags)
 
 
-def compile_expr(ctx, expr: Expr, input_schema: Schema) -> RuntimeExpr:
-    """expression.rs:81-119. Aggregates are outside this path."""
-    if isinstance(expr, AggregateFunction):
-        raise ExecutionError("NotImplemented", "aggregate expressions are not on the device path")
-    return compile_scalar_expr(ctx, expr, input_schema)
+class AggregateExpr:
+    """RuntimeExpr::AggregateFunction { name, f, args, t } (expression.rs:51-56):
+    a dfmi_aggregate handle over the compiled argument (DFMI_FLAG_EXT_AGGREGATE)."""
+
+    def __init__(self, expr: AggregateFunction, handle: int, arg: RuntimeExpr):
+        self.expr = expr
+        self.arg = arg
+        self._handle = C.c_void_p(handle)
+        L = _abi.lib()
+        self.name = L.dfmi_aggregate_name(self._handle).decode("utf-8", errors="surrogateescape")
+        self.t = DataType(L.dfmi_aggregate_type(self._handle))
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._handle
+
+    def get_name(self) -> str:
+        return self.name
+
+    def get_type(self) -> DataType:
+        return self.t
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            try:
+                _abi.lib().dfmi_aggregate_free(h)
+            except Exception:
+                pass
+            self._handle = C.c_void_p(0)
+
+
+def compile_expr(ctx, expr: Expr, input_schema: Schema, flags: int = None):
+    """expression.rs:81-116: an AggregateFunction compiles its single argument
+    with compile_scalar_expr and maps the name to an AggregateType (anything
+    but min/max/count/sum panics); every other expression is
+    compile_scalar_expr."""
+    if flags is None:
+        flags = getattr(ctx, "flags", 0) if ctx is not None else 0
+    if not isinstance(expr, AggregateFunction):
+        return compile_scalar_expr(ctx, expr, input_schema, flags)
+    if len(expr.args) != 1:  # assert_eq!(1, args.len())
+        raise ExecutionError("panic", "assertion failed: `(left == right)`\n  left: `1`,\n right: `%d`"
+                             % len(expr.args))
+    arg = compile_scalar_expr(ctx, expr.args[0], input_schema, flags)
+    out = C.c_void_p()
+    err = _abi.dfmi_error()
+    rc = _abi.lib().dfmi_compile_aggregate(expr.name.encode("utf-8"), arg.handle, int(expr.return_type), flags,
+                                          C.byref(out), C.byref(err))
+    if rc != _abi.DFMI_OK:
+        raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+    return AggregateExpr(expr, out.value, arg)

@@ -354,7 +354,7 @@ class ScalarFunction(Expr):
                         str=self.name.encode()))
 
 
-@dataclass(frozen=True, eq=True)
+@dataclass(frozen=True, eq=True, repr=False)
 class AggregateFunction(ScalarFunction):
     def _postfix(self, out):
         for a in self.args:

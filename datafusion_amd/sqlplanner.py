@@ -12,7 +12,7 @@ from __future__ import annotations
 import re
 from typing import List
 
-from .logicalplan import (BinaryExpr, Cast, Column, DataType, Float64, Int64, IsNotNull, IsNull,
+from .logicalplan import (AggregateFunction, BinaryExpr, Cast, Column, DataType, Float64, Int64, IsNotNull, IsNull,
                           Literal, Operator, PlanError, Utf8, binary_expr_coerced)
 
 _TOKEN = re.compile(r"""\s*(?:(?P<num>\d+\.\d*|\.\d+|\d+)|(?P<str>'(?:[^']|'')*')|(?P<op><>|!=|<=|>=|[=<>+\-*/%(),])|(?P<id>[A-Za-z_][A-Za-z0-9_]*))""")
@@ -82,6 +82,18 @@ class SqlToRel:
         if self._peek() == ("kw", "WHERE"):
             self.i += 1
             where = self._parse_expr(0, schema)
+        group_src = None
+        if self._peek()[0] == "id" and self._peek()[1].upper() == "GROUP":
+            self.i += 1
+            t = self._next()
+            if t[0] != "id" or t[1].upper() != "BY":
+                raise PlanError("expected BY")
+            group_src = []
+            while True:
+                group_src.append(self._parse_expr(0, schema))
+                if self._peek() != ("op", ","):
+                    break
+                self.i += 1
         if self.i != len(self.toks):
             raise PlanError("unexpected token %r" % (self.toks[self.i],))
         end = self.i
@@ -97,6 +109,10 @@ class SqlToRel:
         plan = TableScan(table, schema)
         if where is not None:
             plan = Selection(where, plan)
+        aggr = [e for e in exprs if isinstance(e, AggregateFunction)]
+        if aggr:  # sqlplanner.rs:80-117: only the aggregate expressions are kept
+            from .execution.context import Aggregate
+            return Aggregate(plan, group_src or [], aggr)
         return Projection(exprs, plan, None)
 
     # -- helpers
@@ -180,9 +196,31 @@ class SqlToRel:
                 self.i += 3
             self._expect("op", ")")
             return Cast(e, _TYPES[ty[1].upper()])
+        if t[0] == "id" and self._peek() == ("op", "("):  # SQLFunction (sqlplanner.rs:292-330)
+            return self._parse_function(t[1], schema)
         if t[0] == "id":
             for i, f in enumerate(schema.fields):
                 if f.name == t[1]:
                     return Column(i)
             raise PlanError("Invalid identifier '%s' for schema %s" % (t[1], schema.to_string()))
         raise PlanError("Unsupported ast node %r in sqltorel" % (t,))
+
+    def _parse_function(self, name, schema):
+        self._expect("op", "(")
+        lname = name.lower()
+        args = []
+        while self._peek() != ("op", ")"):
+            if lname == "count" and self._peek() in (("op", "*"), ("num", "1")):
+                self.i += 1  # COUNT(*) / COUNT(1) -> COUNT(first column)
+                args.append(Column(0))
+            else:
+                args.append(self._parse_expr(0, schema))
+            if self._peek() == ("op", ","):
+                self.i += 1
+        self._expect("op", ")")
+        if lname in ("min", "max", "sum", "avg"):
+            # return type is the argument's type (sqlplanner.rs:301-303)
+            return AggregateFunction(name, tuple(args), args[0].get_type(schema))
+        if lname == "count":
+            return AggregateFunction(name, tuple(args), DataType.UInt64)
+        raise PlanError("Invalid function '%s'" % name)

@@ -168,6 +168,13 @@ typedef struct dfmi_expr_node {
                                            commented out in the reference): the operand's
                                            validity as a non-null Boolean */
 
+#define DFMI_FLAG_EXT_AGGREGATE    0x10u /* LogicalPlan::Aggregate without GROUP BY
+                                           (sqlplanner.rs:91-117, compile_expr
+                                           expression.rs:81-116) instead of the
+                                           executor's unimplemented!() (context.rs:161):
+                                           MIN / MAX / SUM / COUNT over the selected
+                                           rows, semantics in DESIGN.md §2 */
+
 /* Opaque compiled expression: the RuntimeExpr::Compiled of expression.rs:43-50. */
 typedef struct dfmi_program dfmi_program;
 
@@ -264,6 +271,79 @@ int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main
  * (0 when its query shape was already compiled: the kernel cache is keyed by
  * the programs and the batch's column types / nullability). */
 int32_t dfmi_last_compile_ms(const dfmi_context* ctx, double* compile_ms);
+
+/* ---------------------------------------------------------------------------
+ * Aggregate extension (DFMI_FLAG_EXT_AGGREGATE). The reference plans
+ * `SELECT SUM(e), ... FROM t [WHERE p]` as Aggregate(Selection?(TableScan))
+ * (sqlplanner.rs:91-117) and compiles each AggregateFunction with
+ * compile_expr (expression.rs:81-116: one argument compiled by
+ * compile_scalar_expr, AggregateType Min/Max/Count/Sum), but its executor
+ * stops at `unimplemented!()` (context.rs:161). Here the whole pull --
+ * FilterRelation::next over every batch plus the aggregation -- is one fused
+ * pass per batch (no filtered batch is materialised), accumulated in a
+ * device state across batches. Semantics (build-defined, oracle-pinned):
+ *   COUNT(e): non-null values of e over the selected rows (UInt64);
+ *   SUM(e):   integers wrap in e's type; Float32/Float64 are the exact sum
+ *             rounded once (round half to even) -- independent of order,
+ *             batch and GPU count; a NaN input or +inf with -inf gives the
+ *             canonical quiet NaN, otherwise an infinite input gives that
+ *             infinity; an exact zero is -0.0 only if every value is -0.0;
+ *   MIN/MAX(e): NaN values are skipped (a set of only NaNs gives the
+ *             canonical NaN), -0.0 orders below +0.0;
+ *   SUM/MIN/MAX over no non-null value is null.
+ * GROUP BY is not implemented (NotImplemented).
+ * ------------------------------------------------------------------------- */
+typedef enum dfmi_agg_fn {       /* AggregateType (expression.rs:33-40) */
+    DFMI_AGG_MIN = 0,
+    DFMI_AGG_MAX = 1,
+    DFMI_AGG_SUM = 2,
+    DFMI_AGG_COUNT = 3
+} dfmi_agg_fn;
+
+typedef struct dfmi_agg_value {
+    int32_t type;      /* dfmi_type of the result (the AggregateFunction return_type) */
+    int32_t is_null;   /* 1: no non-null input value (SUM / MIN / MAX) */
+    int64_t count;     /* non-null input values aggregated */
+    uint64_t bits;     /* integers sign/zero-extended to 64 bits, Float32 bits in the
+                          low 32, Float64 bits */
+} dfmi_agg_value;
+
+typedef struct dfmi_aggregate dfmi_aggregate;
+
+/* compile_expr's AggregateFunction arm (expression.rs:81-116): `name` as the
+ * SQL text spells it (min / max / sum / count, any case; anything else panics
+ * in the reference: DFMI_ERR_PANIC), `argument` compiled by
+ * dfmi_compile_scalar_expr, `return_type` the planner's (sqlplanner.rs:296-330:
+ * the argument's type, UInt64 for count). */
+int32_t dfmi_compile_aggregate(const char* name, const dfmi_program* argument, int32_t return_type,
+                               uint32_t flags, dfmi_aggregate** out, dfmi_error* err);
+const char* dfmi_aggregate_name(const dfmi_aggregate* agg);
+int32_t dfmi_aggregate_type(const dfmi_aggregate* agg);
+void dfmi_aggregate_free(dfmi_aggregate* agg);
+
+/* Device accumulators of one Aggregate plan on one context. */
+typedef struct dfmi_agg_state dfmi_agg_state;
+
+int32_t dfmi_agg_state_create(dfmi_context* ctx, const dfmi_aggregate* const* aggs, int32_t num_aggs,
+                              dfmi_agg_state** out, dfmi_error* err);
+/* One batch of the aggregate's input (FilterRelation::next when predicate is
+ * non-NULL), accumulated on the device; asynchronous on the context stream
+ * except for error reporting, which is synchronous like dfmi_filter_project. */
+int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* state, const dfmi_program* predicate,
+                             const dfmi_batch* input, uint32_t flags, dfmi_error* err);
+/* The aggregate values over every batch so far (num_aggs entries). */
+int32_t dfmi_agg_state_finish(dfmi_context* ctx, dfmi_agg_state* state, dfmi_agg_value* out,
+                              dfmi_error* err);
+/* Multi-GPU: the exact partial state (count, flags, min/max key, integer sum,
+ * exact float sum digits) as dfmi_agg_partial_bytes() host bytes, and the
+ * merge of partials from every shard into final values -- bit-identical to
+ * one state over all the shards' rows. */
+int64_t dfmi_agg_partial_bytes(const dfmi_agg_state* state);
+int32_t dfmi_agg_state_partial(dfmi_context* ctx, dfmi_agg_state* state, void* host_out, dfmi_error* err);
+int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, int32_t num_aggs,
+                                const void* const* partials, int32_t num_partials, dfmi_agg_value* out,
+                                dfmi_error* err);
+void dfmi_agg_state_free(dfmi_agg_state* state);
 
 #ifdef __cplusplus
 }

@@ -855,6 +855,231 @@ Plan make_plan(const dfmi_expr_node* pred_nodes, int32_t pred_len,
     return p;
 }
 
+// ------------------------------------------------ Aggregate extension ---
+// LogicalPlan::Aggregate with no GROUP BY (sqlplanner.rs:91-117; compile_expr
+// expression.rs:81-116; the reference's executor stops at context.rs:161).
+// The input is pulled through FilterRelation::next batch by batch and each
+// argument is evaluated over the filtered batch, the reference's way; the
+// aggregation semantics are the build's (include/dfmi.h).
+
+// Exact sum of binary64 values: a 2176-bit two's complement integer in units
+// of 2^-1074 (every double is m * 2^(b-1074), m < 2^53, 0 <= b <= 2045).
+struct ExactSum {
+    static constexpr int W = 34;
+    uint64_t w[W] = {};
+    void add_shifted(uint64_t m, int b, bool neg) {
+        const int q = b / 64, r = b % 64;
+        uint64_t part[2] = {m << r, r ? (m >> (64 - r)) : 0};
+        if (!neg) {
+            unsigned __int128 c = 0;
+            for (int i = q; i < W; ++i) {
+                const uint64_t a = i - q < 2 ? part[i - q] : 0;
+                c += (unsigned __int128)w[i] + a;
+                w[i] = (uint64_t)c;
+                c >>= 64;
+                if (i - q >= 1 && c == 0) break;
+            }
+        } else {
+            uint64_t borrow = 0;
+            for (int i = q; i < W; ++i) {
+                const uint64_t a = i - q < 2 ? part[i - q] : 0;
+                const uint64_t x = w[i];
+                const uint64_t d = x - a - borrow;
+                borrow = (x < a) || (x - a < borrow) ? 1 : 0;
+                w[i] = d;
+                if (i - q >= 1 && borrow == 0) break;
+            }
+        }
+    }
+    void add(double v) {
+        uint64_t bits;
+        memcpy(&bits, &v, 8);
+        const int e = (int)((bits >> 52) & 0x7ff);
+        uint64_t m = bits & ((1ull << 52) - 1);
+        if (e) m |= 1ull << 52;
+        if (!m) return;
+        add_shifted(m, (e ? e : 1) - 1, bits >> 63);
+    }
+    // Round to a binary format with `prec` significand bits whose smallest
+    // quantum is 2^(qmin-1074); returns the value as a double (exact for
+    // Float32 results, which the caller narrows).
+    double round(int prec, int qmin, double overflow_limit, bool* zero) const {
+        uint64_t m[W];
+        const bool neg = w[W - 1] >> 63;
+        if (neg) {  // magnitude = two's complement negation
+            uint64_t c = 1;
+            for (int i = 0; i < W; ++i) {
+                m[i] = ~w[i] + c;
+                c = (c && m[i] == 0) ? 1 : 0;
+            }
+        } else {
+            memcpy(m, w, sizeof m);
+        }
+        int p = -1;
+        for (int i = W - 1; i >= 0; --i)
+            if (m[i]) {
+                p = 64 * i + 63 - __builtin_clzll(m[i]);
+                break;
+            }
+        *zero = p < 0;
+        if (p < 0) return 0.0;
+        auto bit = [&](int i) -> uint64_t { return i < 0 ? 0 : (m[i / 64] >> (i % 64)) & 1; };
+        int q = std::max(p - (prec - 1), qmin);
+        uint64_t mant = 0;
+        for (int i = p; i >= q; --i) mant = (mant << 1) | bit(i);
+        const uint64_t rb = q >= 1 ? bit(q - 1) : 0;
+        bool sticky = false;
+        for (int i = q - 2; i >= 0 && !sticky; --i) sticky = bit(i);
+        if (rb && (sticky || (mant & 1))) {
+            ++mant;
+            if (mant >> prec) {
+                mant >>= 1;
+                ++q;
+            }
+        }
+        double d = std::ldexp((double)mant, q - 1074);
+        if (d >= overflow_limit) d = std::numeric_limits<double>::infinity();
+        return neg ? -d : d;
+    }
+};
+
+// Total order of non-NaN values: -0.0 below +0.0.
+template <typename T>
+bool agg_less(T a, T b) {
+    if constexpr (std::is_floating_point<T>::value) {
+        if (a == b) return std::signbit(a) && !std::signbit(b);
+    }
+    return a < b;
+}
+
+struct AggState {
+    int fn = 0, arg_type = 0, ret_type = 0;
+    int64_t count = 0;
+    uint64_t isum = 0;            // wrapping integer sum
+    bool has_key = false;         // MIN/MAX: a non-NaN value seen
+    uint64_t key_bits = 0;        // ... its bits
+    bool nan = false, pinf = false, ninf = false, non_negzero = false;
+    ExactSum exact;
+};
+
+template <typename T>
+uint64_t to_bits64(T v) {
+    if constexpr (std::is_same<T, float>::value) {
+        uint32_t b;
+        memcpy(&b, &v, 4);
+        return b;
+    } else if constexpr (std::is_same<T, double>::value) {
+        uint64_t b;
+        memcpy(&b, &v, 8);
+        return b;
+    } else if constexpr (std::is_signed<T>::value) {
+        return (uint64_t)(int64_t)v;
+    } else {
+        return (uint64_t)v;
+    }
+}
+
+template <typename T>
+T from_bits64(uint64_t b) {
+    T v;
+    if constexpr (std::is_same<T, float>::value) {
+        uint32_t x = (uint32_t)b;
+        memcpy(&v, &x, 4);
+    } else if constexpr (std::is_same<T, double>::value) {
+        memcpy(&v, &b, 8);
+    } else {
+        v = (T)b;
+    }
+    return v;
+}
+
+void agg_accumulate(AggState& st, const Array& a) {
+    for (int64_t i = 0; i < a.len; ++i) {
+        if (a.is_null(i)) continue;
+        ++st.count;
+        if (st.fn == DFMI_AGG_COUNT) continue;
+        dispatch_numeric(a.type, [&](auto tag) {
+            using T = decltype(tag);
+            const T v = a.value<T>(i);
+            if constexpr (std::is_floating_point<T>::value) {
+                if (std::isnan(v)) {
+                    st.nan = true;
+                    return;
+                }
+                if (st.fn == DFMI_AGG_SUM) {
+                    if (std::isinf(v)) {
+                        (v > 0 ? st.pinf : st.ninf) = true;
+                        return;
+                    }
+                    if (!(v == 0 && std::signbit(v))) st.non_negzero = true;
+                    st.exact.add((double)v);
+                    return;
+                }
+            } else {
+                if (st.fn == DFMI_AGG_SUM) {
+                    st.isum += (uint64_t)v;  // wraps in u64, narrowed at the end
+                    return;
+                }
+            }
+            const T cur = from_bits64<T>(st.key_bits);
+            const bool take = !st.has_key || (st.fn == DFMI_AGG_MIN ? agg_less(v, cur) : agg_less(cur, v));
+            if (take) st.key_bits = to_bits64(v);
+            st.has_key = true;
+        });
+    }
+}
+
+dfmi_agg_value agg_result(const AggState& st) {
+    dfmi_agg_value r;
+    r.type = st.ret_type;
+    r.count = st.count;
+    r.is_null = 0;
+    r.bits = 0;
+    if (st.fn == DFMI_AGG_COUNT) {
+        r.bits = (uint64_t)st.count;
+        return r;
+    }
+    if (st.count == 0) {
+        r.is_null = 1;
+        return r;
+    }
+    const bool f32 = st.arg_type == DFMI_TYPE_FLOAT32, f64 = st.arg_type == DFMI_TYPE_FLOAT64;
+    const uint64_t qnan = f32 ? 0x7FC00000ull : 0x7FF8000000000000ull;
+    if (st.fn == DFMI_AGG_SUM) {
+        if (f32 || f64) {
+            if (st.nan || (st.pinf && st.ninf)) {
+                r.bits = qnan;
+            } else if (st.pinf || st.ninf) {
+                r.bits = f32 ? to_bits64(st.pinf ? INFINITY : -INFINITY)
+                             : to_bits64(st.pinf ? (double)INFINITY : -(double)INFINITY);
+            } else {
+                bool zero = false;
+                double d = f32 ? st.exact.round(24, 925, 0x1p128, &zero) : st.exact.round(53, 0, INFINITY, &zero);
+                if (zero) d = st.non_negzero ? 0.0 : -0.0;
+                r.bits = f32 ? to_bits64((float)d) : to_bits64(d);
+            }
+        } else {
+            dispatch_numeric(st.arg_type, [&](auto tag) {
+                using T = decltype(tag);
+                r.bits = to_bits64((T)st.isum);  // wrapping: the low bits of the sum
+            });
+        }
+        return r;
+    }
+    r.bits = st.has_key ? st.key_bits : qnan;  // only NaNs seen: the canonical NaN
+    return r;
+}
+
+int agg_fn_of(const std::string& name) {
+    std::string l = name;
+    for (auto& c : l) c = (char)tolower((unsigned char)c);
+    if (l == "min") return DFMI_AGG_MIN;
+    if (l == "max") return DFMI_AGG_MAX;
+    if (l == "count") return DFMI_AGG_COUNT;
+    if (l == "sum") return DFMI_AGG_SUM;
+    fail(DFMI_ERR_PANIC, "not yet implemented: Unsupported aggregate function '" + name + "'");
+}
+
 void set_err(dfmi_error* err, int32_t code, const std::string& m) {
     if (!err) return;
     err->code = code;
@@ -944,6 +1169,45 @@ int32_t oracle_compile_info(const dfmi_expr_node* nodes, int32_t n, const dfmi_s
         Runtime r = compile(*t, *schema, flags);
         if (name && cap > 0) snprintf(name, (size_t)cap, "%s", r.name.c_str());
         if (type) *type = r.t;
+        return DFMI_OK;
+    } catch (const ExecError& e) {
+        set_err(err, e.code, e.msg);
+        return e.code;
+    }
+}
+
+int32_t oracle_aggregate(const dfmi_expr_node* pred_nodes, int32_t pred_len, const char* const* names,
+                         const dfmi_expr_node* const* arg_nodes, const int32_t* arg_lens,
+                         const int32_t* return_types, int32_t n, const dfmi_schema* schema,
+                         const dfmi_batch* input, int64_t batch_rows, uint32_t flags, dfmi_agg_value* out,
+                         dfmi_error* err) {
+    try {
+        set_err(err, DFMI_OK, "");
+        if (!(flags & DFMI_FLAG_EXT_AGGREGATE)) fail(DFMI_ERR_PANIC, "not yet implemented");  // context.rs:161
+        // context.rs order: the input (Selection) first, then compile_expr per aggregate
+        Plan p = make_plan(pred_nodes, pred_len, nullptr, nullptr, 0, schema, flags);
+        std::vector<Runtime> args;
+        std::vector<AggState> st(n);
+        for (int j = 0; j < n; ++j) {
+            const int fn = agg_fn_of(names[j]);
+            ExprP t = build_tree(arg_nodes[j], arg_lens[j]);
+            args.push_back(compile(*t, *schema, flags));
+            st[j].fn = fn;
+            st[j].arg_type = args[j].t;
+            st[j].ret_type = return_types[j];
+            const int want = fn == DFMI_AGG_COUNT ? DFMI_TYPE_UINT64 : args[j].t;
+            if (return_types[j] != want) fail(DFMI_ERR_INVALID_ARGUMENT, "aggregate return type");
+            if (fn != DFMI_AGG_COUNT && !is_numeric(args[j].t))
+                fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("aggregate over ") + type_name(args[j].t));
+        }
+        if (batch_rows <= 0) batch_rows = std::max<int64_t>(1, input->num_rows);
+        for (int64_t r0 = 0; r0 < input->num_rows; r0 += batch_rows) {
+            const int64_t rows = std::min(batch_rows, input->num_rows - r0);
+            Batch in = wrap_input(input, r0, rows);
+            Batch f = run_batch(p, in, flags);  // FilterRelation::next (or the batch itself)
+            for (int j = 0; j < n; ++j) agg_accumulate(st[j], *args[j].f(f));
+        }
+        for (int j = 0; j < n; ++j) out[j] = agg_result(st[j]);
         return DFMI_OK;
     } catch (const ExecError& e) {
         set_err(err, e.code, e.msg);

@@ -55,6 +55,15 @@ int32_t oracle_compile_info(const dfmi_expr_node* nodes, int32_t n, const dfmi_s
                             uint32_t flags, char* name, int64_t name_cap, int32_t* type,
                             dfmi_error* err);
 
+/* Aggregate extension (DFMI_FLAG_EXT_AGGREGATE): Aggregate(Selection?(scan))
+ * with no GROUP BY over `input` pulled in batches of batch_rows (<= 0: one
+ * batch); aggregate j is names[j](arg j) with the planner's return type. */
+int32_t oracle_aggregate(const dfmi_expr_node* pred_nodes, int32_t pred_len, const char* const* names,
+                         const dfmi_expr_node* const* arg_nodes, const int32_t* arg_lens,
+                         const int32_t* return_types, int32_t num_aggs, const dfmi_schema* schema,
+                         const dfmi_batch* input, int64_t batch_rows, uint32_t flags, dfmi_agg_value* out,
+                         dfmi_error* err);
+
 /* Synthetic tables, bit-identical to the device generator. */
 uint64_t oracle_splitmix64(uint64_t x);
 void oracle_gen_unit_f64(uint64_t seed, uint32_t col, int64_t row0, int64_t n, double* out);

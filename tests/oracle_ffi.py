@@ -44,6 +44,10 @@ def oracle_lib() -> C.CDLL:
     L.oracle_compile_info.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(_abi.dfmi_schema), C.c_uint32,
                                       C.c_char_p, C.c_int64, P(C.c_int32), P(_abi.dfmi_error)]
     L.oracle_compile_info.restype = C.c_int32
+    L.oracle_aggregate.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(C.c_char_p), P(P(_abi.dfmi_expr_node)),
+                                   P(C.c_int32), P(C.c_int32), C.c_int32, P(_abi.dfmi_schema), P(_abi.dfmi_batch),
+                                   C.c_int64, C.c_uint32, P(_abi.dfmi_agg_value), P(_abi.dfmi_error)]
+    L.oracle_aggregate.restype = C.c_int32
     L.oracle_gen_unit_f64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_void_p]
     L.oracle_gen_i64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_void_p]
     _L = L
@@ -171,3 +175,29 @@ def gen_i64(seed: int, col: int, row0: int, n: int, lo: int, hi: int) -> np.ndar
     out = np.empty(n, dtype=np.int64)
     oracle_lib().oracle_gen_i64(seed, col, row0, n, lo, hi, out.ctypes.data)
     return out
+
+
+def oracle_aggregate(schema: Schema, batch: RecordBatch, pred: Optional[Expr], aggs: Sequence, flags: int = None,
+                     batch_rows: int = 0):
+    """Aggregate(Selection?(scan)) on the oracle: aggs are logicalplan
+    AggregateFunction expressions; returns dfmi_agg_value per aggregate, or
+    raises ExecutionError. batch_rows > 0 pulls the input in batches."""
+    if flags is None:
+        flags = _abi.DFMI_FLAG_EXT_AGGREGATE
+    L = oracle_lib()
+    hb = Batched(batch)
+    sch, keep = _abi.make_schema([(f.name, f.data_type, f.nullable) for f in schema.fields])
+    pn = _abi.PostfixNodes(pred.to_postfix()) if pred is not None else None
+    arg_nodes = [_abi.PostfixNodes(a.args[0].to_postfix()) for a in aggs]
+    names = (C.c_char_p * len(aggs))(*[a.name.encode() for a in aggs])
+    arr = (C.POINTER(_abi.dfmi_expr_node) * len(aggs))(*[C.cast(x.array, C.POINTER(_abi.dfmi_expr_node))
+                                                           for x in arg_nodes])
+    lens = (C.c_int32 * len(aggs))(*[x.length for x in arg_nodes])
+    rts = (C.c_int32 * len(aggs))(*[int(a.return_type) for a in aggs])
+    out = (_abi.dfmi_agg_value * len(aggs))()
+    err = _abi.dfmi_error()
+    rc = L.oracle_aggregate(pn.array if pn else None, pn.length if pn else 0, names, arr, lens, rts, len(aggs),
+                            C.byref(sch), C.byref(hb.cb), batch_rows, flags, out, C.byref(err))
+    if rc != _abi.DFMI_OK:
+        raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+    return list(out)
