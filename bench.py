@@ -262,6 +262,62 @@ def q6_line(eng, dev, rank, world, steps, warmup, dist, rows):
                          "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_row": round(bpr, 3)}}
 
 
+def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
+    """Real TPC-H Q6 (DFMI_FLAG_EXT_AGGREGATE): SELECT SUM(l_extendedprice *
+    l_discount) FROM lineitem WHERE <Q6 predicate>, one fused predicate +
+    exact-sum pass per step over the C4 table; with --gpus N every rank's exact
+    partial is all_gathered and merged (bit-identical to one GPU over all rows).
+    Gate: the SUM over a 4M-row prefix equals the oracle's bit for bit."""
+    from datafusion_amd.arrow import Array, RecordBatch
+    from datafusion_amd.execution.engine import merge_agg_partials
+    from datafusion_amd.execution.expression import compile_expr
+    from datafusion_amd.logicalplan import AggregateFunction
+    from oracle_ffi import oracle_aggregate
+    flags = _abi.DFMI_FLAG_EXT_AGGREGATE
+    n = rows
+    schema, cols = q6_table(dev, n, SEED + rank)
+    pred_e, projs = q6_query()
+    sum_e = AggregateFunction("SUM", (projs[0],), DataType.Float64)
+    pred = compile_scalar_expr(None, pred_e, schema, flags)
+    agg = compile_expr(None, sum_e, schema, flags)
+    st = eng.agg_state([agg])
+    batch = RecordBatch(schema, [Array(DataType.Float64, n, c.view(torch.uint8)) for c in cols])
+    res = {}
+
+    def step():
+        st.reset()
+        st.add(pred, batch, flags)
+        if dist:
+            mine = torch.frombuffer(bytearray(st.partial()), dtype=torch.uint8).to(dev)
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            v = merge_agg_partials([agg], [p.cpu().numpy().tobytes() for p in parts])[0]
+        else:
+            v = st.finish()[0]
+        res["v"] = v
+        return v.count
+
+    el, kms, selected = timed_steps(step, steps, warmup, dist, eng, dev)
+    # gate: 4M-row prefix against the oracle
+    m = min(n, 1 << 22)
+    pre = RecordBatch(schema, [Array(DataType.Float64, m, c[:m].view(torch.uint8)) for c in cols])
+    g = eng.agg_state([agg])
+    g.add(pred, pre, flags)
+    dv = g.finish()[0]
+    rv = oracle_aggregate(schema, pre.to("cpu"), pred_e, [sum_e], flags)[0]
+    gate = {"rows": m, "sum_bits_equal": bool(dv.bits == rv.bits and dv.count == rv.count), "count": int(rv.count)}
+    s = selected / n
+    bpr = 32.0  # SURVEY §8(d): 4 Float64 inputs; the output is one value
+    ach = n * bpr / (kms * 1e-3) / 1e9
+    v = res["v"]
+    return {"workload": "C4 real Q6: SELECT SUM(l_extendedprice*l_discount) FROM lineitem WHERE <Q6>, 600037902 "
+                        "rows per GPU, exact Float64 sum", "rows_per_s": n * world * steps / el,
+            "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4), "selectivity": round(s, 5),
+            "sum": float(np.array([v.bits], dtype=np.uint64).view(np.float64)[0]), "parity_gate": gate,
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_row": bpr}}
+
+
 def q6_table(dev, n, seed):
     """C4 synthetic lineitem columns in HBM: quantity 1..50,
     extendedprice = quantity * U[900, 2000), discount 0.00..0.10, shipdate day
@@ -478,8 +534,8 @@ def main():
     ap.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
     ap.add_argument("--sel", type=float, default=0.5, help="headline selectivity")
     ap.add_argument("--sweep", default="0.01,0.5,0.99", help="selectivities also reported (first=headline if set)")
-    ap.add_argument("--extra", default="c4,c3,batches",
-                    help="extra config lines (comma list: c4,c3,batches,host; empty = none)")
+    ap.add_argument("--extra", default="c4,q6,c3,batches",
+                    help="extra config lines (comma list: c4,q6,c3,batches,host; empty = none)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -531,6 +587,8 @@ def main():
             continue
         if name == "c4":
             extra["c4"] = q6_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS)
+        elif name == "q6":
+            extra["q6"] = q6_agg_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS)
         elif name == "host":
             if world == 1:
                 extra["host"] = host_line(eng, min(args.steps, 3), 1)

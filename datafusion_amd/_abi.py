@@ -113,6 +113,14 @@ class dfmi_out_column(C.Structure):
     ]
 
 
+class dfmi_shard_placement(C.Structure):
+    _fields_ = [("world", C.c_int32), ("rank", C.c_int32), ("row_offset", C.c_int64), ("total_rows", C.c_int64),
+                ("utf8_base", C.c_int64 * 16), ("utf8_total", C.c_int64 * 16), ("null_total", C.c_int64 * 16)]
+
+
+DFMI_SHARD_ID_BYTES = 128
+
+
 class dfmi_agg_value(C.Structure):
     _fields_ = [("type", C.c_int32), ("is_null", C.c_int32), ("count", C.c_int64), ("bits", C.c_uint64)]
 
@@ -143,6 +151,13 @@ EXPORTED = [
     "dfmi_agg_partial_bytes",
     "dfmi_agg_state_partial",
     "dfmi_agg_merge_partials",
+    "dfmi_agg_state_reset",
+    "dfmi_shard_unique_id",
+    "dfmi_shard_comm_init",
+    "dfmi_shard_comm_destroy",
+    "dfmi_shard_filter_project",
+    "dfmi_shard_gather_to_root",
+    "dfmi_shard_agg_finish",
     "dfmi_agg_state_free",
     "dfmi_generate_column",  # include/dfmi_datasource.h
 ]
@@ -258,6 +273,24 @@ def lib() -> C.CDLL:
     L.dfmi_agg_merge_partials.argtypes = [P(C.c_void_p), C.c_int32, P(C.c_void_p), C.c_int32, P(dfmi_agg_value),
                                           P(dfmi_error)]
     L.dfmi_agg_merge_partials.restype = C.c_int32
+    L.dfmi_agg_state_reset.argtypes = [C.c_void_p, C.c_void_p, P(dfmi_error)]
+    L.dfmi_agg_state_reset.restype = C.c_int32
+    L.dfmi_shard_unique_id.argtypes = [C.c_void_p, P(dfmi_error)]
+    L.dfmi_shard_unique_id.restype = C.c_int32
+    L.dfmi_shard_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, P(C.c_void_p), P(dfmi_error)]
+    L.dfmi_shard_comm_init.restype = C.c_int32
+    L.dfmi_shard_comm_destroy.argtypes = [C.c_void_p]
+    L.dfmi_shard_comm_destroy.restype = None
+    L.dfmi_shard_filter_project.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_void_p), C.c_int32,
+                                            P(dfmi_batch), P(dfmi_out_column), C.c_uint32, P(dfmi_shard_placement),
+                                            P(dfmi_error)]
+    L.dfmi_shard_filter_project.restype = C.c_int32
+    L.dfmi_shard_gather_to_root.argtypes = [C.c_void_p, C.c_void_p, P(dfmi_out_column), P(dfmi_out_column), C.c_int32,
+                                            P(dfmi_error)]
+    L.dfmi_shard_gather_to_root.restype = C.c_int32
+    L.dfmi_shard_agg_finish.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_void_p), C.c_int32,
+                                        P(dfmi_agg_value), P(dfmi_error)]
+    L.dfmi_shard_agg_finish.restype = C.c_int32
     L.dfmi_agg_state_free.argtypes = [C.c_void_p]
     L.dfmi_agg_state_free.restype = None
     _LIB = L

@@ -38,6 +38,7 @@ struct dfmi_agg_state {
     size_t acc_words = 0;
     bool failed = false;      // a batch raised an error: the query has failed
     dfmi_error failure{};
+    std::vector<uint64_t> init;  // the zero state (MIN keys all ones)
 };
 
 namespace {
@@ -370,6 +371,7 @@ extern "C" int32_t dfmi_agg_state_create(dfmi_context* ctx, const dfmi_aggregate
         HIP_TRY(hipMalloc((void**)&st->acc, st->acc_words * 8));
         HIP_TRY(hipMemcpyAsync(st->acc, init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
+        st->init = std::move(init);
         *out = st;
         return DFMI_OK;
     } catch (const Fail& f) {
@@ -377,6 +379,21 @@ extern "C" int32_t dfmi_agg_state_create(dfmi_context* ctx, const dfmi_aggregate
             if (st->acc) (void)hipFree(st->acc);
             delete st;
         }
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+        st->failed = false;
+        st->failure = dfmi_error{};
+        return DFMI_OK;
+    } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
         return f.code;
     }

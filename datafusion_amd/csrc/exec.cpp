@@ -298,6 +298,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                                        const dfmi_batch* in, dfmi_out_column* outs, uint32_t flags,
                                        dfmi_error* err) {
     set_err(err, DFMI_OK, "");
+    if (ctx) ctx->last_err_key = ~0ull;
     try {
         if (!ctx || !in || (np > 0 && !projs) || !outs || (in->num_columns > 0 && !in->columns))
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
@@ -432,10 +433,14 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         if (dev_kind == ERRK_LOOKBACK_TIMEOUT) throw Fail{DFMI_ERR_DEVICE, "device look-back timed out"};
         if (dev_kind == ERRK_CAPACITY) throw Fail{DFMI_ERR_CAPACITY, "Utf8 output data_capacity too small"};
         if (dev_kind && (!se.set || dev_key < se.key)) {
+            ctx->last_err_key = dev_key;
             if (dev_kind == ERRK_DIV_ZERO) throw Fail{DFMI_ERR_DIVIDE_BY_ZERO, "DivideByZero"};
             throw Fail{DFMI_ERR_PANIC, "attempt to divide with overflow"};
         }
-        if (se.set) throw Fail{se.code, se.msg};
+        if (se.set) {
+            ctx->last_err_key = se.key;
+            throw Fail{se.code, se.msg};
+        }
 
         // ---- results
         uint64_t totals[24];

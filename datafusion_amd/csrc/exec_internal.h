@@ -38,6 +38,9 @@ struct dfmi_context {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_total_ms = 0, last_main_ms = 0, last_compile_ms = 0;
     bool timed = false;
+    // evaluation-order key (ordinal << 44 | row << 4) of the error the last
+    // dfmi_filter_project raised; ~0 for none / an error outside that order
+    uint64_t last_err_key = ~0ull;
 };
 
 namespace dfmi {

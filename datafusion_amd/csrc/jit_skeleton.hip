@@ -93,6 +93,12 @@ __device__ __forceinline__ const T* at(const B* base, i64 off) {
 }
 __device__ __forceinline__ u64 bits(double x) { return __builtin_bit_cast(u64, x); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// Lane i's 32 bits, zero-extended (the builtin returns int: a plain cast to
+// 64 bits would sign-extend).
+__device__ __forceinline__ u64 readlane_u(unsigned v, int i) { return (u64)(unsigned)__builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ u64 readlane_u64(u64 v, int i) {
+    return (readlane_u((unsigned)(v >> 32), i) << 32) | readlane_u((unsigned)v, i);
+}
 
 __device__ __forceinline__ unsigned lane_rank(u64 mask) {  // set bits below this lane
     return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
@@ -138,8 +144,7 @@ __device__ __forceinline__ u64 wave_incl_scan(u64 v, int lane) {
 // Sum over the wave (uniform result).
 __device__ __forceinline__ u64 wave_sum(u64 v) {
     const u64 t = wave_incl_scan(v, 0);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)t, 63), hi = __builtin_amdgcn_readlane((unsigned)(t >> 32), 63);
-    return ((u64)hi << 32) | lo;
+    return readlane_u64(t, 63);
 }
 
 // The value of the next lane (lane 63: 0).
@@ -492,7 +497,7 @@ __device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, 
         for (int k = 0; k < K; ++k) {
             // Utf8 byte counts of one slice fit 32 bits (an array holds < 2^31 bytes)
             const u64 s = ch == 0 ? (u64)__builtin_popcountll(__ballot(cnt[0][k] != 0))
-                                  : (u64)__builtin_amdgcn_readlane(wave_incl_scan32(cnt[ch][k], lane), 63);
+                                  : readlane_u(wave_incl_scan32(cnt[ch][k], lane), 63);
             if (lane == 0) T.cnt[ch][k * WAVES + wave] = s;
         }
     lds_sync();
@@ -516,8 +521,7 @@ __device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, 
                 if (w < NW) T.excl[ch][w] = ex;
                 ex += c[i];
             }
-            const u64 agg = ((u64)__builtin_amdgcn_readlane((unsigned)(incl >> 32), 63) << 32) |
-                            __builtin_amdgcn_readlane((unsigned)incl, 63);
+            const u64 agg = readlane_u64(incl, 63);
             if constexpr (NCH == 2) {
                 packed |= agg << (31 * ch);
             } else {
@@ -695,7 +699,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
         const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
         const unsigned incl = wave_incl_scan32(L, lane);
         const unsigned rel = incl - L;
-        const unsigned Ls = __builtin_amdgcn_readlane(incl, 63);
+        const unsigned Ls = (unsigned)readlane_u(incl, 63);
         const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
         if (sel) A.out_offs[o][obase + dst[k]] = (int)(ob0 + rel);
         if ((i64)(ob0 + Ls) > A.out_cap[o]) {
@@ -814,7 +818,7 @@ __device__ __forceinline__ u64 wave_minmax(u64 v) {
     DFMI_MM_STEP(0x111, 0xf) DFMI_MM_STEP(0x112, 0xf) DFMI_MM_STEP(0x114, 0xf)
     DFMI_MM_STEP(0x118, 0xf) DFMI_MM_STEP(0x142, 0xa) DFMI_MM_STEP(0x143, 0xc)
 #undef DFMI_MM_STEP
-    return ((u64)__builtin_amdgcn_readlane((unsigned)(v >> 32), 63) << 32) | __builtin_amdgcn_readlane((unsigned)v, 63);
+    return readlane_u64(v, 63);
 }
 
 // Block-level (LDS) state of NA aggregates, NF of them exact float sums.

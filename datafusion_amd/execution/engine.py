@@ -92,9 +92,11 @@ class DeviceEngine:
         return oc, keep
 
     def filter_project(self, predicate, projections: Optional[Sequence], batch: RecordBatch,
-                       flags: int = 0) -> List[Array]:
+                       flags: int = 0, comm: "ShardComm" = None) -> List[Array]:
         """One pull of ProjectRelation(FilterRelation(batch)). ``predicate`` /
-        ``projections`` are RuntimeExprs (None / [] when absent)."""
+        ``projections`` are RuntimeExprs (None / [] when absent). With a
+        ShardComm the pass is this rank's shard (dfmi_shard_filter_project):
+        the placement lands in comm.placement, the outputs in comm.outputs."""
         L = _abi.lib()
         batch = self.to_device(batch)
         n = batch.num_rows()
@@ -133,8 +135,15 @@ class DeviceEngine:
         progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
         err = _abi.dfmi_error()
         L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
-        rc = L.dfmi_filter_project(self.ctx, predicate.handle if predicate is not None else None,
-                                   progs, len(projections), C.byref(cb), outs, flags, C.byref(err))
+        if comm is None:
+            rc = L.dfmi_filter_project(self.ctx, predicate.handle if predicate is not None else None,
+                                       progs, len(projections), C.byref(cb), outs, flags, C.byref(err))
+        else:
+            place = _abi.dfmi_shard_placement()
+            rc = L.dfmi_shard_filter_project(self.ctx, comm.handle, predicate.handle if predicate is not None else None,
+                                             progs, len(projections), C.byref(cb), outs, flags, C.byref(place),
+                                             C.byref(err))
+            comm.placement, comm.outputs, comm.keep = place, outs, (keeps, out_types)
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
         result = []
@@ -249,6 +258,12 @@ class AggState:
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
 
+    def reset(self) -> None:
+        err = _abi.dfmi_error()
+        rc = _abi.lib().dfmi_agg_state_reset(self.eng.ctx, self.handle, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+
     def finish(self) -> List[_abi.dfmi_agg_value]:
         out = (_abi.dfmi_agg_value * len(self.aggs))()
         err = _abi.dfmi_error()
@@ -289,3 +304,79 @@ def merge_agg_partials(aggs: Sequence, partials: Sequence[bytes]) -> List[_abi.d
     if rc != _abi.DFMI_OK:
         raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
     return list(out)
+
+
+class ShardComm:
+    """dfmi_shard_comm: the RCCL communicator of the C-ABI multi-GPU entry
+    points (include/dfmi.h "Multi-GPU"), one per rank."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(_abi.DFMI_SHARD_ID_BYTES)
+        err = _abi.dfmi_error()
+        rc = _abi.lib().dfmi_shard_unique_id(buf, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        return buf.raw
+
+    def __init__(self, eng: DeviceEngine, world: int, rank: int, uid: bytes):
+        self.eng = eng
+        self.world, self.rank = world, rank
+        out = C.c_void_p()
+        err = _abi.dfmi_error()
+        idb = C.create_string_buffer(uid, _abi.DFMI_SHARD_ID_BYTES)
+        rc = _abi.lib().dfmi_shard_comm_init(eng.ctx, world, rank, idb, C.byref(out), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        self.handle = out
+        self.placement = None
+        self.outputs = None
+        self.keep = None
+
+    def gather_to_root(self, cols: List[Array], root: int = 0) -> Optional[List[Array]]:
+        """The last shard pass's outputs concatenated on `root` (collective)."""
+        place = self.placement
+        n = place.total_rows
+        L = _abi.lib()
+        routs = (_abi.dfmi_out_column * max(1, len(cols)))()
+        keeps = []
+        if self.rank == root:
+            for o, a in enumerate(cols):
+                oc, keep = self.eng._alloc_out(a.data_type, n, bool(place.null_total[o]), int(place.utf8_total[o]))
+                routs[o] = oc
+                keeps.append(keep)
+        err = _abi.dfmi_error()
+        rc = L.dfmi_shard_gather_to_root(self.eng.ctx, self.handle, self.outputs, routs, root, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        if self.rank != root:
+            return None
+        out = []
+        for o, a in enumerate(cols):
+            k = keeps[o]
+            if a.data_type == DataType.Utf8:
+                out.append(Array(a.data_type, n, k["data"], None, k["offsets"], 0))
+            else:
+                nulls = int(place.null_total[o])
+                out.append(Array(a.data_type, n, k["values"], k.get("validity") if nulls else None, None, nulls))
+        return out
+
+    def agg_finish(self, state: "AggState") -> List[_abi.dfmi_agg_value]:
+        """Every rank's exact aggregate partial merged (collective)."""
+        arr = (C.c_void_p * len(state.aggs))(*[a.handle.value for a in state.aggs])
+        out = (_abi.dfmi_agg_value * len(state.aggs))()
+        err = _abi.dfmi_error()
+        rc = _abi.lib().dfmi_shard_agg_finish(self.eng.ctx, self.handle, state.handle, arr, len(state.aggs), out,
+                                              C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        return list(out)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _abi.lib().dfmi_shard_comm_destroy(h)
+            except Exception:
+                pass
+            self.handle = C.c_void_p(0)

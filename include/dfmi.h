@@ -343,7 +343,58 @@ int32_t dfmi_agg_state_partial(dfmi_context* ctx, dfmi_agg_state* state, void* h
 int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, int32_t num_aggs,
                                 const void* const* partials, int32_t num_partials, dfmi_agg_value* out,
                                 dfmi_error* err);
+/* Back to the empty state (asynchronous on the context stream): re-running the query. */
+int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
 void dfmi_agg_state_free(dfmi_agg_state* state);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU. The reference is single-threaded (context.rs:33);
+ * its pull is Relation::next (relation.rs:27-32). Rows are independent
+ * through the Selection / Projection path and filter() keeps row order
+ * (filter.rs:87-91), so a table shards by row range: one host thread or
+ * process per GPU, each with its own context, calls the shard entry points
+ * below on its own rows; per-rank outputs in rank order are the reference's
+ * output stream. The only collective is one RCCL all_gather of a few int64
+ * per rank after each pass (placement and errors); gathering results on one
+ * rank is optional (grouped send/recv over xGMI).
+ * ------------------------------------------------------------------------- */
+#define DFMI_SHARD_ID_BYTES 128
+typedef struct dfmi_shard_comm dfmi_shard_comm;
+
+typedef struct dfmi_shard_placement {
+    int32_t world, rank;
+    int64_t row_offset;       /* first global output row of this rank's outputs */
+    int64_t total_rows;       /* output rows over all ranks */
+    int64_t utf8_base[16];    /* per output: global byte offset of this rank's Utf8 data */
+    int64_t utf8_total[16];   /* per output: Utf8 bytes over all ranks */
+    int64_t null_total[16];   /* per output: nulls over all ranks */
+} dfmi_shard_placement;
+
+/* A new RCCL unique id (rank 0), to be handed to every rank out of band. */
+int32_t dfmi_shard_unique_id(uint8_t* id /* DFMI_SHARD_ID_BYTES */, dfmi_error* err);
+/* Collective over `world` ranks (ncclCommInitRank on the context's device). */
+int32_t dfmi_shard_comm_init(dfmi_context* ctx, int32_t world, int32_t rank, const uint8_t* id,
+                             dfmi_shard_comm** out, dfmi_error* err);
+void dfmi_shard_comm_destroy(dfmi_shard_comm* comm);
+/* dfmi_filter_project over this rank's rows, then the placement exchange.
+ * Collective: every rank calls it. When any rank fails, every rank returns
+ * the error the reference would raise over the whole table (the smallest
+ * evaluation position, then the earliest rows). */
+int32_t dfmi_shard_filter_project(dfmi_context* ctx, dfmi_shard_comm* comm, const dfmi_program* predicate,
+                                  const dfmi_program* const* projections, int32_t num_projections,
+                                  const dfmi_batch* input, dfmi_out_column* outputs, uint32_t flags,
+                                  dfmi_shard_placement* placement, dfmi_error* err);
+/* Concatenate the last dfmi_shard_filter_project outputs on `root`, in rank
+ * order (collective). `root_outputs` (root only) are device buffers sized for
+ * placement.total_rows / utf8_total; Utf8 offsets are rebased, bitmaps
+ * re-aligned. Fails (Capacity) if a gathered Utf8 column would pass 2^31 bytes. */
+int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm* comm, const dfmi_out_column* local_outputs,
+                                  const dfmi_out_column* root_outputs, int32_t root, dfmi_error* err);
+/* Aggregate extension across ranks (collective): every rank's exact partial
+ * all_gathered and merged -- the values one GPU would produce over all rows. */
+int32_t dfmi_shard_agg_finish(dfmi_context* ctx, dfmi_shard_comm* comm, dfmi_agg_state* state,
+                              const dfmi_aggregate* const* aggs, int32_t num_aggs, dfmi_agg_value* out,
+                              dfmi_error* err);
 
 #ifdef __cplusplus
 }

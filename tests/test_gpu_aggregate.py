@@ -40,18 +40,17 @@ def slice_batch(b: RecordBatch, r0: int, n: int) -> RecordBatch:
     for a in b.columns:
         t = a.data_type
         v = a.validity[r0 // 8:] if a.validity is not None else None
-        if t == DataType.Utf8:
-            c = Array(t, n, a.values, v, a.offsets[r0:r0 + n + 1], 0)
-        elif t == DataType.Boolean:
-            c = Array(t, n, a.values[r0 // 8:], v, None, 0)
-        else:
-            w = t.width
-            c = Array(t, n, a.values[r0 * w:(r0 + n) * w], v, None, 0)
+        nulls = 0
         if v is not None:
             bits = np.unpackbits(v[: (n + 7) // 8].cpu().numpy(), bitorder="little")[:n]
-            c.null_count = int(n - bits.sum())
-            if c.null_count == 0:
-                c.validity = None
+            nulls = int(n - bits.sum())
+        if t == DataType.Utf8:
+            c = Array(t, n, a.values, v, a.offsets[r0:r0 + n + 1], nulls)
+        elif t == DataType.Boolean:
+            c = Array(t, n, a.values[r0 // 8:], v, None, nulls)
+        else:
+            w = t.width
+            c = Array(t, n, a.values[r0 * w:(r0 + n) * w], v, None, nulls)
         cols.append(c)
     return RecordBatch(b.schema, cols)
 
