@@ -287,6 +287,12 @@ extern "C" int32_t dfmi_last_timing(const dfmi_context* c, double* total_ms, dou
     return DFMI_OK;
 }
 
+extern "C" int32_t dfmi_last_error_order(const dfmi_context* c, uint64_t* key) {
+    if (!c || !key) return DFMI_ERR_INVALID_ARGUMENT;
+    *key = c->last_err_key;
+    return DFMI_OK;
+}
+
 extern "C" int32_t dfmi_last_compile_ms(const dfmi_context* c, double* compile_ms) {
     if (!c || !compile_ms) return DFMI_ERR_INVALID_ARGUMENT;
     *compile_ms = c->last_compile_ms;

@@ -145,7 +145,11 @@ class DeviceEngine:
                                              C.byref(err))
             comm.placement, comm.outputs, comm.keep = place, outs, (keeps, out_types)
         if rc != _abi.DFMI_OK:
-            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+            e = ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+            key = C.c_uint64()
+            L.dfmi_last_error_order(self.ctx, C.byref(key))
+            e.order_key = key.value  # evaluation-order position (sharded callers pick the first)
+            raise e
         result = []
         for o, t in enumerate(out_types):
             oc = outs[o]

@@ -24,8 +24,10 @@ from typing import Callable, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from .. import _abi
 from ..arrow import Array, RecordBatch
 from ..logicalplan import DataType
+from .error import ExecutionError
 
 
 def shard_range(total_rows: int, rank: int, world: int):
@@ -85,21 +87,71 @@ class ShardedFilterProject:
         self.run_shard = run_shard
 
     def __call__(self, local_batch: RecordBatch) -> ShardResult:
-        cols = self.run_shard(self.predicate, self.projections, local_batch, self.flags)
+        try:
+            cols = self.run_shard(self.predicate, self.projections, local_batch, self.flags)
+        except ExecutionError as e:
+            # still take part in the exchange: every rank must learn the query failed
+            return self.exchange(None, e)
         return self.exchange(cols)
 
-    def exchange(self, cols: List[Array]) -> ShardResult:
+    def exchange(self, cols: Optional[List[Array]], error: Optional[ExecutionError] = None) -> ShardResult:
+        """The one all_gather: [status, error position, rows, Utf8 bytes per
+        output..., nulls per output...] per rank. When any rank failed, every
+        rank raises the error the reference would raise first over the whole
+        table: the smallest evaluation position, then the lowest rank (= the
+        earliest rows), with that rank's message."""
         world = dist.get_world_size(self.group)
         rank = dist.get_rank(self.group)
-        rows = cols[0].length if cols else 0
-        nout = len(cols)
-        mine = [rows] + [c.data_bytes() if c.data_type == DataType.Utf8 else 0 for c in cols] + \
-               [c.null_count for c in cols]
-        counts = exchange_counts(mine, self.group)
+        nout = len(cols) if cols is not None else max(1, len(self.projections))
+        if error is None:
+            rows = cols[0].length if cols else 0
+            mine = [0, 0, rows] + [c.data_bytes() if c.data_type == DataType.Utf8 else 0 for c in cols] + \
+                   [c.null_count for c in cols]
+        else:
+            pos = (getattr(error, "order_key", None) or ((1 << 64) - 1)) >> 44
+            mine = [error.code or _abi.DFMI_ERR_EXECUTION, pos, 0] + [0] * (2 * nout)
+        # every rank sends the same record length (failed ranks pad)
+        width = 3 + 2 * _MAX_OUT
+        mine = mine[:3] + _pad(mine[3:3 + nout], _MAX_OUT) + _pad(mine[3 + nout:], _MAX_OUT)
+        allc = exchange_counts(mine, self.group)
+        failed = [r for r in range(world) if allc[r][0]]
+        if failed:
+            first = min(failed, key=lambda r: (allc[r][1], r))
+            msg = error.message if error is not None else ""
+            msgs = _exchange_messages(msg, self.group)
+            raise ExecutionError.from_status(int(allc[first][0]), msgs[first])
+        counts = [[c[2]] + c[3:3 + nout] + c[3 + _MAX_OUT:3 + _MAX_OUT + nout] for c in allc]
         row_offset = sum(counts[r][0] for r in range(rank))
         total = sum(c[0] for c in counts)
         utf8_base = [sum(counts[r][1 + o] for r in range(rank)) for o in range(nout)]
+        assert width == len(mine)
         return ShardResult(cols, rank, world, row_offset, total, counts, utf8_base)
+
+
+_MAX_OUT = 16
+_MSG = 512
+
+
+def _pad(xs, n):
+    xs = list(xs)[:n]
+    return xs + [0] * (n - len(xs))
+
+
+def _exchange_messages(msg: str, group=None) -> List[str]:
+    """Every rank's (error) message, fixed-size all_gather."""
+    world = dist.get_world_size(group)
+    dev = _exchange_device(group)
+    b = msg.encode("utf-8")[:_MSG - 1]
+    t = torch.zeros(_MSG, dtype=torch.uint8, device=dev)
+    if b:
+        t[:len(b)] = torch.tensor(list(b), dtype=torch.uint8, device=dev)
+    allm = torch.empty(world * _MSG, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(allm, t, group=group)
+    out = []
+    for r in range(world):
+        raw = bytes(allm[r * _MSG:(r + 1) * _MSG].cpu().tolist())
+        out.append(raw.split(b"\0", 1)[0].decode("utf-8", errors="replace"))
+    return out
 
 
 def _values_nbytes(t: DataType, rows: int, utf8_bytes: int) -> int:
@@ -158,10 +210,21 @@ def gather_to_root(res: ShardResult, types: Sequence[DataType], root: int = 0, g
             return a.validity[:nb]
         return _bool_to_bits(torch.ones(a.length, dtype=torch.bool, device=a.values.device))[:nb]
 
+    for o, t in enumerate(types):  # i32 offsets address < 2^31 bytes (arrow BinaryArray)
+        if t == DataType.Utf8 and sum(bytes_of[o]) >= (1 << 31):
+            raise ExecutionError("Capacity", "gathered Utf8 column exceeds 2^31 bytes")
+
+    # every transfer posted at once (batch_isend_irecv): under RCCL the root
+    # receives from all ranks concurrently, over all of its xGMI links
+    ops, keep = [], []
     if rank != root:
         for kind, o, nb in buffers(res.columns, rank):
             if nb:
-                dist.send(local(kind, o, nb).contiguous().to(dev), dst=root, group=group)
+                t = local(kind, o, nb).contiguous().to(dev)
+                keep.append(t)
+                ops.append(dist.P2POp(dist.isend, t, root, group))
+        for req in (dist.batch_isend_irecv(ops) if ops else []):
+            req.wait()
         return None
 
     parts = {}
@@ -172,8 +235,10 @@ def gather_to_root(res: ShardResult, types: Sequence[DataType], root: int = 0, g
             else:
                 buf = torch.empty(nb, dtype=torch.uint8, device=dev)
                 if nb:
-                    dist.recv(buf, src=r, group=group)
+                    ops.append(dist.P2POp(dist.irecv, buf, r, group))
             parts[(kind, o, r)] = buf
+    for req in (dist.batch_isend_irecv(ops) if ops else []):
+        req.wait()
 
     total = sum(rows_of)
     out = []

@@ -272,6 +272,13 @@ int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main
  * the programs and the batch's column types / nullability). */
 int32_t dfmi_last_compile_ms(const dfmi_context* ctx, double* compile_ms);
 
+/* Evaluation-order key of the error the last dfmi_filter_project on ctx
+ * returned: (position of the failing operator in the reference's evaluation
+ * order) << 44 | row << 4; all ones when it returned no such error. Lets a
+ * sharded caller report the error the reference would raise first over the
+ * whole table (smallest key position, then the earliest shard). */
+int32_t dfmi_last_error_order(const dfmi_context* ctx, uint64_t* key);
+
 /* ---------------------------------------------------------------------------
  * Aggregate extension (DFMI_FLAG_EXT_AGGREGATE). The reference plans
  * `SELECT SUM(e), ... FROM t [WHERE p]` as Aggregate(Selection?(TableScan))

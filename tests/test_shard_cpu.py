@@ -136,3 +136,59 @@ def test_sharded_projection_with_nulls_matches_oracle():
     ((_, r),) = oracle_filter_project(SCHEMA, batch, None, DENSE)
     assert out[0][5] == [r.to_pylist()]
     assert out[0][6] == [r.null_count]
+
+
+def _fail_worker(rank, world, port, plan, q):
+    """plan[rank] = None (healthy) or (status code, message, evaluation position)."""
+    try:
+        import torch.distributed as dist
+
+        from datafusion_amd.execution.error import ExecutionError
+        from datafusion_amd.execution.shard import ShardedFilterProject
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = shard_range(N, rank, world)
+        batch, raw = table(lo, hi)
+
+        def run(p, e, bt, f):
+            if plan[rank] is None:
+                return numpy_pass(raw, False)
+            code, msg, pos = plan[rank]
+            err = ExecutionError.from_status(code, msg)
+            err.order_key = (pos << 44) | (5 << 4)
+            raise err
+
+        try:
+            ShardedFilterProject(PRED, PROJS, run_shard=run)(batch)
+            q.put((rank, None, None))
+        except ExecutionError as e:
+            q.put((rank, e.kind, e.message))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put(("error", traceback.format_exc(), str(e)))
+
+
+@pytest.mark.parametrize("plan,want", [
+    # only rank 1 fails: every rank raises its error (none blocks in the exchange)
+    ([None, (5, "DivideByZero", 3), None], ("ArrowError(DivideByZero)", "DivideByZero")),
+    # rank 0 fails at a later operator than rank 2: the earlier operator wins
+    ([(7, "attempt to divide with overflow", 9), None, (5, "DivideByZero", 4)],
+     ("ArrowError(DivideByZero)", "DivideByZero")),
+    # same operator on two ranks: the earlier rows (lower rank) win
+    ([None, (7, "attempt to divide with overflow", 4), (5, "DivideByZero", 4)],
+     ("panic", "attempt to divide with overflow")),
+])
+def test_failing_shard_raises_the_first_error_everywhere(plan, want):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, 3, port, plan, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(3)]
+    for p in procs:
+        p.join(60)
+    errs = [o for o in out if o[0] == "error"]
+    assert not errs, errs[0][1]
+    assert all((o[1], o[2]) == want for o in out), out
