@@ -289,11 +289,13 @@ struct Gen {
                   << ">()) dfmi::report_err(A.err, " << ord << ", row, dfmi::ERRK_DIV_OVERFLOW);\n";
             o << "    }\n";
             if (f)
-                o << "    " << ct << " " << v << " = (" << a.v << ") / (" << b.v << ");\n";
+                o << "    " << ct << " " << v << " = dfmi::sse_nan<" << ct << ">((" << a.v << ") / (" << b.v << "), "
+                  << a.v << ", " << b.v << ");\n";
             else
                 o << "    " << ct << " " << v << " = dfmi::idiv<" << ct << ">(" << a.v << ", " << b.v << ");\n";
         } else if (f) {
-            o << "    " << ct << " " << v << " = (" << a.v << ") " << math_sym(op) << " (" << b.v << ");\n";
+            o << "    " << ct << " " << v << " = dfmi::sse_nan<" << ct << ">((" << a.v << ") " << math_sym(op) << " ("
+              << b.v << "), " << a.v << ", " << b.v << ");\n";
         } else {
             const char* mt = math_type(ty);
             o << "    " << ct << " " << v << " = (" << ct << ")((" << mt << ")(" << a.v << ") " << math_sym(op) << " ("

@@ -190,6 +190,24 @@ __device__ __noinline__ T idiv(T x, T y) {
     return (T)(x / y);
 }
 
+// NaN results of a Float32 / Float64 operator as the reference's scalar
+// loops produce them on x86-64 (SSE2, left operand first): a NaN operand
+// propagates quieted, the left one first; an invalid operation on non-NaN
+// operands gives x86's negative default NaN. gfx950 would otherwise return
+// its own canonical NaN.
+template <typename T>
+__device__ __forceinline__ T sse_nan(T r, T a, T b) {
+    if (r == r) return r;
+    if constexpr (sizeof(T) == 8) {
+        const u64 x = a != a ? (bits(a) | (1ull << 51)) : (b != b ? (bits(b) | (1ull << 51)) : 0xFFF8000000000000ull);
+        return f64(x);
+    } else {
+        const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+        const unsigned x = a != a ? (ua | (1u << 22)) : (b != b ? (ub | (1u << 22)) : 0xFFC00000u);
+        return __builtin_bit_cast(float, x);
+    }
+}
+
 // iN::MIN as a value of T (signed T only).
 template <typename T>
 __device__ __forceinline__ constexpr T int_min() {
@@ -233,6 +251,18 @@ __device__ __forceinline__ bool num_cast(From x, To& out) {
             if (__builtin_isfinite(d) && (d < -0x1.fffffep127 || d > 0x1.fffffep127)) {
                 out = (To)0;
                 return false;
+            }
+            if (d != d) {  // x86 cvtsd2ss: quieted, the fraction's top 22 bits kept
+                const u64 b = bits(d);
+                out = __builtin_bit_cast(float, (unsigned)((b >> 32) & 0x80000000u) | 0x7FC00000u |
+                                                    (unsigned)((b >> 29) & 0x3FFFFFu));
+                return true;
+            }
+        } else if constexpr (sizeof(From) < sizeof(To)) {
+            if (x != x) {  // x86 cvtss2sd: quieted, the fraction widened
+                const unsigned b = __builtin_bit_cast(unsigned, (float)x);
+                out = f64(((u64)(b & 0x80000000u) << 32) | 0x7FF8000000000000ull | ((u64)(b & 0x3FFFFFu) << 29));
+                return true;
             }
         }
         out = (To)x;

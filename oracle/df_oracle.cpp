@@ -416,6 +416,31 @@ template <typename T> T wrap_mul(T a, T b) {
 // arrow 0.12 math_op: null if either side is null (value slot 0), else op.
 // divide: a non-null zero divisor (0, -0.0) is ArrowError::DivideByZero; the
 // Rust `/` on iN::MIN / -1 panics ("attempt to divide with overflow").
+// NaN results as the reference's scalar loops produce them on x86-64 (SSE2
+// addsd/subsd/mulsd/divsd with the left operand as the destination): a NaN
+// operand propagates quieted, the left one first; an invalid operation on
+// non-NaN operands (inf - inf, 0 * inf, ...) gives the default NaN, which on
+// x86 is negative (0xFFF8000000000000 / 0xFFC00000). Written out so that
+// the result does not depend on which operand order the compiler emits.
+template <typename T>
+T sse_nan(T r, T a, T b) {
+    if (!std::isnan(r)) return r;
+    if constexpr (sizeof(T) == 8) {
+        uint64_t x;
+        if (std::isnan(a)) memcpy(&x, &a, 8), x |= 1ull << 51;
+        else if (std::isnan(b)) memcpy(&x, &b, 8), x |= 1ull << 51;
+        else x = 0xFFF8000000000000ull;
+        memcpy(&r, &x, 8);
+    } else {
+        uint32_t x;
+        if (std::isnan(a)) memcpy(&x, &a, 4), x |= 1u << 22;
+        else if (std::isnan(b)) memcpy(&x, &b, 4), x |= 1u << 22;
+        else x = 0xFFC00000u;
+        memcpy(&r, &x, 4);
+    }
+    return r;
+}
+
 template <typename T>
 ArrayRef math(int op, int type, const Array& l, const Array& r) {
     if (l.len != r.len)
@@ -440,6 +465,7 @@ ArrayRef math(int op, int type, const Array& l, const Array& r) {
                 }
                 v = x / y;
         }
+        if constexpr (std::is_floating_point<T>::value) v = sse_nan(v, x, y);
         b.push(v);
     }
     return b.finish(type);

@@ -257,3 +257,26 @@ def test_compile_names_and_errors():
     assert err(BinaryExpr(Column(0), Operator.Modulus, Column(1))) == ("ExecutionError", "operator: Modulus")
     assert err(IsNull(Column(0))) == ("ExecutionError", "expression #0 IS NULL")
     assert err(Column(9))[0] == "panic"
+
+
+def test_oracle_x86_nan_rules():
+    """The oracle's NaN results follow x86 SSE: a NaN operand
+    propagates quieted, the left one first; invalid operations give the
+    negative default NaN."""
+    import numpy as np
+    from datafusion_amd.arrow import Array, Field, RecordBatch, Schema
+    from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Operator
+    from oracle_ffi import oracle_filter_project
+    q1 = np.array([0x7FF8000000000001], dtype=np.uint64).view(np.float64)[0]
+    s1 = np.array([0xFFF0000000000002], dtype=np.uint64).view(np.float64)[0]  # signalling, negative
+    a = np.array([q1, 1.0, s1, np.inf, 0.0, q1])
+    b = np.array([s1, s1, 2.0, np.inf, np.inf, 3.0])
+    s = Schema([Field("a", DataType.Float64, False), Field("b", DataType.Float64, False)])
+    bt = RecordBatch(s, [Array.from_numpy(DataType.Float64, a), Array.from_numpy(DataType.Float64, b)])
+    (_, add), (_, sub), (_, mul) = oracle_filter_project(
+        s, bt, None, [BinaryExpr(Column(0), op, Column(1)) for op in (Operator.Plus, Operator.Minus, Operator.Multiply)])
+    bits = lambda arr: [hex(int(x)) for x in arr.numpy_values().view(np.uint64)]
+    assert bits(add)[:3] == ["0x7ff8000000000001", "0xfff8000000000002", "0xfff8000000000002"]
+    assert bits(sub)[3] == "0xfff8000000000000"   # inf - inf
+    assert bits(mul)[4] == "0xfff8000000000000"   # 0 * inf
+    assert bits(add)[5] == "0x7ff8000000000001"
