@@ -78,7 +78,7 @@ class FusedStep:
         return self.outs[0].length
 
 
-PROFILE_TAG = "profiles/r01"
+PROFILE_TAG = "profiles/r02"
 PROFILE_DIR = os.path.join(ROOT, PROFILE_TAG)
 
 
@@ -485,45 +485,74 @@ HOST_ROWS = 100_000_000
 
 def host_line(eng, steps, warmup):
     """PCIe-inclusive rate: the C2 query at s=0.5 over a HOST
-    batch through dfmi_filter_project_host (pinned staging H2D, kernel, D2H of
-    the selected rows into library-owned host buffers). Never `value`."""
-    from datafusion_amd.arrow import Array, RecordBatch
-    from datafusion_amd.execution.engine import column_struct
+    batch through dfmi_filter_project_host (row chunks pipelined: host staging,
+    H2D, kernel and D2H of consecutive chunks overlap; the selected rows land
+    in library-owned host buffers). Two variants: pageable input buffers
+    (staged through pinned memory by host threads) and input buffers in pinned
+    memory from dfmi_host_alloc (DMA'd straight from the caller's buffers, as
+    a reader parsing into them would hand over). Never `value`."""
+    import numpy as np
     from oracle_ffi import gen_unit_f64
     n = HOST_ROWS
     schema = Schema([Field(c, DataType.Float64, False) for c in "abc"])
-    b = RecordBatch(schema, [Array.from_numpy(DataType.Float64, gen_unit_f64(SEED, j, 0, n)) for j in range(3)])
+    host_cols = [gen_unit_f64(SEED, j, 0, n) for j in range(3)]
     pred_e, proj_e = query(0.5)
     pred = compile_scalar_expr(None, pred_e, schema)
     projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
-    carr = (_abi.dfmi_column * 3)(*[column_struct(a) for a in b.columns])
-    cb = _abi.dfmi_batch(3, 0, n, carr)
     progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
     L = _abi.lib()
     err = _abi.dfmi_error()
 
-    def step():
-        res = C.c_void_p()
-        rc = L.dfmi_filter_project_host(eng.ctx, pred.handle, progs, 3, C.byref(cb), 0, C.byref(res), C.byref(err))
-        if rc != 0:
-            raise RuntimeError(err.message.decode())
-        v = _abi.dfmi_column()
-        L.dfmi_host_result_column(res, 0, C.byref(v))
-        sel = v.length
-        L.dfmi_host_result_free(res)
-        return sel
+    def batch_of(ptrs):
+        carr = (_abi.dfmi_column * 3)()
+        for i, p in enumerate(ptrs):
+            carr[i].type = int(DataType.Float64)
+            carr[i].length = n
+            carr[i].values = p
+        return _abi.dfmi_batch(3, 0, n, carr), carr
 
-    for _ in range(warmup):
-        step()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        sel = step()
-    el = (time.perf_counter() - t0) / steps
-    moved = n * 24 + sel * 24
+    def run(cb):
+        def step():
+            res = C.c_void_p()
+            rc = L.dfmi_filter_project_host(eng.ctx, pred.handle, progs, 3, C.byref(cb), 0, C.byref(res),
+                                            C.byref(err))
+            if rc != 0:
+                raise RuntimeError(err.message.decode())
+            v = _abi.dfmi_column()
+            L.dfmi_host_result_column(res, 2, C.byref(v))
+            sel = v.length
+            chk = float(np.ctypeslib.as_array(C.cast(v.values, C.POINTER(C.c_double)), shape=(sel,))[::4099].sum())
+            L.dfmi_host_result_free(res)
+            return sel, chk
+        for _ in range(warmup):
+            step()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sel, chk = step()
+        el = (time.perf_counter() - t0) / steps
+        moved = n * 24 + sel * 24
+        return {"rows_per_s": n / el, "ms_per_step": el * 1e3, "selected": sel, "pcie_gbs": round(moved / el / 1e9, 1),
+                "bytes_moved_per_step": moved, "checksum": chk}
+
+    cb, keep = batch_of([c.ctypes.data for c in host_cols])
+    pageable = run(cb)
+    pinned_ptrs = []
+    try:
+        for c in host_cols:
+            p = C.c_void_p()
+            if L.dfmi_host_alloc(c.nbytes, C.byref(p), C.byref(err)) != 0:
+                raise RuntimeError(err.message.decode())
+            pinned_ptrs.append(p.value)
+            C.memmove(p.value, c.ctypes.data, c.nbytes)
+        cb2, keep2 = batch_of(pinned_ptrs)
+        pinned = run(cb2)
+    finally:
+        for p in pinned_ptrs:
+            L.dfmi_host_free(p)
+    assert (pinned["selected"], pinned["checksum"]) == (pageable["selected"], pageable["checksum"])
     return {"workload": "C2 query, s=0.5, %d-row HOST batch (dfmi_filter_project_host)" % n,
-            "rows_per_s": n / el, "ms_per_step": el * 1e3, "selected": sel,
-            "pcie_gbs": round(moved / el / 1e9, 1), "bytes_moved_per_step": moved,
-            "note": "host->HBM staging + kernel + HBM->host of the selected rows; not the headline value"}
+            **pageable, "pinned_input": pinned,
+            "note": "host->HBM + kernel + HBM->host of the selected rows, chunks pipelined; not the headline value"}
 
 
 def main():

@@ -139,6 +139,10 @@ EXPORTED = [
     "dfmi_host_result_num_columns",
     "dfmi_host_result_column",
     "dfmi_host_result_free",
+    "dfmi_host_alloc",
+    "dfmi_host_free",
+    "dfmi_host_register",
+    "dfmi_host_unregister",
     "dfmi_last_timing",
     "dfmi_last_compile_ms",
     "dfmi_last_error_order",
@@ -245,6 +249,14 @@ def lib() -> C.CDLL:
     L.dfmi_host_result_column.restype = C.c_int32
     L.dfmi_host_result_free.argtypes = [C.c_void_p]
     L.dfmi_host_result_free.restype = None
+    L.dfmi_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(dfmi_error)]
+    L.dfmi_host_alloc.restype = C.c_int32
+    L.dfmi_host_free.argtypes = [C.c_void_p]
+    L.dfmi_host_free.restype = C.c_int32
+    L.dfmi_host_register.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(dfmi_error)]
+    L.dfmi_host_register.restype = C.c_int32
+    L.dfmi_host_unregister.argtypes = [C.c_void_p]
+    L.dfmi_host_unregister.restype = C.c_int32
     L.dfmi_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.dfmi_last_timing.restype = C.c_int32
     L.dfmi_last_compile_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]

@@ -258,6 +258,7 @@ namespace dfmi {
 int ctx_device(const dfmi_context* c) { return c->device; }
 hipStream_t ctx_stream(const dfmi_context* c) { return c->stream; }
 void*& ctx_host_arena(dfmi_context* c) { return c->host_arena; }
+uint64_t& ctx_last_err_key(dfmi_context* c) { return c->last_err_key; }
 void host_arena_release(dfmi_context* c);
 }  // namespace dfmi
 

@@ -246,10 +246,14 @@ int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* predicate,
  * reference's arrow 0.12 buffers from csv::Reader, csv_sql.rs:49): the same
  * pull as dfmi_filter_project -- FilterRelation::next (filter.rs:46-72) +
  * filter() (filter.rs:80-111) + ProjectRelation::next (projection.rs:45-66)
- * -- but `input` holds HOST pointers. The library moves the buffers into HBM
- * (pinned staging), runs the fused pass, and copies the exact-size results
- * into host buffers it owns until dfmi_host_result_free. Passthrough columns
- * (Arc clones, expression.rs:272-276) are returned as copies.
+ * -- but `input` holds HOST pointers. Rows are independent, so the library
+ * cuts the batch into row chunks (~48 MiB of input each) and pipelines them:
+ * host staging copies, H2D DMA, the fused pass and D2H DMA of consecutive
+ * chunks overlap; chunk results are concatenated in row order into host
+ * buffers the library owns until dfmi_host_result_free. The result and any
+ * error are those of one pull over the whole batch (the first error in the
+ * reference's evaluation order over all rows). Passthrough columns (Arc
+ * clones, expression.rs:272-276) are returned as copies.
  * ------------------------------------------------------------------------- */
 typedef struct dfmi_host_result dfmi_host_result;
 
@@ -262,6 +266,17 @@ int32_t dfmi_host_result_num_columns(const dfmi_host_result* result);
  * `validity` is NULL when null_count == 0 (filtered outputs never have one). */
 int32_t dfmi_host_result_column(const dfmi_host_result* result, int32_t i, dfmi_column* view);
 void dfmi_host_result_free(dfmi_host_result* result);
+
+/* Pinned host memory for batch buffers (e.g. a CSV reader parsing straight
+ * into them; csv_sql.rs:49's DataSource side). Columns whose buffers lie in
+ * such memory -- or in any hipHostMalloc'd allocation of at least 1 MiB --
+ * are DMA'd by dfmi_filter_project_host straight from the caller's memory
+ * instead of through the library's pinned staging. dfmi_host_register pins
+ * an existing range (hipHostRegister) until dfmi_host_unregister. */
+int32_t dfmi_host_alloc(size_t bytes, void** out, dfmi_error* err);
+int32_t dfmi_host_free(void* ptr);
+int32_t dfmi_host_register(void* ptr, size_t bytes, dfmi_error* err);
+int32_t dfmi_host_unregister(void* ptr);
 
 /* Device time in milliseconds of the last dfmi_filter_project's kernels
  * (HIP events on the context stream), and the dominant kernel's share. */

@@ -3,6 +3,8 @@ same inputs. Bit-exact for masks, integers, Utf8 and comparisons; Float64 and
 Float32 bit-exact too (one rounding per operator on both sides,
 -ffp-contract=off), NaN payloads included: both sides follow the x86 NaN
 rules the reference's scalar loops produce (DESIGN.md "Semantics")."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,8 @@ from golden_cases import CITIES, GOLDEN, NUMERICS, all_types_schema, expected_ro
 from oracle_ffi import gen_i64, gen_unit_f64, oracle_filter_project
 
 pytestmark = pytest.mark.gpu
+
+HOST_CHUNK = 512  # rows per pipelined chunk in run_both's second host-path call
 
 CMP = [Operator.Eq, Operator.NotEq, Operator.Lt, Operator.LtEq, Operator.Gt, Operator.GtEq]
 MATH = [Operator.Plus, Operator.Minus, Operator.Multiply, Operator.Divide]
@@ -67,6 +71,28 @@ def run_both(schema, batch, pred, projs, flags=0):
             host = engine().filter_project_host(p, cp, batch, flags)
         except ExecutionError as e:
             host_err = e
+        if batch.num_rows() > HOST_CHUNK:
+            # ... and again cut into HOST_CHUNK-row pipelined chunks: the same
+            # result or the same first error (evaluation order over all rows)
+            prev = os.environ.get("DFMI_HOST_CHUNK_ROWS")
+            os.environ["DFMI_HOST_CHUNK_ROWS"] = str(HOST_CHUNK)
+            try:
+                try:
+                    chunked = engine().filter_project_host(p, cp, batch, flags)
+                    cerr = None
+                except ExecutionError as e:
+                    chunked, cerr = None, e
+            finally:
+                if prev is None:
+                    del os.environ["DFMI_HOST_CHUNK_ROWS"]
+                else:
+                    os.environ["DFMI_HOST_CHUNK_ROWS"] = prev
+            if host_err is not None:
+                assert cerr is not None and (cerr.kind, cerr.message) == (host_err.kind, host_err.message), cerr
+            else:
+                assert cerr is None, cerr
+                for h, c in zip(host, chunked):
+                    assert_same(c, h, "chunked host path")
         dev = engine().filter_project(p, cp, batch, flags)
     except ExecutionError as e:
         dev_err = e
@@ -369,6 +395,53 @@ def test_host_batch_many_staging_chunks():
         assert np.array_equal(h.numpy_values().view(np.uint64), d.numpy_values().view(np.uint64))
 
 
+def test_host_batch_pinned_inputs_and_chunk_errors():
+    """dfmi_filter_project_host with input buffers in pinned memory (DMA'd
+    straight from them, no staging) equals the pageable-input call; and over
+    many pipelined chunks the error is the one of the whole batch in the
+    reference's evaluation order: a divide-by-zero whose operator comes first
+    in the predicate wins over an earlier-row one that comes later, wherever
+    the chunk boundaries fall."""
+    n = 3_000_000
+    s, b = synth(n, seed=5, nullable=True)
+    pinned = RecordBatch(s, [Array(a.data_type, a.length, a.values.pin_memory(),
+                                   a.validity.pin_memory() if a.validity is not None else None, None, a.null_count)
+                             for a in b.columns])
+    assert pinned.columns[0].values.is_pinned()
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.3))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.8))))
+    projs = [Column(0), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus, Column(2))]
+    p = compile_scalar_expr(None, pred, s)
+    cp = [compile_scalar_expr(None, e, s) for e in projs]
+    base = engine().filter_project_host(p, cp, b)
+    for chunk in (None, "65536"):
+        if chunk:
+            os.environ["DFMI_HOST_CHUNK_ROWS"] = chunk
+        try:
+            got = engine().filter_project_host(p, cp, pinned)
+        finally:
+            os.environ.pop("DFMI_HOST_CHUNK_ROWS", None)
+        for g, r in zip(got, base):
+            assert_same(g, r, "pinned inputs, chunk %s" % chunk)
+    # zero divisors: column b at row 2_900_000 (late chunk), column c at row 10
+    n2 = 1_000_000
+    sch = Schema([Field(c, DataType.Float64, False) for c in "abc"])
+    vals = [gen_unit_f64(9, j, 0, n2) + 0.5 for j in range(3)]
+    vals[1][900_000] = 0.0
+    vals[2][10] = -0.0
+    bb = RecordBatch(sch, [Array.from_numpy(DataType.Float64, v) for v in vals])
+    first = BinaryExpr(BinaryExpr(Column(0), Operator.Divide, Column(1)), Operator.Gt, Literal(Float64(0.1)))
+    second = BinaryExpr(BinaryExpr(Column(0), Operator.Divide, Column(2)), Operator.Gt, Literal(Float64(0.1)))
+    for chunk in ("4096", "65536", None):
+        if chunk:
+            os.environ["DFMI_HOST_CHUNK_ROWS"] = chunk
+        try:
+            assert run_both(sch, bb, BinaryExpr(first, Operator.And, second), [Column(0)]) is None
+            assert run_both(sch, bb, BinaryExpr(second, Operator.And, first), [Column(0)]) is None
+        finally:
+            os.environ.pop("DFMI_HOST_CHUNK_ROWS", None)
+
+
 def test_static_errors_match():
     s, batch = synth(1000)
     cases = [
@@ -412,6 +485,18 @@ def test_q6_style_predicate():
     out = rel.next().columns[0].cpu().numpy_values()
     m = (ship >= 8766) & (ship < 9131) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24)
     assert np.array_equal(out, (price * disc)[m])
+
+
+def test_c4_bench_generator_against_oracle():
+    """C4 (Q6-style projection) over 1,048,577 rows of the bench's own
+    generator (bench.q6_table), device and host paths against the oracle."""
+    import bench
+    n = (1 << 20) + 1
+    s, dcols = bench.q6_table(engine().device, n, 42)
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, c.cpu().numpy()) for c in dcols])
+    pred, projs = bench.q6_query()
+    dev, ref = run_both(s, b, pred, projs)
+    assert 0.01 < ref[0][1].length / n < 0.03
 
 
 def _nan_cols(n, rng, dt):
