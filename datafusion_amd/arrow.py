@@ -60,7 +60,8 @@ class Field:
 
     def __init__(self, name: str, data_type: DataType, nullable: bool = True):
         self.name = name
-        self.data_type = DataType(data_type)
+        # nested types (serde.StructType / ListType) appear only in serialized schemas
+        self.data_type = DataType(data_type) if isinstance(data_type, int) else data_type
         self.nullable = nullable
 
     def __repr__(self):

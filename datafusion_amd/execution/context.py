@@ -16,9 +16,13 @@ from .relation import DataSourceRelation, Relation
 
 
 class TableScan:
-    def __init__(self, table_name: str, schema: Schema):
+    """LogicalPlan::TableScan { schema_name, table_name, schema, projection } (logicalplan.rs:337-343)."""
+
+    def __init__(self, table_name: str, schema: Schema, schema_name: str = "", projection=None):
         self.table_name = table_name
         self.schema = schema
+        self.schema_name = schema_name
+        self.projection = projection
 
 
 class Selection:
