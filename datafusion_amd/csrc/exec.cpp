@@ -212,8 +212,12 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
     if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;  // diagnostics only
-    if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) & 1;  // diagnostics only
+    if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 3;  // diagnostics only (2 = serial)
     if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;  // diagnostics only
+    // a numeric predicate's tiles are VGPR-limited (3 blocks/CU): LDS has room
+    // for a 4 KiB staging arena per wave, which stages ~4 slices per round trip
+    if (!X.utf8_outs.empty() && !X.pred_slots.empty()) X.arena = 256;
+    if (const char* e = getenv("DFMI_UTF8_ARENA")) X.arena = std::max(128, std::min(1024, atoi(e)));  // diagnostics only
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 256)
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;

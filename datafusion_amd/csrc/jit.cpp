@@ -614,6 +614,7 @@ std::string generate(const Plan& P, Launch& X) {
                 if (P.outs[oi].nullable)
                     o << "  { const u64 s_ = dfmi::wave_sum((u64)nn" << oi << "); if (lane == 0 && s_) atomicAdd(&A.totals[8 + "
                       << oi << "], s_); }\n";
+            if (!X.utf8_outs.empty()) o << "  if (!(A.mode & 8)) {  // mode bit 3: skip the byte copies (diagnostics)\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
                 const int u = X.utf8_outs[j].second;
                 if (X.gather == 0)
@@ -621,10 +622,12 @@ std::string generate(const Plan& P, Launch& X) {
                       << X.utf8_outs[j].first << ", selm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
                       << ", lane, wave);\n";
                 else
-                    o << "  dfmi::utf8_gather<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << u << ", "
+                    o << "  dfmi::utf8_gather" << (X.gather == 2 ? "_serial" : "") << "<BLOCK, K, NCH, ARENA>(A, " << T
+                      << ", " << (j + 1) << ", " << u << ", "
                       << X.utf8_outs[j].first << ", selm, wm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
                       << ", G[wave], lane, wave);\n";
             }
+            if (!X.utf8_outs.empty()) o << "  }\n";
             if (!X.utf8_outs.empty()) {
                 o << "  if (tid == 0 && t == (unsigned)A.n_tiles - 1) {\n";
                 for (size_t j = 0; j < X.utf8_outs.size(); ++j)
@@ -640,7 +643,8 @@ std::string generate(const Plan& P, Launch& X) {
             // one tile per block in dispatch order (in order per XCD, so every
             // tile a block waits on in the look-back is running or done)
             o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
-            if (!X.utf8_outs.empty() && X.gather) o << "  __shared__ dfmi::Utf8Stage G[WAVES];\n";
+            if (!X.utf8_outs.empty() && X.gather)
+                o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA> G[WAVES];\n";
             o << "  const unsigned t = blockIdx.x;\n";
             emit_decls(o, X.pred_slots, X, "", true);
             emit_decls(o, X.proj_slots, X, "", false);
@@ -727,7 +731,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, os.out_type);
         put(k, (char)os.nullable);
     }
-    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather, X.late_proj};
+    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather, X.late_proj, X.arena};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -678,12 +678,27 @@ __device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK
     }
 }
 
-// LDS staging of one wave's Utf8 gather (per 64-row slice).
-constexpr int kStageChunks = 128;  // 16-byte source chunks: 2 KiB per wave
+// LDS staging of one wave's Utf8 gather.
+constexpr int kStageChunks = 128;  // 16-byte source chunks of one slice's span: 2 KiB (longer: per-lane copy)
+template <int ARENA = kStageChunks>
 struct Utf8Stage {
-    uint4 src[kStageChunks];      // the slice's source span, whole aligned 16-byte chunks
-    uint4 dst[kStageChunks + 1];  // its output bytes, at their output address modulo 4
+    static_assert(ARENA >= kStageChunks, "the arena holds at least one slice's span");
+    uint4 src[ARENA];              // source spans of consecutive slices, whole aligned 16-byte chunks
+    uint4 dst[kStageChunks + 1];   // one slice's output bytes, at their output address modulo 4
 };
+
+typedef __attribute__((address_space(1))) void dfmi_gvoid;
+typedef __attribute__((address_space(3))) void dfmi_lvoid;
+
+// Chunks [0, n) of the 16-byte-chunk span at global `sp` into LDS at `dst`
+// (wave-uniform) with direct global->LDS loads (global_load_lds_dwordx4:
+// lane l of an instruction writes dst + 16 l; no VGPRs). Completion:
+// wait_vm_loads().
+__device__ __forceinline__ void stage_span(const uint4* sp, uint4* dst, int n, int lane) {
+    for (int c = 0; c < n; c += 64)
+        if (c + lane < n) __builtin_amdgcn_global_load_lds((dfmi_gvoid*)(sp + c + lane), (dfmi_lvoid*)(dst + c), 16, 0, 0);
+}
+__device__ __forceinline__ void wait_vm_loads() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Orders this wave's LDS accesses (a wave's LDS operations execute in
 // order; this keeps the compiler from moving them across).
@@ -707,12 +722,14 @@ __device__ __forceinline__ unsigned byte_mask(int lo, int hi) {
 // there); the wave then stores the image as coalesced aligned words --
 // bytewise only the two edge words the slice shares with its neighbours. A
 // span over 2 KiB (long strings) falls back to a per-lane copy. Source reads
-// are whole aligned 16-byte chunks holding span bytes.
-template <int BLOCK, int K, int NCH>
-__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
-                                            unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
-                                            const int (&s)[K], const int (&nx)[K], Utf8Stage& G, int lane,
-                                            int wave) {
+// are whole aligned 16-byte chunks holding span bytes. One global round trip
+// per slice (diagnostic variant DFMI_UTF8_GATHER=2; utf8_gather below stages
+// consecutive slices together).
+template <int BLOCK, int K, int NCH, int ARENA>
+__device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+                                                   unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
+                                                   const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA>& G,
+                                                   int lane, int wave) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -768,6 +785,152 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
                 __hip_atomic_fetch_or(gd + w, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
         }
+        wave_lds_fence();
+        for (int j = lane; j < nw; j += 64) {
+            const unsigned val = gd[j];
+            const int p = 4 * j - sh;  // output position of the word's first byte
+            if (p >= 0 && p + 4 <= (int)Ls) {
+                *at<unsigned>(w0, 4 * j) = val;
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (p + b >= 0 && p + b < (int)Ls) w0[4 * j + b] = (u8)(val >> (8 * b));
+            }
+        }
+        wave_lds_fence();
+    }
+}
+
+// One string into the zeroed LDS output image gd: source bytes [a, a + L)
+// of the staged span sg, output bytes [d, d + L) of gd (L > 0). Words
+// inside the string are this string's alone and are written whole (one
+// v_alignbyte of two aligned source words, two words per iteration); only
+// its first and last word, which it may share with the neighbouring
+// strings, are OR-merged masked. (Storing the inside words straight to
+// global memory instead of through the image measured slower: 1.32 -> 1.34
+// ms per C3 batch)
+__device__ __forceinline__ void utf8_place(const unsigned* sg, unsigned* gd, int a, int d, int L) {
+    const int delta = a - d;  // source byte = output byte + delta
+    const int wf = d >> 2, wl = (d + L - 1) >> 2;
+    auto edge = [&](int w) {
+        const int p = 4 * w - d;  // position of the word's first byte in the string (>= -3)
+        const int sb = a + p;     // ... in the span (>= -3)
+        const int sw = sb >> 2;   // arithmetic shift: -1 at most
+        const unsigned lo = sg[sw < 0 ? 0 : sw], hi = sg[sw + 1];
+        const unsigned val = __builtin_amdgcn_alignbyte(hi, lo, (unsigned)sb & 3u);
+        const unsigned msk = byte_mask(p < 0 ? -p : 0, p + 4 > L ? L - p : 4);
+        __hip_atomic_fetch_or(gd + w, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
+    edge(wf);
+    if (wl != wf) edge(wl);
+    int w = wf + 1;
+    for (; w + 1 < wl; w += 2) {
+        const int sb = 4 * w + delta;  // >= 0: an interior word starts inside the string
+        const int sw = sb >> 2;
+        const unsigned sh = (unsigned)sb & 3u;
+        const unsigned x0 = sg[sw], x1 = sg[sw + 1], x2 = sg[sw + 2];
+        gd[w] = __builtin_amdgcn_alignbyte(x1, x0, sh);
+        gd[w + 1] = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    }
+    if (w < wl) {
+        const int sb = 4 * w + delta;
+        const int sw = sb >> 2;
+        gd[w] = __builtin_amdgcn_alignbyte(sg[sw + 1], sg[sw], (unsigned)sb & 3u);
+    }
+}
+
+// The 16-byte-chunk source span of slice k (wave-uniform): chunks from the
+// one holding the first selected string's first byte to the one holding the
+// last one's last byte, as an offset from src and a count (0: no bytes).
+__device__ __forceinline__ void utf8_span(u64 m, int s, int e, i64 sm, i64& c0, int& nch) {
+    const int fl = __builtin_ctzll(m), ll = 63 - __builtin_clzll(m);
+    const i64 s0 = __builtin_amdgcn_readlane(s, fl), s1 = __builtin_amdgcn_readlane(e, ll);
+    c0 = ((s0 + sm) & ~15ll) - sm;  // offset of the 16-byte chunk holding byte s0, from src
+    nch = s1 > s0 ? (int)(((s1 - 1 - c0) >> 4)) + 1 : 0;
+}
+
+// Copy the selected rows of Utf8 input u into output o (rebased i32
+// offsets + bytes, filter.rs:94-105) as utf8_gather_serial does slice by
+// slice -- LDS image of each slice's output, coalesced word stores -- but
+// the source spans of consecutive slices are staged into the ARENA together
+// with direct global->LDS loads, one wait per arena-full: a tile's gather
+// pays about K * (span bytes) / (arena bytes) global round trips instead of K.
+// Only scalar state (where the staged round ends, the next arena offset) is
+// carried between slices.
+template <int BLOCK, int K, int NCH, int ARENA>
+__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+                                            unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
+                                            const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA>& G, int lane,
+                                            int wave) {
+    constexpr int WAVES = BLOCK / 64;
+    const u64 bpre = T.prefix[ch];
+    const i64 obase = (i64)T.prefix[0];
+    const u8* src = A.bytes[u];
+    u8* out = A.out_data[o];
+    const unsigned* gs = (const unsigned*)G.src;
+    unsigned* gd = (unsigned*)G.dst;
+    const i64 sm = (i64)((u64)src & 15u);
+    int staged_to = -1;  // slices <= staged_to are in the arena (or need no staging)
+    int aoff = 0;        // arena chunk of the next staged slice to process
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const u64 m = wm[k];
+        if (!m) continue;
+        if (k > staged_to) {
+            // stage slice k and the following ones while their spans fit
+            int used = 0;
+            bool full = false;
+#pragma unroll
+            for (int j = k; j < K; ++j) {
+                if (full || !wm[j]) continue;
+                i64 cj;
+                int nj;
+                utf8_span(wm[j], s[j], utf8_end(s[j], nx[j], lane), sm, cj, nj);
+                if (nj > kStageChunks) {  // copied per lane when processed
+                    if (j == k) staged_to = j;
+                    else full = true;
+                    continue;
+                }
+                if (used + nj > ARENA) {
+                    full = true;
+                    continue;
+                }
+                stage_span(at<uint4>(src, cj), G.src + used, nj, lane);
+                used += nj;
+                staged_to = j;
+            }
+            wait_vm_loads();
+            wave_lds_fence();
+            aoff = 0;
+        }
+        const bool sel = (selm >> k) & 1;
+        const int e = utf8_end(s[k], nx[k], lane);
+        const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
+        const unsigned incl = wave_incl_scan32(L, lane);
+        const unsigned rel = incl - L;
+        const unsigned Ls = (unsigned)readlane_u(incl, 63);
+        const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
+        if (sel) A.out_offs[o][obase + dst[k]] = (int)(ob0 + rel);
+        i64 c0;
+        int nch;
+        utf8_span(m, s[k], e, sm, c0, nch);
+        const int my_off = aoff;
+        if (nch <= kStageChunks) aoff += nch;
+        if ((i64)(ob0 + Ls) > A.out_cap[o]) {
+            if (lane == 0) report_err(A.err, 0, 0, ERRK_CAPACITY);
+            continue;
+        }
+        if (Ls == 0) continue;
+        if (nch > kStageChunks) {
+            if (sel && L) utf8_copy(src + s[k], out + ob0 + rel, L);
+            continue;
+        }
+        const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
+        u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word holding the slice's first byte
+        const int nw = (sh + (int)Ls + 3) >> 2;
+        for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_fence();
+        if (L) utf8_place(gs + 4 * my_off, gd, (int)(s[k] - c0), sh + (int)rel, (int)L);
         wave_lds_fence();
         for (int j = lane; j < nw; j += 64) {
             const unsigned val = gd[j];

@@ -10,7 +10,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     constexpr int BLOCK = 512, K = 8, WAVES = BLOCK / 64, NCH = 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);
     __shared__ dfmi::Tile<BLOCK, K, NCH> T;
-    __shared__ dfmi::Utf8Stage G[WAVES];
+    __shared__ dfmi::Utf8Stage<> G[WAVES];
     const unsigned tile = blockIdx.x;
     const i64 base = (i64)tile * (BLOCK * K);
     const i64 rem = A.n_rows - base;
@@ -39,7 +39,8 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);
     for (int k = 0; k < K; ++k)
         if ((selm >> k) & 1) ((u64*)A.out[0] + obase)[dst[k]] = c0[k];
-    dfmi::utf8_gather<BLOCK, K, NCH>(A, T, 1, 0, 1, selm, wm, dst, us, ue, G[wave], lane, wave);
+    dfmi::utf8_gather<BLOCK, K, NCH, dfmi::kStageChunks>(A, T, 1, 0, 1, selm, wm, dst, us, ue, G[wave], lane, wave);
+    dfmi::utf8_gather_serial<BLOCK, K, NCH, dfmi::kStageChunks>(A, T, 1, 0, 1, selm, wm, dst, us, ue, G[wave], lane, wave);
     dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, 1, 0, 1, selm, dst, us, ue, lane, wave);
     const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0) &&
                    dfmi::utf8_eq_col(A, 0, 1, base) && dfmi::utf8_valid(A, 0, base);
