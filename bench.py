@@ -555,6 +555,80 @@ def host_line(eng, steps, warmup):
             "note": "host->HBM + kernel + HBM->host of the selected rows, chunks pipelined; not the headline value"}
 
 
+CSV_ROWS = 5_000_000
+
+
+def csv_line(eng, steps, warmup):
+    """Ingest from a CSV file (never `value`): the native
+    reader (csrc/csv_reader.cpp: host threads parse into pinned Arrow batches,
+    one batch ahead) alone, and feeding the C2 query (s = 0.5) through the
+    pipelined host entry point batch by batch, as ctx.sql over a CSV table
+    runs. File: CSV_ROWS rows of the seed-42 a, b, c columns (repr floats)."""
+    import tempfile
+    import pandas as pd
+    from datafusion_amd.execution import NativeCsvDataSource
+    from datafusion_amd.execution.engine import column_struct
+    from oracle_ffi import gen_unit_f64
+    n = CSV_ROWS
+    schema = Schema([Field(c, DataType.Float64, False) for c in "abc"])
+    d = tempfile.mkdtemp(prefix="dfmi_csv_")
+    path = os.path.join(d, "c2.csv")
+    pd.DataFrame({c: gen_unit_f64(SEED, j, 0, n) for j, c in enumerate("abc")}).to_csv(path, index=False)
+    size = os.path.getsize(path)
+    pred_e, proj_e = query(0.5)
+    pred = compile_scalar_expr(None, pred_e, schema)
+    projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+    progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
+    L = _abi.lib()
+    err = _abi.dfmi_error()
+    batch = 1 << 20
+
+    def parse_only():
+        src = NativeCsvDataSource(schema, path, True, batch)
+        rows = 0
+        while True:
+            b = src.next()
+            if b is None:
+                return rows
+            rows += b.num_rows()
+
+    def end_to_end():
+        src = NativeCsvDataSource(schema, path, True, batch)
+        rows = sel = 0
+        while True:
+            b = src.next()
+            if b is None:
+                return rows, sel
+            carr = (_abi.dfmi_column * 3)(*[column_struct(a) for a in b.columns])
+            cb = _abi.dfmi_batch(3, 0, b.num_rows(), carr)
+            res = C.c_void_p()
+            rc = L.dfmi_filter_project_host(eng.ctx, pred.handle, progs, 3, C.byref(cb), 0, C.byref(res),
+                                            C.byref(err))
+            if rc != 0:
+                raise RuntimeError(err.message.decode())
+            v = _abi.dfmi_column()
+            L.dfmi_host_result_column(res, 0, C.byref(v))
+            sel += v.length
+            L.dfmi_host_result_free(res)
+            rows += b.num_rows()
+
+    out = {"workload": "CSV file of %d rows x 3 Float64 (%.0f MB), batches of %d rows" % (n, size / 1e6, batch)}
+    for name, fn in (("parse_only", parse_only), ("csv_sql_c2", end_to_end)):
+        for _ in range(warmup):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = fn()
+        el = (time.perf_counter() - t0) / steps
+        out[name] = {"ms": round(el * 1e3, 1), "rows_per_s": n / el, "csv_gbs": round(size / el / 1e9, 2)}
+        if name == "csv_sql_c2":
+            out[name]["selected"] = r[1]
+    out["host_threads"] = int(os.environ.get("DFMI_CSV_THREADS", "0")) or min(8, os.cpu_count() or 1)
+    os.remove(path)
+    os.rmdir(d)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -564,7 +638,7 @@ def main():
     ap.add_argument("--sel", type=float, default=0.5, help="headline selectivity")
     ap.add_argument("--sweep", default="0.01,0.5,0.99", help="selectivities also reported (first=headline if set)")
     ap.add_argument("--extra", default="c4,q6,c3,batches",
-                    help="extra config lines (comma list: c4,q6,c3,batches,host; empty = none)")
+                    help="extra config lines (comma list: c4,q6,c3,batches,host,csv; empty = none)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -621,6 +695,9 @@ def main():
         elif name == "host":
             if world == 1:
                 extra["host"] = host_line(eng, min(args.steps, 3), 1)
+        elif name == "csv":
+            if world == 1:
+                extra["csv"] = csv_line(eng, min(args.steps, 3), 1)
         elif name == "c3":
             extra["c3"] = c3_line(eng, dev, rank, world, args.steps, args.warmup, dist)
         else:

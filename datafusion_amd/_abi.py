@@ -25,6 +25,7 @@ DFMI_ERR_PANIC = 7
 DFMI_ERR_INVALID_ARGUMENT = 8
 DFMI_ERR_CAPACITY = 9
 DFMI_ERR_DEVICE = 10
+DFMI_ERR_ARROW_PARSE = 11
 
 DFMI_FLAG_EXT_GATHER_ALL = 0x1
 DFMI_FLAG_EXT_UTF8_COMPARE = 0x2
@@ -49,6 +50,7 @@ STATUS_NAMES = {
     DFMI_ERR_INVALID_ARGUMENT: "InvalidArgument",
     DFMI_ERR_CAPACITY: "Capacity",
     DFMI_ERR_DEVICE: "Device",
+    DFMI_ERR_ARROW_PARSE: "ArrowError(ParseError)",
 }
 
 
@@ -165,6 +167,10 @@ EXPORTED = [
     "dfmi_shard_agg_finish",
     "dfmi_agg_state_free",
     "dfmi_generate_column",  # include/dfmi_datasource.h
+    "dfmi_csv_open",
+    "dfmi_csv_next",
+    "dfmi_csv_num_records",
+    "dfmi_csv_close",
 ]
 
 DFMI_GEN_UNIT_F64 = 1
@@ -266,6 +272,15 @@ def lib() -> C.CDLL:
     L.dfmi_generate_column.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_void_p, C.POINTER(dfmi_error)]
     L.dfmi_generate_column.restype = C.c_int32
+    L.dfmi_csv_open.argtypes = [C.c_char_p, C.POINTER(dfmi_schema), C.c_int32, C.c_int64, C.c_int32,
+                                C.POINTER(C.c_void_p), C.POINTER(dfmi_error)]
+    L.dfmi_csv_open.restype = C.c_int32
+    L.dfmi_csv_next.argtypes = [C.c_void_p, C.POINTER(dfmi_batch), C.POINTER(C.c_int32), C.POINTER(dfmi_error)]
+    L.dfmi_csv_next.restype = C.c_int32
+    L.dfmi_csv_num_records.argtypes = [C.c_void_p]
+    L.dfmi_csv_num_records.restype = C.c_int64
+    L.dfmi_csv_close.argtypes = [C.c_void_p]
+    L.dfmi_csv_close.restype = None
     P = C.POINTER
     L.dfmi_compile_aggregate.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_uint32, P(C.c_void_p), P(dfmi_error)]
     L.dfmi_compile_aggregate.restype = C.c_int32

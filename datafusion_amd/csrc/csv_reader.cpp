@@ -1,0 +1,563 @@
+// Native CSV source: the reference's CsvDataSource (datasource.rs:31-50) over
+// arrow 0.12's csv::Reader (csv_sql.rs:49: schema, has_header, batch size),
+// producing Arrow batches straight into pinned host memory, so
+// dfmi_filter_project_host DMAs them without a staging copy.
+//
+//   open : mmap the file, index the records (one pass: memchr over '\n' when
+//          the file holds no quote character, a quote-aware scan otherwise);
+//   next : the batch parsed by host threads (row ranges of whole 64-row
+//          words, so validity / Boolean bitmap words are never shared);
+//          while the caller works on batch i the reader already parses
+//          batch i+1 into the other of two pinned buffer sets.
+//
+// Field rules (arrow 0.12 reader, as tests/golden_cases' restatement): ','
+// separated, a field starting with '"' is quoted ("" = one quote), records
+// end at '\n' (a preceding '\r' is dropped), empty records are skipped, a
+// missing trailing field or an empty numeric field is null, Utf8 keeps the
+// bytes (a null Utf8 field is ""), Boolean is true/false (any case), numbers
+// as Rust's str::parse (decimal; inf / infinity / nan words), anything else
+// is ArrowError(ParseError) "Error while parsing value <field>".
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/dfmi.h"
+#include "../../include/dfmi_datasource.h"
+
+namespace {
+
+int width_of(int t) {
+    switch (t) {
+        case DFMI_TYPE_INT8: case DFMI_TYPE_UINT8: return 1;
+        case DFMI_TYPE_INT16: case DFMI_TYPE_UINT16: return 2;
+        case DFMI_TYPE_INT32: case DFMI_TYPE_UINT32: case DFMI_TYPE_FLOAT32: return 4;
+        case DFMI_TYPE_INT64: case DFMI_TYPE_UINT64: case DFMI_TYPE_FLOAT64: return 8;
+        default: return 0;
+    }
+}
+
+void set_err(dfmi_error* err, int32_t code, const std::string& m) {
+    if (!err) return;
+    err->code = code;
+    snprintf(err->message, sizeof err->message, "%s", m.c_str());
+}
+
+// Grow-only host buffer, pinned (hipHostMalloc) when a device is present --
+// the DMA engines then read it directly -- else 64-byte aligned pageable
+// memory (the host path stages pageable buffers itself).
+struct PinBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    void release() {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else free(p);
+        }
+        p = nullptr;
+        cap = 0;
+    }
+    bool reserve(size_t n) {
+        n = (std::max<size_t>(n, 64) + 63) & ~(size_t)63;
+        if (n <= cap) return true;
+        release();
+        if (hipHostMalloc((void**)&p, n, hipHostMallocPortable) == hipSuccess) {
+            pinned = true;
+        } else {
+            (void)hipGetLastError();
+            pinned = false;
+            p = (uint8_t*)aligned_alloc(64, n);
+            if (!p) return false;
+        }
+        cap = n;
+        return true;
+    }
+    ~PinBuf() { release(); }
+};
+
+// One parsed field: [b, e) of the file, quoted (unescape "" when copying).
+struct Field {
+    const char* b = nullptr;
+    const char* e = nullptr;
+    bool quoted = false, present = false;
+};
+
+// Fields of the record [p, end) (end excludes the line terminator).
+void split_record(const char* p, const char* end, int ncols, Field* out) {
+    for (int i = 0; i < ncols; ++i) out[i] = Field{};
+    int i = 0;
+    while (true) {
+        Field f;
+        f.present = true;
+        if (p < end && *p == '"') {
+            f.quoted = true;
+            const char* q = p + 1;
+            const char* s = q;
+            while (q < end) {
+                if (*q == '"') {
+                    if (q + 1 < end && q[1] == '"') {
+                        q += 2;
+                        continue;
+                    }
+                    break;
+                }
+                ++q;
+            }
+            f.b = s;
+            f.e = q;  // closing quote (or end)
+            p = q < end ? q + 1 : end;
+            while (p < end && *p != ',') ++p;  // bytes after the closing quote are dropped
+        } else {
+            const char* q = (const char*)memchr(p, ',', (size_t)(end - p));
+            if (!q) q = end;
+            f.b = p;
+            f.e = q;
+            p = q;
+        }
+        if (i < ncols) out[i] = f;
+        ++i;
+        if (p >= end) break;
+        ++p;  // the ','
+    }
+}
+
+size_t field_len(const Field& f) {
+    if (!f.present) return 0;
+    if (!f.quoted) return (size_t)(f.e - f.b);
+    size_t n = 0;
+    for (const char* q = f.b; q < f.e; ++q, ++n)
+        if (*q == '"' && q + 1 < f.e && q[1] == '"') ++q;
+    return n;
+}
+
+void field_copy(const Field& f, uint8_t* dst) {
+    if (!f.present) return;
+    if (!f.quoted) {
+        memcpy(dst, f.b, (size_t)(f.e - f.b));
+        return;
+    }
+    for (const char* q = f.b; q < f.e; ++q) {
+        *dst++ = (uint8_t)*q;
+        if (*q == '"' && q + 1 < f.e && q[1] == '"') ++q;
+    }
+}
+
+std::string field_text(const Field& f) {
+    std::string s(field_len(f), '\0');
+    field_copy(f, (uint8_t*)&s[0]);
+    return s;
+}
+
+bool lower_eq(const std::string& s, const char* w) {
+    if (s.size() != strlen(w)) return false;
+    for (size_t i = 0; i < s.size(); ++i)
+        if (tolower((unsigned char)s[i]) != w[i]) return false;
+    return true;
+}
+
+// Rust f64::from_str: [+-] then decimal digits with an optional '.', an
+// optional exponent, or the words inf / infinity / nan (any case).
+bool parse_float(const std::string& s, double* v) {
+    size_t i = 0;
+    bool neg = false;
+    if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+    const std::string rest = s.substr(i);
+    if (lower_eq(rest, "inf") || lower_eq(rest, "infinity")) {
+        *v = neg ? -INFINITY : INFINITY;
+        return true;
+    }
+    if (lower_eq(rest, "nan")) {
+        *v = NAN;
+        return true;
+    }
+    size_t digits = 0;
+    while (i < s.size() && isdigit((unsigned char)s[i])) ++i, ++digits;
+    if (i < s.size() && s[i] == '.') {
+        ++i;
+        while (i < s.size() && isdigit((unsigned char)s[i])) ++i, ++digits;
+    }
+    if (!digits) return false;
+    if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
+        ++i;
+        if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
+        size_t ed = 0;
+        while (i < s.size() && isdigit((unsigned char)s[i])) ++i, ++ed;
+        if (!ed) return false;
+    }
+    if (i != s.size()) return false;
+    *v = strtod(s.c_str(), nullptr);  // glibc: correctly rounded, as Rust's parser
+    return true;
+}
+
+// Rust iN / uN::from_str: optional sign ('-' only for signed), decimal digits, in range.
+bool parse_int(const std::string& s, bool is_signed, int bits, int64_t* v) {
+    size_t i = 0;
+    bool neg = false;
+    if (i < s.size() && (s[i] == '+' || s[i] == '-')) {
+        neg = s[i] == '-';
+        if (neg && !is_signed) return false;
+        ++i;
+    }
+    if (i == s.size()) return false;
+    unsigned __int128 acc = 0;
+    for (; i < s.size(); ++i) {
+        if (!isdigit((unsigned char)s[i])) return false;
+        acc = acc * 10 + (unsigned)(s[i] - '0');
+        if (acc > ((unsigned __int128)1 << 64)) return false;
+    }
+    if (is_signed) {
+        const unsigned __int128 lim = (unsigned __int128)1 << (bits - 1);
+        if (neg ? acc > lim : acc >= lim) return false;
+        *v = neg ? (int64_t)(0 - (uint64_t)acc) : (int64_t)(uint64_t)acc;
+    } else {
+        if (bits < 64 ? acc >= ((unsigned __int128)1 << bits) : acc > (unsigned __int128)UINT64_MAX) return false;
+        *v = (int64_t)(uint64_t)acc;
+    }
+    return true;
+}
+
+struct ColBufs {
+    PinBuf values, validity, offsets;
+};
+
+struct BatchSet {
+    std::vector<ColBufs> cols;
+    std::vector<dfmi_column> view;
+    int64_t rows = 0;
+    int32_t code = DFMI_OK;
+    std::string msg;
+};
+
+}  // namespace
+
+struct dfmi_csv_reader {
+    int fd = -1;
+    const char* data = nullptr;
+    size_t size = 0;
+    std::vector<int> types;
+    int64_t batch_size = 1024;
+    int threads = 1;
+    std::vector<uint64_t> rec_b, rec_e;  // record byte ranges (without terminators)
+    size_t next_row = 0;                 // first record of the batch the next prefetch parses
+    BatchSet sets[2];
+    int cur = 0;
+    std::thread prefetch;
+    bool prefetching = false;
+    bool ended = false;
+
+    ~dfmi_csv_reader() {
+        if (prefetch.joinable()) prefetch.join();
+        if (data) munmap((void*)data, size);
+        if (fd >= 0) close(fd);
+    }
+
+    void index_records(bool has_header) {
+        const char* p = data;
+        const char* end = data + size;
+        const bool quotes = memchr(data, '"', size) != nullptr;
+        auto add = [&](const char* b, const char* e) {
+            if (e > b && e[-1] == '\r') --e;
+            if (e > b) {  // empty records are skipped
+                rec_b.push_back((uint64_t)(b - data));
+                rec_e.push_back((uint64_t)(e - data));
+            }
+        };
+        if (!quotes) {
+            while (p < end) {
+                const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+                const char* e = nl ? nl : end;
+                add(p, e);
+                p = nl ? nl + 1 : end;
+            }
+        } else {
+            // a quote opens a quoted field only at the field's start; inside
+            // one, "" is a literal quote and a lone " closes it
+            enum { START, PLAIN, QUOTED, QUOTE } st = START;
+            const char* b = p;
+            for (; p < end; ++p) {
+                const char ch = *p;
+                switch (st) {
+                    case START:
+                        st = ch == '"' ? QUOTED : PLAIN;
+                        if (ch == ',') st = START;
+                        break;
+                    case PLAIN:
+                        if (ch == ',') st = START;
+                        break;
+                    case QUOTED:
+                        if (ch == '"') st = QUOTE;
+                        break;
+                    case QUOTE:  // "" (literal quote) or the field's end
+                        st = ch == '"' ? QUOTED : (ch == ',' ? START : PLAIN);
+                        break;
+                }
+                if (ch == '\n' && st != QUOTED) {
+                    add(b, p);
+                    b = p + 1;
+                    st = START;
+                }
+            }
+            if (b < end) add(b, end);
+        }
+        if (has_header && !rec_b.empty()) {
+            rec_b.erase(rec_b.begin());
+            rec_e.erase(rec_e.begin());
+        }
+    }
+
+    // Parse records [r0, r0 + n) into set S.
+    void parse(BatchSet& S, size_t r0, int64_t n) {
+        const int nc = (int)types.size();
+        S.rows = n;
+        S.code = DFMI_OK;
+        S.msg.clear();
+        S.cols.resize(nc);
+        S.view.assign(std::max(1, nc), dfmi_column{});
+        const size_t bm = (size_t)((n + 63) / 64) * 8;
+        for (int c = 0; c < nc; ++c) {
+            const int t = types[c];
+            ColBufs& B = S.cols[c];
+            bool ok = B.validity.reserve(bm);
+            if (t == DFMI_TYPE_UTF8) ok = ok && B.offsets.reserve((size_t)(n + 1) * 4);
+            else ok = ok && B.values.reserve(t == DFMI_TYPE_BOOLEAN ? bm : (size_t)n * width_of(t));
+            if (!ok) {
+                S.code = DFMI_ERR_DEVICE;
+                S.msg = "hipHostMalloc failed for a CSV batch";
+                return;
+            }
+        }
+        // row ranges of whole 64-row words per thread (bitmap words are never shared)
+        const int64_t words = (n + 63) / 64;
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, words));
+        std::vector<int64_t> nulls((size_t)nt * std::max(1, nc), 0);
+        // a parse error: arrow's reader builds the batch column by column, so
+        // the one it reports is the first failing row of the first failing column
+        std::vector<std::string> errs(nt);
+        std::vector<int64_t> err_row(nt, -1);
+        std::vector<int> err_col(nt, 1 << 30);
+        auto range = [&](int t, int64_t& a, int64_t& b) {
+            a = std::min<int64_t>(n, words * t / nt * 64);
+            b = std::min<int64_t>(n, words * (t + 1) / nt * 64);
+        };
+        // pass 1: numeric / Boolean values, validity, Utf8 lengths (into offsets[row + 1])
+        auto pass1 = [&](int t) {
+            int64_t a, b;
+            range(t, a, b);
+            std::vector<Field> f(std::max(1, nc));
+            for (int64_t r = a; r < b; ++r) {
+                split_record(data + rec_b[r0 + r], data + rec_e[r0 + r], nc, f.data());
+                for (int c = 0; c < nc; ++c) {
+                    const int ty = types[c];
+                    ColBufs& B = S.cols[c];
+                    uint64_t* vw = (uint64_t*)B.validity.p;
+                    const int64_t w = r >> 6;
+                    const uint64_t bit = 1ull << (r & 63);
+                    if ((r & 63) == 0) vw[w] = 0;
+                    if (ty == DFMI_TYPE_UTF8) {
+                        ((int32_t*)B.offsets.p)[r + 1] = (int32_t)field_len(f[c]);
+                        if (f[c].present) vw[w] |= bit;
+                        else ++nulls[(size_t)t * nc + c];
+                        continue;
+                    }
+                    if (ty == DFMI_TYPE_BOOLEAN && (r & 63) == 0) ((uint64_t*)B.values.p)[w] = 0;
+                    const bool empty = !f[c].present || f[c].e == f[c].b;
+                    if (empty) {  // null
+                        if (ty != DFMI_TYPE_BOOLEAN) memset(B.values.p + (size_t)r * width_of(ty), 0, width_of(ty));
+                        ++nulls[(size_t)t * nc + c];
+                        continue;
+                    }
+                    vw[w] |= bit;
+                    const std::string s = field_text(f[c]);
+                    bool ok = true;
+                    if (ty == DFMI_TYPE_BOOLEAN) {
+                        if (lower_eq(s, "true")) ((uint64_t*)B.values.p)[w] |= bit;
+                        else ok = lower_eq(s, "false");
+                    } else if (ty == DFMI_TYPE_FLOAT64 || ty == DFMI_TYPE_FLOAT32) {
+                        double d = 0;
+                        ok = parse_float(s, &d);
+                        if (ty == DFMI_TYPE_FLOAT64) memcpy(B.values.p + (size_t)r * 8, &d, 8);
+                        else {
+                            const float x = ok ? strtof(s.c_str(), nullptr) : 0.f;  // direct to f32: one rounding
+                            memcpy(B.values.p + (size_t)r * 4, &x, 4);
+                        }
+                    } else {
+                        const bool sg = ty >= DFMI_TYPE_INT8 && ty <= DFMI_TYPE_INT64;
+                        const int wdt = width_of(ty);
+                        int64_t v = 0;
+                        ok = parse_int(s, sg, 8 * wdt, &v);
+                        memcpy(B.values.p + (size_t)r * wdt, &v, wdt);  // little-endian low bytes
+                    }
+                    if (!ok && c < err_col[t]) {
+                        err_col[t] = c;
+                        err_row[t] = r;
+                        errs[t] = "Error while parsing value " + s;
+                    }
+                }
+            }
+        };
+        run(nt, pass1);
+        int bt = -1;
+        for (int t = 0; t < nt; ++t)  // threads hold ascending row ranges
+            if (err_row[t] >= 0 && (bt < 0 || err_col[t] < err_col[bt])) bt = t;
+        if (bt >= 0) {
+            S.code = DFMI_ERR_ARROW_PARSE;
+            S.msg = errs[bt];
+            return;
+        }
+        // Utf8 offsets: prefix sums; bytes: pass 2
+        for (int c = 0; c < nc; ++c) {
+            if (types[c] != DFMI_TYPE_UTF8) continue;
+            int32_t* of = (int32_t*)S.cols[c].offsets.p;
+            of[0] = 0;
+            int64_t acc = 0;
+            for (int64_t r = 0; r < n; ++r) {
+                acc += of[r + 1];
+                if (acc >= ((int64_t)1 << 31)) {
+                    S.code = DFMI_ERR_CAPACITY;
+                    S.msg = "a CSV batch's Utf8 column exceeds 2^31 bytes (i32 offsets)";
+                    return;
+                }
+                of[r + 1] = (int32_t)acc;
+            }
+            if (!S.cols[c].values.reserve((size_t)acc + 8)) {
+                S.code = DFMI_ERR_DEVICE;
+                S.msg = "hipHostMalloc failed for a CSV batch";
+                return;
+            }
+        }
+        bool any_utf8 = false;
+        for (int c = 0; c < nc; ++c) any_utf8 |= types[c] == DFMI_TYPE_UTF8;
+        if (any_utf8) {
+            auto pass2 = [&](int t) {
+                int64_t a, b;
+                range(t, a, b);
+                std::vector<Field> f(std::max(1, nc));
+                for (int64_t r = a; r < b; ++r) {
+                    split_record(data + rec_b[r0 + r], data + rec_e[r0 + r], nc, f.data());
+                    for (int c = 0; c < nc; ++c)
+                        if (types[c] == DFMI_TYPE_UTF8)
+                            field_copy(f[c], S.cols[c].values.p + ((int32_t*)S.cols[c].offsets.p)[r]);
+                }
+            };
+            run(nt, pass2);
+        }
+        for (int c = 0; c < nc; ++c) {
+            int64_t nn = 0;
+            for (int t = 0; t < nt; ++t) nn += nulls[(size_t)t * nc + c];
+            dfmi_column& v = S.view[c];
+            v.type = types[c];
+            v.length = n;
+            v.null_count = types[c] == DFMI_TYPE_UTF8 ? 0 : nn;  // a null Utf8 field reads as "" (no validity)
+            v.validity = (types[c] != DFMI_TYPE_UTF8 && nn) ? S.cols[c].validity.p : nullptr;
+            v.values = S.cols[c].values.p;
+            v.offsets = types[c] == DFMI_TYPE_UTF8 ? (const int32_t*)S.cols[c].offsets.p : nullptr;
+        }
+    }
+
+    template <class F>
+    void run(int nt, F& f) {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back([&, t] { f(t); });
+        f(0);
+        for (auto& x : th) x.join();
+    }
+
+    void start_prefetch(int set) {
+        const size_t r0 = next_row;
+        const int64_t n = (int64_t)std::min<size_t>((size_t)batch_size, rec_b.size() - r0);
+        next_row = r0 + (size_t)n;
+        prefetching = true;
+        prefetch = std::thread([this, set, r0, n] { parse(sets[set], r0, n); });
+    }
+};
+
+extern "C" int32_t dfmi_csv_open(const char* path, const dfmi_schema* schema, int32_t has_header, int64_t batch_size,
+                                 int32_t threads, dfmi_csv_reader** out, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    if (!path || !schema || !out || batch_size <= 0 || (schema->num_fields > 0 && !schema->fields)) {
+        set_err(err, DFMI_ERR_INVALID_ARGUMENT, "bad argument");
+        return DFMI_ERR_INVALID_ARGUMENT;
+    }
+    *out = nullptr;
+    dfmi_csv_reader* R = new dfmi_csv_reader();
+    for (int i = 0; i < schema->num_fields; ++i) {
+        const int t = schema->fields[i].type;
+        if (t != DFMI_TYPE_UTF8 && t != DFMI_TYPE_BOOLEAN && !width_of(t)) {
+            delete R;
+            set_err(err, DFMI_ERR_NOT_IMPLEMENTED, "CSV column type");
+            return DFMI_ERR_NOT_IMPLEMENTED;
+        }
+        R->types.push_back(t);
+    }
+    R->batch_size = batch_size;
+    if (threads <= 0)
+        if (const char* e = getenv("DFMI_CSV_THREADS")) threads = atoi(e);
+    R->threads = threads > 0 ? std::min(threads, 64)
+                             : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    R->fd = open(path, O_RDONLY);
+    if (R->fd < 0) {
+        const std::string m = std::string(path) + ": " + strerror(errno);
+        delete R;
+        set_err(err, DFMI_ERR_GENERAL, "IoError: " + m);  // ExecutionError::IoError (error.rs:27)
+        return DFMI_ERR_GENERAL;
+    }
+    struct stat st;
+    fstat(R->fd, &st);
+    R->size = (size_t)st.st_size;
+    if (R->size) {
+        void* m = mmap(nullptr, R->size, PROT_READ, MAP_PRIVATE, R->fd, 0);
+        if (m == MAP_FAILED) {
+            delete R;
+            set_err(err, DFMI_ERR_GENERAL, "IoError: mmap failed");
+            return DFMI_ERR_GENERAL;
+        }
+        R->data = (const char*)m;
+        madvise(m, R->size, MADV_SEQUENTIAL);
+        R->index_records(has_header != 0);
+    }
+    if (!R->rec_b.empty()) R->start_prefetch(0);
+    *out = R;
+    return DFMI_OK;
+}
+
+extern "C" int32_t dfmi_csv_next(dfmi_csv_reader* R, dfmi_batch* out, int32_t* has_batch, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    if (!R || !out || !has_batch) {
+        set_err(err, DFMI_ERR_INVALID_ARGUMENT, "NULL argument");
+        return DFMI_ERR_INVALID_ARGUMENT;
+    }
+    *has_batch = 0;
+    if (!R->prefetching) return DFMI_OK;  // end of the file
+    R->prefetch.join();
+    R->prefetching = false;
+    const int set = R->cur;
+    BatchSet& S = R->sets[set];
+    if (S.code != DFMI_OK) {
+        set_err(err, S.code, S.msg);
+        return S.code;
+    }
+    R->cur ^= 1;
+    if (R->next_row < R->rec_b.size()) R->start_prefetch(R->cur);  // batch i+1 while the caller runs batch i
+    out->num_columns = (int32_t)R->types.size();
+    out->reserved = 0;
+    out->num_rows = S.rows;
+    out->columns = S.view.data();
+    *has_batch = 1;
+    return DFMI_OK;
+}
+
+extern "C" int64_t dfmi_csv_num_records(const dfmi_csv_reader* R) { return R ? (int64_t)R->rec_b.size() : -1; }
+
+extern "C" void dfmi_csv_close(dfmi_csv_reader* R) { delete R; }

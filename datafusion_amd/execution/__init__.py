@@ -1,6 +1,6 @@
 """Execution layer mirror (src/execution/)."""
 from .context import ExecutionContext, Projection, Selection, TableScan
-from .datasource import CsvDataSource, DataSource, MemoryDataSource
+from .datasource import CsvDataSource, DataSource, MemoryDataSource, NativeCsvDataSource
 from .error import ExecutionError
 from .expression import RuntimeExpr, compile_expr, compile_scalar_expr
 from .filter import FilterRelation

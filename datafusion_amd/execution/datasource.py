@@ -33,6 +33,20 @@ def _parse_bool(s: str) -> bool:
     raise ExecutionError("ArrowError(ParseError)", "Error while parsing value %s" % s)
 
 
+def _parse_number(dt: DataType, s: str):
+    try:
+        if dt in (DataType.Float32, DataType.Float64):
+            return float(s)
+        v = int(s, 10)
+    except ValueError:
+        raise ExecutionError("ArrowError(ParseError)", "Error while parsing value %s" % s)
+    from ..arrow import np_dtype
+    info = np.iinfo(np_dtype(dt))
+    if not info.min <= v <= info.max:
+        raise ExecutionError("ArrowError(ParseError)", "Error while parsing value %s" % s)
+    return v
+
+
 def _parse_column(dt: DataType, cells: List[Optional[str]]) -> Array:
     if dt == DataType.Utf8:
         return Array.from_strings([("" if c is None else c).encode("utf-8") for c in cells])
@@ -45,10 +59,8 @@ def _parse_column(dt: DataType, cells: List[Optional[str]]) -> Array:
         valid.append(True)
         if dt == DataType.Boolean:
             vals.append(_parse_bool(c))
-        elif dt in (DataType.Float32, DataType.Float64):
-            vals.append(float(c))
         else:
-            vals.append(int(c))
+            vals.append(_parse_number(dt, c))
     valid = np.array(valid, dtype=bool)
     if dt == DataType.Boolean:
         return Array.from_numpy(dt, np.array(vals, dtype=bool), None if valid.all() else valid)
@@ -81,6 +93,84 @@ class CsvDataSource(DataSource):
         for i, f in enumerate(self._schema.fields):
             cols.append(_parse_column(f.data_type, [r[i] if i < len(r) else None for r in chunk]))
         return RecordBatch(self._schema, cols)
+
+
+class NativeCsvDataSource(DataSource):
+    """CsvDataSource over the native reader (dfmi_csv_open, include/dfmi_datasource.h):
+    host threads parse straight into pinned Arrow buffers and the next batch
+    is parsed while the caller works on this one. Same batches as
+    CsvDataSource; each stays valid until the next ``next()`` (the reference's
+    pull order), or pass ``copy=True`` to keep them."""
+
+    def __init__(self, schema: Schema, path: str, has_header: bool = True, batch_size: int = 1024,
+                 threads: int = 0, copy: bool = False):
+        import ctypes as C
+        from .. import _abi
+        self._schema = schema
+        self._copy = copy
+        L = _abi.lib()
+        fields = (_abi.dfmi_field * max(1, len(schema.fields)))()
+        self._names = [f.name.encode() for f in schema.fields]
+        for i, f in enumerate(schema.fields):
+            fields[i].name = self._names[i]
+            fields[i].type = int(f.data_type)
+            fields[i].nullable = 1 if f.nullable else 0
+        sch = _abi.dfmi_schema(len(schema.fields), 0, fields)
+        err = _abi.dfmi_error()
+        h = C.c_void_p()
+        rc = L.dfmi_csv_open(path.encode(), C.byref(sch), 1 if has_header else 0, batch_size, threads, C.byref(h),
+                             C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        self._h = h
+        self._close = L.dfmi_csv_close
+
+    def schema(self) -> Schema:
+        return self._schema
+
+    def num_records(self) -> int:
+        from .. import _abi
+        return int(_abi.lib().dfmi_csv_num_records(self._h))
+
+    def next(self) -> Optional[RecordBatch]:
+        import ctypes as C
+        import torch
+        from .. import _abi
+        L = _abi.lib()
+        b = _abi.dfmi_batch()
+        has = C.c_int32()
+        err = _abi.dfmi_error()
+        rc = L.dfmi_csv_next(self._h, C.byref(b), C.byref(has), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        if not has.value:
+            return None
+        n = b.num_rows
+
+        def view(ptr, nbytes, dtype=np.uint8):
+            if not nbytes:
+                return torch.zeros(8, dtype=torch.uint8 if dtype == np.uint8 else torch.int32)
+            a = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,)).view(dtype)
+            return torch.from_numpy(a.copy() if self._copy else a)
+        cols = []
+        for i, f in enumerate(self._schema.fields):
+            c = b.columns[i]
+            t = DataType(c.type)
+            vb = view(c.validity, (n + 7) // 8) if (c.null_count and c.validity) else None
+            if t == DataType.Utf8:
+                offs = view(c.offsets, 4 * (n + 1), np.int32)
+                nbytes = int(offs[n]) if n else 0
+                cols.append(Array(t, n, view(c.values, nbytes), None, offs, 0))
+            else:
+                nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
+                cols.append(Array(t, n, view(c.values, nb), vb, None, c.null_count))
+        return RecordBatch(self._schema, cols)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._close(h)
+            self._h = None
 
 
 class MemoryDataSource(DataSource):

@@ -25,7 +25,11 @@ class FilterRelation(Relation):
         batch = self.input.next()
         if batch is None:
             return None
-        cols = engine(self.device).filter_project(self.expr, None, batch, self.flags)
+        eng = engine(self.device)
+        if all(c.values.device.type == "cpu" for c in batch.columns):
+            cols = eng.filter_project_host(self.expr, None, batch, self.flags)  # host batch: host results
+        else:
+            cols = eng.filter_project(self.expr, None, batch, self.flags)
         return RecordBatch(Schema.empty(), cols)
 
     def schema(self) -> Schema:

@@ -40,7 +40,13 @@ class ProjectRelation(Relation):
             pred = None
         if batch is None:
             return None
-        cols = engine(self.device).filter_project(pred, self.expr, batch, self.flags)
+        eng = engine(self.device)
+        if all(c.values.device.type == "cpu" for c in batch.columns):
+            # a host batch (e.g. a CSV source's pinned buffers): the pipelined
+            # host entry point, host results -- what a Rust caller gets
+            cols = eng.filter_project_host(pred, self.expr, batch, self.flags)
+        else:
+            cols = eng.filter_project(pred, self.expr, batch, self.flags)
         schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
         return RecordBatch(schema, cols)
 

@@ -62,7 +62,8 @@ typedef enum dfmi_status {
     DFMI_ERR_PANIC = 7,           /* the reference panics (unwrap / i64 overflow) */
     DFMI_ERR_INVALID_ARGUMENT = 8,/* ABI misuse (bad pointer, alignment, sizes) */
     DFMI_ERR_CAPACITY = 9,        /* caller-provided output buffer too small */
-    DFMI_ERR_DEVICE = 10          /* HIP runtime failure / device timeout */
+    DFMI_ERR_DEVICE = 10,         /* HIP runtime failure / device timeout */
+    DFMI_ERR_ARROW_PARSE = 11     /* ExecutionError::ArrowError(ParseError): CSV field */
 } dfmi_status;
 
 typedef struct dfmi_error {

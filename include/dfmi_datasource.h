@@ -26,6 +26,25 @@ int32_t dfmi_generate_column(dfmi_context* ctx, int32_t kind, uint64_t seed, uin
                              int64_t row0, int64_t n, int64_t lo, int64_t hi, void* out,
                              dfmi_error* err);
 
+/* ---------------------------------------------------------------------------
+ * CSV source: CsvDataSource::new(schema, csv::Reader::new(file, schema,
+ * has_header, batch_size, None)) (datasource.rs:31-50, csv_sql.rs:49), native.
+ * Batches come back as HOST columns in pinned memory (ready for
+ * dfmi_filter_project_host's direct DMA); they stay valid until the next
+ * dfmi_csv_next or dfmi_csv_close. The reader parses batch i+1 (host threads)
+ * while the caller works on batch i. `threads` <= 0: up to 8.
+ * Errors: IoError (open) as DFMI_ERR_GENERAL "IoError: ...", a field that does
+ * not parse as ArrowError(ParseError) "Error while parsing value <field>".
+ * ------------------------------------------------------------------------- */
+typedef struct dfmi_csv_reader dfmi_csv_reader;
+
+int32_t dfmi_csv_open(const char* path, const dfmi_schema* schema, int32_t has_header, int64_t batch_size,
+                      int32_t threads, dfmi_csv_reader** out, dfmi_error* err);
+/* *has_batch = 0 at the end of the file. */
+int32_t dfmi_csv_next(dfmi_csv_reader* reader, dfmi_batch* out, int32_t* has_batch, dfmi_error* err);
+int64_t dfmi_csv_num_records(const dfmi_csv_reader* reader);
+void dfmi_csv_close(dfmi_csv_reader* reader);
+
 #ifdef __cplusplus
 }
 #endif
