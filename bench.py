@@ -159,15 +159,20 @@ def batches_line(eng, schema, cols, sel, dev):
         for _ in range(50):
             step()
         torch.cuda.synchronize(dev)
-        kern = 0.0
+        _abi.lib().dfmi_context_set_timing(eng.ctx, 0)  # production setting: no profiling events
         t0 = time.perf_counter()
         for _ in range(calls):
             step()
-            kern += eng.last_timing()[1]
         el = time.perf_counter() - t0
+        _abi.lib().dfmi_context_set_timing(eng.ctx, 1)
+        torch.cuda.synchronize(dev)
+        kern = 0.0  # device time from HIP events, in a loop of its own (reading them waits)
+        for _ in range(200):
+            step()
+            kern += eng.last_timing()[1]
         us = el / calls * 1e6
-        out["%d_rows" % m] = {"us_per_batch": round(us, 2), "kernel_us": round(kern / calls * 1e3, 2),
-                              "host_overhead_us": round(us - kern / calls * 1e3, 2), "calls": calls,
+        out["%d_rows" % m] = {"us_per_batch": round(us, 2), "kernel_us": round(kern / 200 * 1e3, 2),
+                              "host_overhead_us": round(us - kern / 200 * 1e3, 2), "calls": calls,
                               "rows_per_s": m / (us * 1e-6)}
     # a new query shape: generate + hipRTC compile on the first call, cached after
     pred, projs = query(sel)

@@ -141,6 +141,7 @@ EXPORTED = [
     "dfmi_host_result_num_columns",
     "dfmi_host_result_column",
     "dfmi_host_result_free",
+    "dfmi_context_set_timing",
     "dfmi_host_alloc",
     "dfmi_host_free",
     "dfmi_host_register",
@@ -255,6 +256,8 @@ def lib() -> C.CDLL:
     L.dfmi_host_result_column.restype = C.c_int32
     L.dfmi_host_result_free.argtypes = [C.c_void_p]
     L.dfmi_host_result_free.restype = None
+    L.dfmi_context_set_timing.argtypes = [C.c_void_p, C.c_int32]
+    L.dfmi_context_set_timing.restype = C.c_int32
     L.dfmi_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(dfmi_error)]
     L.dfmi_host_alloc.restype = C.c_int32
     L.dfmi_host_free.argtypes = [C.c_void_p]

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -160,61 +161,75 @@ std::string field_text(const Field& f) {
     return s;
 }
 
-bool lower_eq(const std::string& s, const char* w) {
-    if (s.size() != strlen(w)) return false;
-    for (size_t i = 0; i < s.size(); ++i)
-        if (tolower((unsigned char)s[i]) != w[i]) return false;
+bool lower_eq(const char* b, const char* e, const char* w) {
+    const size_t n = strlen(w);
+    if ((size_t)(e - b) != n) return false;
+    for (size_t i = 0; i < n; ++i)
+        if (tolower((unsigned char)b[i]) != w[i]) return false;
     return true;
 }
 
-// Rust f64::from_str: [+-] then decimal digits with an optional '.', an
-// optional exponent, or the words inf / infinity / nan (any case).
-bool parse_float(const std::string& s, double* v) {
-    size_t i = 0;
+// Rust f32 / f64 ::from_str on [b, e): [+-] then decimal digits with an
+// optional '.', an optional exponent, or the words inf / infinity / nan (any
+// case); correctly rounded to T (std::from_chars, no locale, no copy).
+template <typename T>
+bool parse_float(const char* b, const char* e, T* v) {
+    const char* p = b;
     bool neg = false;
-    if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
-    const std::string rest = s.substr(i);
-    if (lower_eq(rest, "inf") || lower_eq(rest, "infinity")) {
+    if (p < e && (*p == '+' || *p == '-')) neg = *p++ == '-';
+    if (lower_eq(p, e, "inf") || lower_eq(p, e, "infinity")) {
         *v = neg ? -INFINITY : INFINITY;
         return true;
     }
-    if (lower_eq(rest, "nan")) {
+    if (lower_eq(p, e, "nan")) {
         *v = NAN;
         return true;
     }
+    const char* q = p;
     size_t digits = 0;
-    while (i < s.size() && isdigit((unsigned char)s[i])) ++i, ++digits;
-    if (i < s.size() && s[i] == '.') {
-        ++i;
-        while (i < s.size() && isdigit((unsigned char)s[i])) ++i, ++digits;
+    while (q < e && isdigit((unsigned char)*q)) ++q, ++digits;
+    if (q < e && *q == '.') {
+        ++q;
+        while (q < e && isdigit((unsigned char)*q)) ++q, ++digits;
     }
     if (!digits) return false;
-    if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
-        ++i;
-        if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
+    if (q < e && (*q == 'e' || *q == 'E')) {
+        ++q;
+        if (q < e && (*q == '+' || *q == '-')) ++q;
         size_t ed = 0;
-        while (i < s.size() && isdigit((unsigned char)s[i])) ++i, ++ed;
+        while (q < e && isdigit((unsigned char)*q)) ++q, ++ed;
         if (!ed) return false;
     }
-    if (i != s.size()) return false;
-    *v = strtod(s.c_str(), nullptr);  // glibc: correctly rounded, as Rust's parser
+    if (q != e) return false;
+    T x = 0;
+    const auto r = std::from_chars(p, e, x);  // p: after any sign ('+' is not from_chars syntax)
+    if (r.ec == std::errc::result_out_of_range) {
+        // beyond T's range: strtod/strtof give +inf above and 0 / the nearest
+        // subnormal below, as Rust's parser does
+        const std::string t(p, e);
+        x = sizeof(T) == 4 ? (T)strtof(t.c_str(), nullptr) : (T)strtod(t.c_str(), nullptr);
+    } else if (r.ec != std::errc() || r.ptr != e) {
+        return false;
+    }
+    *v = neg ? -x : x;
     return true;
 }
 
-// Rust iN / uN::from_str: optional sign ('-' only for signed), decimal digits, in range.
-bool parse_int(const std::string& s, bool is_signed, int bits, int64_t* v) {
-    size_t i = 0;
+// Rust iN / uN::from_str on [b, e): optional sign ('-' only for signed),
+// decimal digits, in range.
+bool parse_int(const char* b, const char* e, bool is_signed, int bits, int64_t* v) {
+    const char* p = b;
     bool neg = false;
-    if (i < s.size() && (s[i] == '+' || s[i] == '-')) {
-        neg = s[i] == '-';
+    if (p < e && (*p == '+' || *p == '-')) {
+        neg = *p == '-';
         if (neg && !is_signed) return false;
-        ++i;
+        ++p;
     }
-    if (i == s.size()) return false;
+    if (p == e) return false;
     unsigned __int128 acc = 0;
-    for (; i < s.size(); ++i) {
-        if (!isdigit((unsigned char)s[i])) return false;
-        acc = acc * 10 + (unsigned)(s[i] - '0');
+    for (; p < e; ++p) {
+        if (!isdigit((unsigned char)*p)) return false;
+        acc = acc * 10 + (unsigned)(*p - '0');
         if (acc > ((unsigned __int128)1 << 64)) return false;
     }
     if (is_signed) {
@@ -379,30 +394,38 @@ struct dfmi_csv_reader {
                         continue;
                     }
                     vw[w] |= bit;
-                    const std::string s = field_text(f[c]);
+                    // the field's text: in place, unless quoted ("" unescaped)
+                    std::string unq;
+                    const char* fb = f[c].b;
+                    const char* fe = f[c].e;
+                    if (f[c].quoted) {
+                        unq = field_text(f[c]);
+                        fb = unq.data();
+                        fe = fb + unq.size();
+                    }
                     bool ok = true;
                     if (ty == DFMI_TYPE_BOOLEAN) {
-                        if (lower_eq(s, "true")) ((uint64_t*)B.values.p)[w] |= bit;
-                        else ok = lower_eq(s, "false");
-                    } else if (ty == DFMI_TYPE_FLOAT64 || ty == DFMI_TYPE_FLOAT32) {
+                        if (lower_eq(fb, fe, "true")) ((uint64_t*)B.values.p)[w] |= bit;
+                        else ok = lower_eq(fb, fe, "false");
+                    } else if (ty == DFMI_TYPE_FLOAT64) {
                         double d = 0;
-                        ok = parse_float(s, &d);
-                        if (ty == DFMI_TYPE_FLOAT64) memcpy(B.values.p + (size_t)r * 8, &d, 8);
-                        else {
-                            const float x = ok ? strtof(s.c_str(), nullptr) : 0.f;  // direct to f32: one rounding
-                            memcpy(B.values.p + (size_t)r * 4, &x, 4);
-                        }
+                        ok = parse_float(fb, fe, &d);
+                        memcpy(B.values.p + (size_t)r * 8, &d, 8);
+                    } else if (ty == DFMI_TYPE_FLOAT32) {
+                        float x = 0;  // parsed to f32 directly: one rounding, as Rust's f32 parse
+                        ok = parse_float(fb, fe, &x);
+                        memcpy(B.values.p + (size_t)r * 4, &x, 4);
                     } else {
                         const bool sg = ty >= DFMI_TYPE_INT8 && ty <= DFMI_TYPE_INT64;
                         const int wdt = width_of(ty);
                         int64_t v = 0;
-                        ok = parse_int(s, sg, 8 * wdt, &v);
+                        ok = parse_int(fb, fe, sg, 8 * wdt, &v);
                         memcpy(B.values.p + (size_t)r * wdt, &v, wdt);  // little-endian low bytes
                     }
                     if (!ok && c < err_col[t]) {
                         err_col[t] = c;
                         err_row[t] = r;
-                        errs[t] = "Error while parsing value " + s;
+                        errs[t] = "Error while parsing value " + std::string(fb, fe);
                     }
                 }
             }

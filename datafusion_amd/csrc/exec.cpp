@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -203,21 +204,27 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         X.window = 16;
         X.waves_per_eu = 8;
     }
-    if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
-    if (const char* bb = getenv("DFMI_BLOCK")) X.BLOCK = atoi(bb);        // diagnostics only
-    if (const char* ww = getenv("DFMI_WAVES_PER_EU")) X.waves_per_eu = atoi(ww);  // diagnostics only
-    // look-back / tile-order variants (diagnostics only)
-    if (const char* e = getenv("DFMI_LOOKBACK_R")) X.R = std::max(1, std::min(16, atoi(e)));
-    if (const char* e = getenv("DFMI_LOOKBACK_SLEEP")) X.sleep = std::max(0, std::min(127, atoi(e)));
-    if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
-    if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;  // diagnostics only
-    if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 3;  // diagnostics only (2 = serial)
-    if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;  // diagnostics only
+    // diagnostic knobs (tools/*): read only when DFMI_DIAG is set -- a dozen
+    // getenv scans per call would cost the 1024-row batch path microseconds
+    const bool diag = getenv("DFMI_DIAG") != nullptr;
+    if (diag) {
+        if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);
+        if (const char* bb = getenv("DFMI_BLOCK")) X.BLOCK = atoi(bb);
+        if (const char* ww = getenv("DFMI_WAVES_PER_EU")) X.waves_per_eu = atoi(ww);
+        // look-back / tile-order variants
+        if (const char* e = getenv("DFMI_LOOKBACK_R")) X.R = std::max(1, std::min(16, atoi(e)));
+        if (const char* e = getenv("DFMI_LOOKBACK_SLEEP")) X.sleep = std::max(0, std::min(127, atoi(e)));
+        if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
+        if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
+        if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;
+        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 3;  // 2 = serial
+        if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
+    }
     // a numeric predicate's tiles are VGPR-limited (3 blocks/CU): LDS has room
     // for a 4 KiB staging arena per wave, which stages ~4 slices per round trip
     if (!X.utf8_outs.empty() && !X.pred_slots.empty()) X.arena = 256;
-    if (const char* e = getenv("DFMI_UTF8_ARENA")) X.arena = std::max(128, std::min(1024, atoi(e)));  // diagnostics only
+    if (diag)
+        if (const char* e = getenv("DFMI_UTF8_ARENA")) X.arena = std::max(128, std::min(1024, atoi(e)));
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 256)
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
@@ -246,6 +253,7 @@ extern "C" int32_t dfmi_context_create(int32_t device, void* stream, dfmi_contex
         c->device = device;
         c->stream = (hipStream_t)stream;
         HIP_TRY(hipHostMalloc((void**)&c->host_hdr, kHdrAlloc, hipHostMallocDefault));
+
         HIP_TRY(hipEventCreate(&c->ev0));
         HIP_TRY(hipEventCreate(&c->ev1));
         HIP_TRY(hipEventCreate(&c->ev2));
@@ -285,6 +293,12 @@ extern "C" int32_t dfmi_context_set_stream(dfmi_context* c, void* stream) {
     return DFMI_OK;
 }
 
+extern "C" int32_t dfmi_context_set_timing(dfmi_context* c, int32_t enable) {
+    if (!c) return DFMI_ERR_INVALID_ARGUMENT;
+    c->timing = enable != 0;
+    return DFMI_OK;
+}
+
 extern "C" int32_t dfmi_last_timing(const dfmi_context* c, double* total_ms, double* main_ms) {
     if (!c || !c->timed) return DFMI_ERR_INVALID_ARGUMENT;
     if (total_ms) *total_ms = c->last_total_ms;
@@ -310,12 +324,24 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                                        dfmi_error* err) {
     set_err(err, DFMI_OK, "");
     if (ctx) ctx->last_err_key = ~0ull;
+    // DFMI_DIAG + DFMI_CALL_PROFILE: per-phase host time of this entry point,
+    // averaged over 1000 calls on stderr (diagnostics only)
+    static thread_local double ph[6];
+    static thread_local long ncalls;
+    static const bool prof = getenv("DFMI_DIAG") && getenv("DFMI_CALL_PROFILE");
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    auto tms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+    };
+    auto t_a = tnow();
     try {
         if (!ctx || !in || (np > 0 && !projs) || !outs || (in->num_columns > 0 && !in->columns))
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
         Built B;
         build_plan(pred, projs, np, in, outs, flags, B);
+        auto t_b = tnow();
+        if (prof) ph[0] += tms(t_a, t_b);
         Err& se = B.se;
         jit::Plan& plan = B.plan;
         jit::Launch& X = B.X;
@@ -342,6 +368,8 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 if (se.set) throw Fail{se.code, se.msg};  // the reference fails first
                 throw;
             }
+            auto t_c = tnow();
+            if (prof) ph[1] += tms(t_b, t_c);
             const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
             const size_t status_bytes = (size_t)n_chan * n_tiles * 8 * X.spread;
             // filtered outputs written as one byte per row and packed into a
@@ -404,21 +432,28 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             A.clear_words = ws.clear_words;
             A.clear_hdr = (unsigned long long*)ws.clear_hdr;
             A.mode = 0;
-            if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
+            if (getenv("DFMI_DIAG"))
+                if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
             const unsigned grid = (unsigned)n_tiles;  // one block per tile
-            HIP_TRY(hipEventRecord(ctx->ev0, st));
+            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
             size_t asz = sizeof A;
             void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
             HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
             ws_commit(ctx, ws);
-            HIP_TRY(hipEventRecord(ctx->ev1, st));
+            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
             for (int o = 0; o < nout; ++o)
                 if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
             for (int o : valid_out)
                 HIP_TRY(launch_pack_bools(A.out_valid[o], outs[o].validity, A.totals, n, st));
+            auto t_d = tnow();
+            if (prof) ph[2] += tms(t_c, t_d);
+            auto t_e = tnow();
+            if (prof) ph[3] += tms(t_d, t_e);
             HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipEventRecord(ctx->ev2, st));
+            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev2, st));
             HIP_TRY(hipStreamSynchronize(st));
+            auto t_f = tnow();
+            if (prof) ph[4] += tms(t_e, t_f);
             uint64_t ew;
             memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
             if (ew) {
@@ -432,12 +467,24 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 fprintf(stderr, "dfmi look-back: tiles %lld polls %llu sleeps %llu wait %.3f ms (summed over tiles)\n",
                         (long long)n_tiles, (unsigned long long)st3[0], (unsigned long long)st3[1], st3[2] * 1e-5);
             }
-            float m1 = 0, m2 = 0;
-            (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
-            (void)hipEventElapsedTime(&m2, ctx->ev0, ctx->ev2);
-            ctx->last_main_ms = m1;
-            ctx->last_total_ms = m2;
-            ctx->timed = true;
+            if (ctx->timing) {
+                float m1 = 0, m2 = 0;
+                (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
+                (void)hipEventElapsedTime(&m2, ctx->ev0, ctx->ev2);
+                ctx->last_main_ms = m1;
+                ctx->last_total_ms = m2;
+                ctx->timed = true;
+            }
+            if (prof) {
+                ph[5] += tms(t_f, tnow());
+                if (++ncalls % 1000 == 0)
+                    fprintf(stderr,
+                            "dfmi call (us, mean of 1000): plan %.2f, kernel lookup %.2f, launch %.2f, header "
+                            "copy %.2f, sync %.2f, timing %.2f\n",
+                            ph[0] / 1000, ph[1] / 1000, ph[2] / 1000, ph[3] / 1000, ph[4] / 1000, ph[5] / 1000);
+                if (ncalls % 1000 == 0)
+                    for (double& x : ph) x = 0;
+            }
         }
 
         // ---- errors: the reference raises the first in evaluation order

@@ -34,6 +34,7 @@ struct dfmi_context {
     uint8_t* scratch = nullptr;  // Boolean output bytes (filtered)
     size_t scratch_bytes = 0;
     uint8_t* host_hdr = nullptr; // pinned copy of the header
+    bool timing = true;  // record HIP events around launches (dfmi_context_set_timing)
     void* host_arena = nullptr;  // host_batch.cpp's staging arena (per context: no shared state)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_total_ms = 0, last_main_ms = 0, last_compile_ms = 0;

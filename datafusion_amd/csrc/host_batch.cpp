@@ -409,7 +409,7 @@ struct Arena {
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
     hipStream_t h2d = nullptr, d2h = nullptr;
-    hipEvent_t h2d_done[kSlots] = {}, d2h_done[kSlots] = {};
+    hipEvent_t h2d_done[kSlots] = {}, d2h_done[kSlots] = {}, kdone[kSlots] = {};
     bool slot_used[kSlots] = {};
     Pool* pool = nullptr;
     std::shared_ptr<dfmi_host::PinnedPool> results = std::make_shared<dfmi_host::PinnedPool>();
@@ -421,6 +421,7 @@ struct Arena {
         for (int s = 0; s < kSlots; ++s) {
             HIP_TRY(hipEventCreateWithFlags(&h2d_done[s], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&d2h_done[s], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&kdone[s], hipEventDisableTiming));
         }
         pool = new Pool(host_threads() - 1);
     }
@@ -448,6 +449,7 @@ struct Arena {
         for (int s = 0; s < kSlots; ++s) {
             if (h2d_done[s]) (void)hipEventDestroy(h2d_done[s]);
             if (d2h_done[s]) (void)hipEventDestroy(d2h_done[s]);
+            if (kdone[s]) (void)hipEventDestroy(kdone[s]);
         }
         if (h2d) (void)hipStreamDestroy(h2d);
         if (d2h) (void)hipStreamDestroy(d2h);
@@ -807,6 +809,8 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
         auto issue_h2d = [&](int k) {
             const int s = k % kSlots;
             const InPlan& P = inplans[k];
+            // the slot's inputs were read by the kernel of chunk k - kSlots
+            if (A.slot_used[s]) HIP_TRY(hipStreamWaitEvent(A.h2d, A.kdone[s], 0));
             if (P.staged_bytes)
                 HIP_TRY(hipMemcpyAsync(dev_in(s), pin_in(s), P.staged_bytes, hipMemcpyHostToDevice, A.h2d));
             for (const Buf& b : P.bufs)
@@ -877,6 +881,10 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
                 failed = true;
                 return;
             }
+            // the D2H of these results (and the slot's next H2D) run on other
+            // streams: they wait for the kernel on the device, not the host
+            HIP_TRY(hipEventRecord(A.kdone[s], st));
+            HIP_TRY(hipStreamWaitEvent(A.d2h, A.kdone[s], 0));
             D.row_base = rows_so_far;
             D.byte_base.assign(nout, 0);
             int64_t L = 0;

@@ -279,6 +279,10 @@ int32_t dfmi_host_free(void* ptr);
 int32_t dfmi_host_register(void* ptr, size_t bytes, dfmi_error* err);
 int32_t dfmi_host_unregister(void* ptr);
 
+/* HIP events around each launch (default on): dfmi_last_timing needs them;
+ * off saves two event records per call on the small-batch path. */
+int32_t dfmi_context_set_timing(dfmi_context* ctx, int32_t enable);
+
 /* Device time in milliseconds of the last dfmi_filter_project's kernels
  * (HIP events on the context stream), and the dominant kernel's share. */
 int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main_kernel_ms);

@@ -53,6 +53,7 @@ def main():
     for var in variants:
         env = {}
         if var != "-":
+            env["DFMI_DIAG"] = "1"  # the library reads its diagnostic knobs only then
             for kv in var.split(","):
                 k, v = kv.split("=", 1)
                 env[k] = v

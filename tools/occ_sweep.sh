@@ -1,6 +1,7 @@
 #!/bin/bash
 # Occupancy-hint sweep (diagnostics): C2 sweep + C3 at DFMI_WAVES_PER_EU=0/8.
 set -o pipefail
+export DFMI_DIAG=1  # the library reads its diagnostic knobs only then
 mkdir -p gpurun_out
 for W in 0 8; do
   DFMI_WAVES_PER_EU=$W timeout -k 10 240 python bench.py --steps 10 --warmup 2 --no-cpu --extra c3,c4 > gpurun_out/occ_w$W.json 2> gpurun_out/occ_w$W.err || exit 1

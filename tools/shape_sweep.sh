@@ -1,6 +1,7 @@
 #!/bin/bash
 # Tile-shape sweep (diagnostics): C2 s=0.5 + C3 at (BLOCK, K) pairs.
 set -o pipefail
+export DFMI_DIAG=1  # the library reads its diagnostic knobs only then
 mkdir -p gpurun_out
 for BK in 512:8 256:8 256:16; do
   B=${BK%:*}; K=${BK#*:}
