@@ -18,7 +18,7 @@
 // as Rust's str::parse (decimal; inf / infinity / nan words), anything else
 // is ArrowError(ParseError) "Error while parsing value <field>".
 #include <fcntl.h>
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
