@@ -72,10 +72,12 @@ def run_both(schema, batch, pred, projs, flags=0):
         except ExecutionError as e:
             host_err = e
         if batch.num_rows() > HOST_CHUNK:
-            # ... and again cut into HOST_CHUNK-row pipelined chunks: the same
-            # result or the same first error (evaluation order over all rows)
+            # ... and again cut into pipelined chunks (HOST_CHUNK rows, or ~16
+            # chunks for big batches): the same result or the same first error
+            # (evaluation order over all rows)
+            chunk = max(HOST_CHUNK, (batch.num_rows() // 16) // 512 * 512)
             prev = os.environ.get("DFMI_HOST_CHUNK_ROWS")
-            os.environ["DFMI_HOST_CHUNK_ROWS"] = str(HOST_CHUNK)
+            os.environ["DFMI_HOST_CHUNK_ROWS"] = str(chunk)
             try:
                 try:
                     chunked = engine().filter_project_host(p, cp, batch, flags)

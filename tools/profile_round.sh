@@ -9,7 +9,7 @@ TAG=${1:-rNN}
 R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --durations=15 --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
