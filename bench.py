@@ -78,7 +78,7 @@ class FusedStep:
         return self.outs[0].length
 
 
-PROFILE_TAG = "profiles/r02"
+PROFILE_TAG = "profiles/r02_final"
 PROFILE_DIR = os.path.join(ROOT, PROFILE_TAG)
 
 
