@@ -355,7 +355,9 @@ struct dfmi_csv_reader {
         }
         // row ranges of whole 64-row words per thread (bitmap words are never shared)
         const int64_t words = (n + 63) / 64;
-        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, words));
+        // a thread per >= 16 Ki rows: csv_sql.rs:49's 1024-row batches parse on one
+        // thread (starting threads would cost more than the parse)
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, std::min<int64_t>(words, n / 16384 + 1)));
         std::vector<int64_t> nulls((size_t)nt * std::max(1, nc), 0);
         // a parse error: arrow's reader builds the batch column by column, so
         // the one it reports is the first failing row of the first failing column
