@@ -36,6 +36,15 @@ from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Float64, Li
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md "Chip-level parameters"
 SEED = 42
+# DFMI_BENCH_BACKEND=gloo: rehearsal of the --gpus N path with N ranks sharing
+# the visible GPUs (rank -> GPU local_rank % count) and the collectives over
+# gloo on host tensors. Timings of such a run are not a scaling measurement.
+BACKEND = os.environ.get("DFMI_BENCH_BACKEND", "nccl")
+
+
+def coll_device(dev):
+    """Where collective tensors live: the GPU under RCCL, the host under gloo."""
+    return dev if BACKEND == "nccl" else torch.device("cpu")
 
 
 def query(sel):
@@ -141,7 +150,7 @@ def timed_steps(step, steps, warmup, dist, eng, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        tt = torch.tensor([el], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = tt.item()
     return el, float(np.mean(kern_ms)), selected
@@ -293,7 +302,7 @@ def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
         st.reset()
         st.add(pred, batch, flags)
         if dist:
-            mine = torch.frombuffer(bytearray(st.partial()), dtype=torch.uint8).to(dev)
+            mine = torch.frombuffer(bytearray(st.partial()), dtype=torch.uint8).to(coll_device(dev))
             parts = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(parts, mine)
             v = merge_agg_partials([agg], [p.cpu().numpy().tobytes() for p in parts])[0]
@@ -650,12 +659,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if BACKEND != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(BACKEND)
 
     n = int(args.rows)
     eng = engine(dev)
@@ -726,7 +740,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic (splitmix64 seed 42, generated in HBM)",
         "config": {"workload": "C2: 1e9-row Float64 a,b,c per GPU; s=%.2f" % args.sel, "rows_per_gpu": n,
-                   "selectivity": round(h["s"], 4), "parallelism": "row-range shards, RCCL count all_gather"},
+                   "selectivity": round(h["s"], 4), "parallelism": "row-range shards, RCCL count all_gather"
+                   if BACKEND == "nccl" else "row-range shards, %s rehearsal on shared GPUs" % BACKEND},
         "roofline": {"bound": "hbm", "achieved": round(h["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(h["achieved"] / HBM_PEAK_GBS, 4),
                      "traffic": traffic,

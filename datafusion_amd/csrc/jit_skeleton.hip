@@ -418,7 +418,7 @@ __device__ u64 lb_resolve(u64* st, unsigned tile, u64 agg, int lane, u64* err, u
     i64 j = (i64)tile - 1;  // highest predecessor not yet accounted for
     const u64 t_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     u64 t0 = t_start;  // last progress: the timeout is time WITHOUT progress
-    unsigned polls = 0, sleeps = 0;
+    unsigned polls = 0, sleeps = 0, idle = 0;  // idle: stalled polls since the last progress
     while (true) {
         ++polls;
         const i64 j_before = j;
@@ -458,9 +458,12 @@ __device__ u64 lb_resolve(u64* st, unsigned tile, u64 agg, int lane, u64* err, u
             const u64 now = __builtin_amdgcn_s_memrealtime();
             if (j != j_before) {
                 t0 = now;  // predecessors resolved this round: progress
-            } else if (now - t0 > 200000000ull) {
-                // 2 s without a single predecessor resolving (a preempted or
-                // time-sliced GPU is far below this): report, do not hang
+                idle = 0;
+            } else if (++idle > 200000u && now - t0 > 200000000ull) {
+                // 2 s and 200k polls without a single predecessor resolving:
+                // report, do not hang. Both bounds: a queue time-sliced off the
+                // GPU (processes sharing it) sees the clock jump while its
+                // waves are saved, but polls nothing meanwhile.
                 if (lane == 0) report_err(err, 0, 0, ERRK_LOOKBACK_TIMEOUT);
                 break;
             }
