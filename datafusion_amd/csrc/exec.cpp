@@ -26,6 +26,9 @@
 namespace dfmi {
 hipError_t launch_pack_bools(const uint8_t* bytes, uint8_t* bits, const unsigned long long* count,
                              long long max_rows, hipStream_t st);
+hipError_t launch_utf8_copy_rows(const int32_t* offs, const int32_t* spos, const uint8_t* src, uint8_t* out,
+                                 const unsigned long long* totals, int chan, long long cap, long long max_rows,
+                                 hipStream_t st);
 }  // namespace dfmi
 
 using namespace dfmi;
@@ -217,7 +220,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;
-        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 3;  // 2 = serial
+        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 4;  // 2 = serial, 3 = two-pass
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
     }
     // a numeric predicate's tiles are VGPR-limited (3 blocks/CU): LDS has room
@@ -280,6 +283,7 @@ extern "C" void dfmi_context_destroy(dfmi_context* c) {
     dfmi::host_arena_release(c);
     if (c->ws) (void)hipFree(c->ws);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->utf8_src) (void)hipFree(c->utf8_src);
     if (c->host_hdr) (void)hipHostFree(c->host_hdr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -385,6 +389,9 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             const size_t row_bytes = (size_t)((n + 63) & ~63ll);
             if (!bool_out.empty() || !valid_out.empty())
                 ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, (bool_out.size() + valid_out.size()) * row_bytes);
+            const bool two_pass = pred && X.gather == 3 && !X.utf8_outs.empty();
+            const size_t src_bytes = ((size_t)n * 4 + 255) & ~(size_t)255;  // one i32 source start per row
+            if (two_pass) ensure(ctx, &ctx->utf8_src, &ctx->utf8_src_bytes, X.utf8_outs.size() * src_bytes);
             A.n_rows = n;
             A.n_tiles = (int)n_tiles;
             for (size_t s = 0; s < X.num_cols.size(); ++s) {
@@ -411,6 +418,9 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                 A.out_data[o] = outs[o].data;
                 A.out_cap[o] = outs[o].data_capacity;
             }
+            if (two_pass)
+                for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                    A.out_src[X.utf8_outs[j].first] = (int*)(ctx->utf8_src + j * src_bytes);
             for (size_t i = 0; i < bool_out.size(); ++i) {
                 bool_dst[bool_out[i]] = (uint8_t*)outs[bool_out[i]].values;
                 A.out[bool_out[i]] = ctx->scratch + i * row_bytes;
@@ -440,6 +450,12 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
             HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
             ws_commit(ctx, ws);
+            if (two_pass && !(A.mode & 8))
+                for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+                    const int o = X.utf8_outs[j].first;
+                    HIP_TRY(launch_utf8_copy_rows(A.out_offs[o], A.out_src[o], A.bytes[X.utf8_outs[j].second],
+                                                  A.out_data[o], A.totals, 1 + (int)j, A.out_cap[o], n, st));
+                }
             if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
             for (int o = 0; o < nout; ++o)
                 if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));

@@ -33,6 +33,8 @@ struct dfmi_context {
     bool ws_valid = false;       // the invariant above holds (else re-zero everything)
     uint8_t* scratch = nullptr;  // Boolean output bytes (filtered)
     size_t scratch_bytes = 0;
+    uint8_t* utf8_src = nullptr;  // two-pass Utf8 gather: source start per selected row
+    size_t utf8_src_bytes = 0;
     uint8_t* host_hdr = nullptr; // pinned copy of the header
     bool timing = true;  // record HIP events around launches (dfmi_context_set_timing)
     void* host_arena = nullptr;  // host_batch.cpp's staging arena (per context: no shared state)

@@ -617,7 +617,11 @@ std::string generate(const Plan& P, Launch& X) {
             if (!X.utf8_outs.empty()) o << "  if (!(A.mode & 8)) {  // mode bit 3: skip the byte copies (diagnostics)\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
                 const int u = X.utf8_outs[j].second;
-                if (X.gather == 0)
+                if (X.gather == 3)
+                    o << "  dfmi::utf8_offsets_src<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", "
+                      << X.utf8_outs[j].first << ", selm, wm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
+                      << ", lane, wave);\n";
+                else if (X.gather == 0)
                     o << "  dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << u << ", "
                       << X.utf8_outs[j].first << ", selm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
                       << ", lane, wave);\n";
@@ -643,7 +647,7 @@ std::string generate(const Plan& P, Launch& X) {
             // one tile per block in dispatch order (in order per XCD, so every
             // tile a block waits on in the look-back is running or done)
             o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
-            if (!X.utf8_outs.empty() && X.gather)
+            if (!X.utf8_outs.empty() && X.gather && X.gather != 3)
                 o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA> G[WAVES];\n";
             o << "  const unsigned t = blockIdx.x;\n";
             emit_decls(o, X.pred_slots, X, "", true);

@@ -58,7 +58,8 @@ struct Launch {
     int window = 8;
     int late_proj = 0;  // projection-only columns loaded after the look-back (byte-light predicates)
     int gather = 1;  // Utf8 gather: 1 = wave-cooperative, consecutive slices staged together;
-                     // 2 = one slice per round trip, 0 = per-lane copy (diagnostics)
+                     // 2 = one slice per round trip, 0 = per-lane copy (diagnostics);
+                     // 3 = two passes: offsets + source starts, then k_utf8_copy_rows
     int arena = 128; // Utf8 gather staging arena per wave, 16-byte chunks
     // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores
     int nt = 0;

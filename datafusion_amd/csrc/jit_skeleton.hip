@@ -44,6 +44,7 @@ struct Args {
     int* out_offs[kArgOut];            // Utf8 outputs
     u8* out_data[kArgOut];
     i64 out_cap[kArgOut];
+    int* out_src[kArgOut];             // two-pass Utf8 gather: source start of each selected row
     u64 lits[kArgLits];
     int str_off[8];
     int str_len[8];
@@ -947,6 +948,34 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
             }
         }
         wave_lds_fence();
+    }
+}
+
+// Two-pass Utf8 gather, first pass (Launch::gather == 3): the rebased output
+// offset and the source start of each selected row of Utf8 input u; the
+// library's k_utf8_copy_rows (kernels.hip) then copies the bytes as a dense
+// pass over the compacted rows -- lanes on consecutive output words, no
+// per-string loops in the query kernel.
+template <int BLOCK, int K, int NCH>
+__device__ __forceinline__ void utf8_offsets_src(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int o,
+                                                 unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
+                                                 const int (&s)[K], const int (&nx)[K], int lane, int wave) {
+    constexpr int WAVES = BLOCK / 64;
+    const u64 bpre = T.prefix[ch];
+    const i64 obase = (i64)T.prefix[0];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (!wm[k]) continue;
+        const bool sel = (selm >> k) & 1;
+        const int e = utf8_end(s[k], nx[k], lane);  // every lane (DPP)
+        const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
+        const unsigned incl = wave_incl_scan32(L, lane);
+        const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
+        if (sel) {
+            A.out_offs[o][obase + dst[k]] = (int)(ob0 + incl - L);
+            A.out_src[o][obase + dst[k]] = s[k];
+        }
+        if (lane == 63 && (i64)(ob0 + incl) > A.out_cap[o]) report_err(A.err, 0, 0, ERRK_CAPACITY);
     }
 }
 

@@ -375,6 +375,19 @@ def test_utf8_multi_channel_many_tiles():
         run_both(s, b, BinaryExpr(Column(c), Operator.NotEq, Literal(Utf8(w))), [Column(c)], DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
+@pytest.mark.parametrize("variant", ["3", "2", "0"])
+def test_utf8_gather_variants(monkeypatch, variant):
+    """The diagnostic Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG:
+    3 = two passes -- offsets + source starts in the query kernel, bytes by
+    k_utf8_copy_rows --, 2 = one staged slice per round trip, 0 = per-lane
+    copy) against the oracle on the Utf8 parity cases above."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_UTF8_GATHER", variant)
+    test_utf8_gather_and_equality()
+    test_utf8_many_tiles()
+    test_utf8_multi_channel_many_tiles()
+
+
 def test_host_batch_many_staging_chunks():
     """dfmi_filter_project_host over a batch larger than the two 64 MB pinned
     staging chunks (H2D 20 chunks, D2H 10 per output): identical to the
