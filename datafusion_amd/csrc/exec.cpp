@@ -441,6 +441,10 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             A.clear_status = (unsigned long long*)ws.clear_status;
             A.clear_words = ws.clear_words;
             A.clear_hdr = (unsigned long long*)ws.clear_hdr;
+            // one block: the kernel writes the header into host_hdr itself (no D2H copy)
+            const bool hdr_direct = n_tiles == 1;
+            A.hdr = (const unsigned long long*)hdr;
+            A.host_hdr = hdr_direct ? (unsigned long long*)ctx->host_hdr : nullptr;
             A.mode = 0;
             if (getenv("DFMI_DIAG"))
                 if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
@@ -465,7 +469,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             if (prof) ph[2] += tms(t_c, t_d);
             auto t_e = tnow();
             if (prof) ph[3] += tms(t_d, t_e);
-            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
+            if (!hdr_direct) HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
             if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev2, st));
             HIP_TRY(hipStreamSynchronize(st));
             auto t_f = tnow();

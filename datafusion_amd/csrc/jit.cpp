@@ -690,7 +690,7 @@ std::string generate(const Plan& P, Launch& X) {
                 o << "  if (lane == 0 && nulls[" << oi << "]) atomicAdd(&A.totals[8 + " << oi << "], (u64)nulls[" << oi
                   << "]);\n";
     }
-    o << "}\n";
+    o << "  dfmi::publish_header<BLOCK>(A, tid);\n}\n";
     return std::string(dfmi_skeleton_src) + o.str();
 }
 
