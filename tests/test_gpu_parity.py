@@ -385,7 +385,8 @@ def test_utf8_gather_variants(monkeypatch, variant):
     monkeypatch.setenv("DFMI_UTF8_GATHER", variant)
     test_utf8_gather_and_equality()
     test_utf8_many_tiles()
-    test_utf8_multi_channel_many_tiles()
+    if variant == "3":  # the default path's per-lane fallback is what 0 runs; 2 differs only in staging
+        test_utf8_multi_channel_many_tiles()
 
 
 def test_host_batch_many_staging_chunks():
