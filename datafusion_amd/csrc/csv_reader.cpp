@@ -281,7 +281,6 @@ struct dfmi_csv_reader {
     void index_records(bool has_header) {
         const char* p = data;
         const char* end = data + size;
-        const bool quotes = memchr(data, '"', size) != nullptr;
         auto add = [&](const char* b, const char* e) {
             if (e > b && e[-1] == '\r') --e;
             if (e > b) {  // empty records are skipped
@@ -289,12 +288,44 @@ struct dfmi_csv_reader {
                 rec_e.push_back((uint64_t)(e - data));
             }
         };
-        if (!quotes) {
-            while (p < end) {
-                const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+        // Without quote characters records are lines: host threads index
+        // the lines starting in their share of the file (and look for quotes
+        // on the way); any quote falls back to the sequential state machine.
+        const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, size / ((size_t)4 << 20) + 1));
+        std::vector<std::vector<uint64_t>> lb(nt), le(nt);
+        std::vector<char> quoted(nt, 0);
+        auto index_share = [&](int t) {
+            const char* c0 = data + size / nt * t;
+            const char* c1 = t + 1 == nt ? end : data + size / nt * (t + 1);
+            quoted[t] = memchr(c0, '"', (size_t)(c1 - c0)) != nullptr;
+            if (quoted[t]) return;
+            const char* q = c0;
+            if (t > 0 && c0[-1] != '\n') {  // the line in progress belongs to the share before
+                const char* nl = (const char*)memchr(c0, '\n', (size_t)(end - c0));
+                q = nl ? nl + 1 : end;
+            }
+            while (q < c1) {
+                const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
                 const char* e = nl ? nl : end;
-                add(p, e);
-                p = nl ? nl + 1 : end;
+                const char* e2 = (e > q && e[-1] == '\r') ? e - 1 : e;
+                if (e2 > q) {  // empty records are skipped
+                    lb[t].push_back((uint64_t)(q - data));
+                    le[t].push_back((uint64_t)(e2 - data));
+                }
+                q = nl ? nl + 1 : end;
+            }
+        };
+        run(nt, index_share);
+        bool quotes = false;
+        for (char x : quoted) quotes = quotes || x;
+        if (!quotes) {
+            size_t total = 0;
+            for (int t = 0; t < nt; ++t) total += lb[t].size();
+            rec_b.reserve(total);
+            rec_e.reserve(total);
+            for (int t = 0; t < nt; ++t) {
+                rec_b.insert(rec_b.end(), lb[t].begin(), lb[t].end());
+                rec_e.insert(rec_e.end(), le[t].begin(), le[t].end());
             }
         } else {
             // a quote opens a quoted field only at the field's start; inside

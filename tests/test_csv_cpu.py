@@ -118,6 +118,34 @@ def test_no_quotes_fast_index(tmp_path):
     assert np.array_equal(np.concatenate(got), a)
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_no_quotes_parallel_index(tmp_path, threads):
+    """A quote-free file over 4 MiB is indexed by several host threads, each
+    taking the lines that start in its share: lines of every length across the
+    share boundaries, CRLF and LF endings, empty lines, no final newline."""
+    rng = np.random.default_rng(threads)
+    n = 400_000
+    a = rng.standard_normal(n) * 10.0 ** rng.integers(-3, 12, n)
+    b = rng.integers(-(1 << 62), 1 << 62, n)
+    ends = rng.choice(["\n", "\r\n", "\n\n", "\r\n\n"], n, p=[0.7, 0.2, 0.05, 0.05])
+    text = "a,b\n" + "".join("%r,%d%s" % (float(x), int(y), e) for x, y, e in zip(a, b, ends))
+    p = tmp_path / "nqp.csv"
+    p.write_text(text.rstrip("\r\n"))
+    assert p.stat().st_size > 3 * (4 << 20)
+    schema = Schema([Field("a", DataType.Float64, False), Field("b", DataType.Int64, False)])
+    src = NativeCsvDataSource(schema, str(p), True, 1 << 16, threads=threads)
+    assert src.num_records() == n
+    ga, gb = [], []
+    while True:
+        bt = src.next()
+        if bt is None:
+            break
+        ga.append(bt.columns[0].numpy_values().copy())
+        gb.append(bt.columns[1].numpy_values().copy())
+    assert np.array_equal(np.concatenate(ga), a)
+    assert np.array_equal(np.concatenate(gb), b)
+
+
 def test_parse_errors_in_reference_order(tmp_path):
     """arrow builds a batch column by column: the first failing column's first
     bad row is the error, even when a later column fails on an earlier row."""
