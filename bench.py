@@ -320,7 +320,7 @@ def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
     dv = g.finish()[0]
     rv = oracle_aggregate(schema, pre.to("cpu"), pred_e, [sum_e], flags)[0]
     gate = {"rows": m, "sum_bits_equal": bool(dv.bits == rv.bits and dv.count == rv.count), "count": int(rv.count)}
-    s = selected / n
+    s = selected / (n * world)  # the merged count covers every rank's rows
     bpr = 32.0  # 4 Float64 inputs; the output is one value
     ach = n * bpr / (kms * 1e-3) / 1e9
     v = res["v"]

@@ -126,3 +126,32 @@ def test_c3_full_batch_against_torch():
         assert torch.equal(gb[want_offs[r0]:want_offs[r1]], want), (r0, r1)
     del got, s, v
     torch.cuda.empty_cache()
+
+
+def test_q6_full_size_exact_sum():
+    """Real Q6 (DFMI_FLAG_EXT_AGGREGATE) over 600,037,902 rows: the device SUM
+    of extendedprice*discount over the selected rows is the correctly rounded
+    exact sum of the rounded products (math.fsum), and its count is the mask's."""
+    import math
+    import numpy as np
+    from datafusion_amd.execution.expression import compile_expr
+    from datafusion_amd.logicalplan import AggregateFunction
+    dev = torch.device("cuda", 0)
+    eng = engine(dev)
+    flags = _abi.DFMI_FLAG_EXT_AGGREGATE
+    n = bench.Q6_ROWS
+    schema, cols = bench.q6_table(dev, n, bench.SEED)
+    pred_e, proj_e = bench.q6_query()
+    agg = compile_expr(None, AggregateFunction("SUM", (proj_e[0],), DataType.Float64), schema, flags)
+    st = eng.agg_state([agg])
+    st.add(compile_scalar_expr(None, pred_e, schema, flags),
+           RecordBatch(schema, [Array(DataType.Float64, n, c.view(torch.uint8)) for c in cols]), flags)
+    v = st.finish()[0]
+    qty, price, disc, ship = cols
+    mask = (ship >= 8766.0) & (ship < 9131.0) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24.0)
+    prods = (price[mask] * disc[mask]).cpu().numpy()
+    assert v.count == prods.size
+    want = math.fsum(prods.tolist())
+    assert v.bits == int(np.array([want], dtype=np.float64).view(np.uint64)[0])
+    del cols, mask
+    torch.cuda.empty_cache()
