@@ -239,6 +239,9 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
 
     B.n_tiles = n_tiles;
+    // a single-tile launch publishes its header itself (its own kernel
+    // variant: the copy code stays out of the multi-tile kernels)
+    X.publish = n_tiles == 1;
 }
 
 }  // namespace
@@ -442,7 +445,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             A.clear_words = ws.clear_words;
             A.clear_hdr = (unsigned long long*)ws.clear_hdr;
             // one block: the kernel writes the header into host_hdr itself (no D2H copy)
-            const bool hdr_direct = n_tiles == 1;
+            const bool hdr_direct = X.publish;
             A.hdr = (const unsigned long long*)hdr;
             A.host_hdr = hdr_direct ? (unsigned long long*)ctx->host_hdr : nullptr;
             A.mode = 0;
