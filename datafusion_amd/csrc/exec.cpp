@@ -239,9 +239,6 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
 
     B.n_tiles = n_tiles;
-    // a single-tile launch publishes its header itself (its own kernel
-    // variant: the copy code stays out of the multi-tile kernels)
-    X.publish = n_tiles == 1;
 }
 
 }  // namespace
@@ -444,10 +441,6 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             A.clear_status = (unsigned long long*)ws.clear_status;
             A.clear_words = ws.clear_words;
             A.clear_hdr = (unsigned long long*)ws.clear_hdr;
-            // one block: the kernel writes the header into host_hdr itself (no D2H copy)
-            const bool hdr_direct = X.publish;
-            A.hdr = (const unsigned long long*)hdr;
-            A.host_hdr = hdr_direct ? (unsigned long long*)ctx->host_hdr : nullptr;
             A.mode = 0;
             if (getenv("DFMI_DIAG"))
                 if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
@@ -472,7 +465,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             if (prof) ph[2] += tms(t_c, t_d);
             auto t_e = tnow();
             if (prof) ph[3] += tms(t_d, t_e);
-            if (!hdr_direct) HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
             if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev2, st));
             HIP_TRY(hipStreamSynchronize(st));
             auto t_f = tnow();

@@ -690,7 +690,6 @@ std::string generate(const Plan& P, Launch& X) {
                 o << "  if (lane == 0 && nulls[" << oi << "]) atomicAdd(&A.totals[8 + " << oi << "], (u64)nulls[" << oi
                   << "]);\n";
     }
-    if (X.publish) o << "  dfmi::publish_header<BLOCK>(A, tid);\n";
     o << "}\n";
     return std::string(dfmi_skeleton_src) + o.str();
 }
@@ -736,7 +735,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, os.out_type);
         put(k, (char)os.nullable);
     }
-    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather, X.late_proj, X.arena, X.publish};
+    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather, X.late_proj, X.arena};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

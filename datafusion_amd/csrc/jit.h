@@ -57,7 +57,6 @@ struct Launch {
     // (64 cost ~9% of the C2 kernel in polling traffic)
     int window = 8;
     int late_proj = 0;  // projection-only columns loaded after the look-back (byte-light predicates)
-    int publish = 0;    // single-tile launch: the block copies the header to host memory (publish_header)
     int gather = 1;  // Utf8 gather: 1 = wave-cooperative, consecutive slices staged together;
                      // 2 = one slice per round trip, 0 = per-lane copy (diagnostics);
                      // 3 = two passes: offsets + source starts, then k_utf8_copy_rows

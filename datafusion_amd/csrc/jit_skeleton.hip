@@ -61,21 +61,7 @@ struct Args {
     i64 clear_words;                   // ... [0, clear_words) to zero
     u64* clear_hdr;                    // previous launch's 512-byte header
     u64* agg;                          // aggregate extension: [copies][aggs][kAggWords] accumulators
-    const u64* hdr;                    // this launch's 512-byte device header (ticket, err, totals, stats)
-    u64* host_hdr;                     // single-tile launches: the context's pinned host header, else null
 };
-
-// Single-tile launches (n_tiles == 1, e.g. csv_sql.rs:49's 1024-row
-// batches): the one block is the whole launch, so after its last write it
-// copies the header (error word, totals, statistics) into the context's pinned
-// host header itself, and the host reads it after the stream synchronisation
-// instead of issuing a device-to-host copy per call.
-template <int BLOCK>
-__device__ __forceinline__ void publish_header(const Args& A, int tid) {
-    if (!A.host_hdr) return;  // kernel argument: uniform
-    __syncthreads();
-    if (tid < 64) A.host_hdr[tid] = __hip_atomic_load(A.hdr + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // This block's share of zeroing the previous launch's workspace.
 template <int BLOCK>

@@ -43,7 +43,6 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     dfmi::utf8_gather_serial<BLOCK, K, NCH, dfmi::kStageChunks>(A, T, 1, 0, 1, selm, wm, dst, us, ue, G[wave], lane, wave);
     dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, 1, 0, 1, selm, dst, us, ue, lane, wave);
     dfmi::utf8_offsets_src<BLOCK, K, NCH>(A, T, 1, 1, selm, wm, dst, us, ue, lane, wave);
-    dfmi::publish_header<BLOCK>(A, tid);
     const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0) &&
                    dfmi::utf8_eq_col(A, 0, 1, base) && dfmi::utf8_valid(A, 0, base);
     if (b) dfmi::report_err(A.err, 1, base, dfmi::ERRK_DIV_ZERO);
