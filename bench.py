@@ -57,9 +57,12 @@ def query(sel):
 
 
 class FusedStep:
-    """Pre-built C-ABI call: dfmi_filter_project over a resident batch."""
+    """Pre-built C-ABI call: dfmi_filter_project over a resident batch -- or,
+    with a ShardComm, dfmi_shard_filter_project: this rank's pass plus the
+    RCCL all_gather of placement records (the path a Rust caller of
+    Relation::next takes on each GPU, relation.rs:27-32)."""
 
-    def __init__(self, eng, schema, cols, n, pred_e, proj_e, outs):
+    def __init__(self, eng, schema, cols, n, pred_e, proj_e, outs, comm=None):
         self.eng = eng
         self.pred = compile_scalar_expr(None, pred_e, schema)
         self.projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
@@ -78,30 +81,67 @@ class FusedStep:
         self.no = no
         self.err = _abi.dfmi_error()
         self.L = _abi.lib()
+        self.comm = comm
+        self.place = _abi.dfmi_shard_placement()
 
     def __call__(self):
-        rc = self.L.dfmi_filter_project(self.eng.ctx, self.pred.handle, self.progs, self.no, C.byref(self.cb),
-                                        self.outs, 0, C.byref(self.err))
+        if self.comm is None:
+            rc = self.L.dfmi_filter_project(self.eng.ctx, self.pred.handle, self.progs, self.no, C.byref(self.cb),
+                                            self.outs, 0, C.byref(self.err))
+        else:
+            rc = self.L.dfmi_shard_filter_project(self.eng.ctx, self.comm.handle, self.pred.handle, self.progs,
+                                                  self.no, C.byref(self.cb), self.outs, 0, C.byref(self.place),
+                                                  C.byref(self.err))
+            self.comm.placement, self.comm.outputs = self.place, self.outs
         if rc != 0:
             raise RuntimeError(self.err.message.decode())
         return self.outs[0].length
 
 
-PROFILE_TAG = "profiles/r02_final"
+PROFILE_TAG = "profiles/r03"
 PROFILE_DIR = os.path.join(ROOT, PROFILE_TAG)
 
 
-def pmc_traffic(n, sel):
-    """HBM bytes per launch of the query kernel measured by the rocprofv3
-    FETCH_SIZE / WRITE_SIZE passes of tools/profile_round.sh on this
-    configuration (corrected by tools/traffic.py); None if not profiled."""
+def kernel_name(eng):
+    """The query kernel the context launched last (dfmi_<kind>_<hash>, as rocprofv3 names it)."""
+    return _abi.lib().dfmi_last_kernel_name(eng.ctx).decode()
+
+
+def profiled(kernel, run="main"):
+    """The committed rocprofv3 record of `kernel` (tools/profile_r03.sh: kernel
+    trace + separate FETCH_SIZE / WRITE_SIZE passes of the same bench command,
+    tools/traffic.py): the entry of its largest grid in PROFILE_DIR/<run>, or None."""
     try:
-        t = json.load(open(os.path.join(PROFILE_DIR, "traffic.json")))
+        t = json.load(open(os.path.join(PROFILE_DIR, run, "traffic.json")))
     except (OSError, ValueError):
         return None
-    if t.get("rows") != n or abs(t.get("selectivity", -1) - sel) > 1e-9:
-        return None
-    return t["traffic_bytes"]
+    hits = [e for e in t["kernels"] if e["kernel"] == kernel]
+    return max(hits, key=lambda e: e["grid"]) if hits else None
+
+
+def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
+    """roofline object of one bench line: ALGORITHMIC bytes per
+    launch over the kernel's average launch time from HIP events on the launch
+    stream, plus -- from the committed profile of the same command -- the
+    rocprofv3 average (its frac must agree) and the PMC HBM bytes."""
+    ach = alg_bytes / (kms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": kernel, "kernel_ms": round(kms, 4),
+         "launches_per_step": launches, "algorithmic_bytes_per_row": round(alg_bytes * launches / rows, 3),
+         "traffic": None}
+    p = profiled(kernel, run)
+    if p:
+        per_launch_alg = alg_bytes / launches
+        avg_ms = p["avg_ns"] * 1e-6
+        r["rocprof"] = {"source": "%s/%s/traffic.json" % (PROFILE_TAG, run), "avg_ms": round(avg_ms, 4),
+                        "launches": p["launches"], "frac": round(per_launch_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "vgpr": p["vgpr"], "sgpr": p["sgpr"], "scratch": p["scratch"], "lds": p["lds"]}
+        if "traffic_bytes" in p:
+            r["traffic"] = round(p["traffic_bytes"])
+            r["traffic_bytes_per_row"] = round(p["traffic_bytes"] * launches / rows, 3)
+            r["traffic_gbs"] = round(p["traffic_bytes"] / (avg_ms * 1e-3) / 1e9, 1)
+            r["traffic_frac"] = round(r["traffic_gbs"] / HBM_PEAK_GBS, 4)
+    return r
 
 
 def cpu_baseline(sel, budget_s=12.0):
@@ -128,9 +168,10 @@ def cpu_baseline(sel, budget_s=12.0):
                       % (n, SEED, sel, rows, t)}
 
 
-def timed_steps(step, steps, warmup, dist, eng, dev):
+def timed_steps(step, steps, warmup, dist, eng, dev, py_exchange=True):
     """W untimed + K timed steps between barrier + synchronize; per step the
-    RCCL count exchange of the sharded path. Returns (max-over-ranks wall s,
+    count exchange of the sharded path (inside the step on the C-ABI path,
+    else torch.distributed's all_gather here). Returns (max-over-ranks wall s,
     mean kernel ms, selected rows of the last step)."""
     for _ in range(warmup):
         step()
@@ -143,7 +184,7 @@ def timed_steps(step, steps, warmup, dist, eng, dev):
     for _ in range(steps):
         selected = step()
         kern_ms.append(eng.last_timing()[1])
-        if dist:  # per-GPU selected counts -> global output offsets
+        if dist and py_exchange:  # per-GPU selected counts -> global output offsets
             exchange_counts([selected])
     torch.cuda.synchronize(dev)
     if dist:
@@ -154,6 +195,96 @@ def timed_steps(step, steps, warmup, dist, eng, dev):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = tt.item()
     return el, float(np.mean(kern_ms)), selected
+
+
+def abi_comm(eng, dist, rank, world, dev):
+    """The C-ABI RCCL communicator (dfmi_shard_unique_id on rank 0, handed to
+    every rank out of band -- here a torch.distributed broadcast -- then
+    dfmi_shard_comm_init), as a Rust caller with one thread per GPU sets it up."""
+    from datafusion_amd.execution.engine import ShardComm
+    uid = ShardComm.unique_id() if rank == 0 else bytes(_abi.DFMI_SHARD_ID_BYTES)
+    if dist:
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=coll_device(dev))
+        dist.broadcast(t, 0)
+        uid = bytes(t.cpu().tolist())
+    return ShardComm(eng, world, rank, uid)
+
+
+def _checksum(t):
+    """Wrapping int64 sum of a buffer's 8-byte words (order-independent check)."""
+    return int(t.view(torch.int64).sum().item()) if t.numel() else 0
+
+
+def gather_line(eng, comm, schema, cols, n, sel, dist, rank, world, dev, root=0):
+    """SURVEY §8(e) / C5's "result gather over xGMI": one dfmi_shard_gather_to_root
+    of the C2 outputs (a, b, a*b+c at s=sel) of every rank onto `root`,
+    grouped ncclSend/ncclRecv posted at once, timed between barriers (max over
+    ranks). Reported apart from `value`: the leg is bound by the root's xGMI
+    ingress. Check: every rank's per-column checksum equals the checksum of
+    its segment of the gathered columns on the root."""
+    outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
+    step = FusedStep(eng, schema, cols, n, *query(sel), outs, comm=comm)
+    local_rows = step()
+    place = comm.placement
+    total = place.total_rows
+    need = 3 * total * 8
+    free = torch.cuda.mem_get_info(dev)[0] if rank == root else 0
+    ok = torch.tensor([1 if (rank != root or need + (4 << 30) < free) else 0], device=coll_device(dev))
+    if dist:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if not ok.item():
+        return {"skipped": "root lacks %.1f GB of free HBM for the gathered columns" % (need / 1e9)}
+    routs = (_abi.dfmi_out_column * 3)()
+    keep = []
+    if rank == root:
+        for j in range(3):
+            t = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
+            keep.append(t)
+            routs[j].values = t.data_ptr()
+    err = _abi.dfmi_error()
+    L = _abi.lib()
+    times = []
+    for it in range(3):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        rc = L.dfmi_shard_gather_to_root(eng.ctx, comm.handle, comm.outputs, routs, root, C.byref(err))
+        if rc != 0:
+            raise RuntimeError(err.message.decode())
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            tt = torch.tensor([el], dtype=torch.float64, device=coll_device(dev))
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+        times.append(el)
+    # checksums: each rank's outputs vs its segment on the root
+    mine = torch.tensor([_checksum(o[:local_rows]) for o in outs] + [local_rows], dtype=torch.int64,
+                        device=coll_device(dev))
+    allc = [torch.empty_like(mine) for _ in range(world)] if dist else [mine]
+    if dist:
+        dist.all_gather(allc, mine)
+    checks = None
+    if rank == root:
+        checks, r0 = True, 0
+        for r in range(world):
+            cs = allc[r].cpu().tolist()
+            rows = cs[3]
+            for j in range(3):
+                checks = checks and _checksum(keep[j][r0:r0 + rows]) == cs[j]
+            r0 += rows
+        checks = checks and r0 == total
+    el = min(times)
+    moved = (total - (local_rows if rank == root else 0)) * 24 if world > 1 else total * 24
+    del keep, outs, step
+    return {"workload": "gather C2 outputs (3 x Float64, s=%.2f) of %d rank(s) to rank %d" % (sel, world, root),
+            "rows": total, "bytes": total * 24, "ms": round(el * 1e3, 3),
+            "transfer": "xGMI (RCCL grouped send/recv)" if world > 1 else "local HBM copy (one rank: no xGMI)",
+            "bytes_into_root": moved, "gbs_into_root": round(moved / el / 1e9, 1),
+            "checksums_match": checks, "note": "not in value: results stay sharded by default (DESIGN.md §8)"}
 
 
 def batches_line(eng, schema, cols, sel, dev):
@@ -180,7 +311,8 @@ def batches_line(eng, schema, cols, sel, dev):
             step()
             kern += eng.last_timing()[1]
         us = el / calls * 1e6
-        out["%d_rows" % m] = {"us_per_batch": round(us, 2), "kernel_us": round(kern / 200 * 1e3, 2),
+        out["%d_rows" % m] = {"kernel": kernel_name(eng), "us_per_batch": round(us, 2),
+                              "kernel_us": round(kern / 200 * 1e3, 2),
                               "host_overhead_us": round(us - kern / 200 * 1e3, 2), "calls": calls,
                               "rows_per_s": m / (us * 1e-6)}
     # a new query shape: generate + hipRTC compile on the first call, cached after
@@ -249,7 +381,7 @@ def _popcount(bits, m):
 Q6_ROWS = 600_037_902  # TPC-H SF100 lineitem
 
 
-def q6_line(eng, dev, rank, world, steps, warmup, dist, rows):
+def q6_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
     """C4 (BASELINE.json configs[3]): Q6-style predicate over 4 Float64 columns,
     projecting extendedprice*discount (no aggregate: the reference has none).
     Inputs generated on the device with torch (seeded); parity of the query
@@ -259,24 +391,23 @@ def q6_line(eng, dev, rank, world, steps, warmup, dist, rows):
     pred, projs = q6_query()
     outs = [torch.empty(n, dtype=torch.float64, device=dev)]
     torch.cuda.synchronize(dev)
-    step = FusedStep(eng, schema, cols, n, pred, projs, outs)
-    el, kms, selected = timed_steps(step, steps, warmup, dist, eng, dev)
+    step = FusedStep(eng, schema, cols, n, pred, projs, outs, comm=comm)
+    el, kms, selected = timed_steps(step, steps, warmup, dist, eng, dev, py_exchange=comm is None)
+    kname = kernel_name(eng)
     del outs, step
     from datafusion_amd.arrow import Array
     gate = prefix_gate(eng, schema, [Array(DataType.Float64, n, c.view(torch.uint8)) for c in cols], 1 << 22,
                        pred, projs)
     s = selected / n
     bpr = 32.0 + 8.0 * s  # 4 Float64 inputs, s * 8 B output
-    ach = n * bpr / (kms * 1e-3) / 1e9
     return {"workload": "C4: TPC-H SF100 lineitem Q6-style predicate, 600037902 rows per GPU, "
                         "SELECT l_extendedprice*l_discount (Float64)",
             "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4),
             "selectivity": round(s, 5), "selected": selected, "parity_gate": gate,
-            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_row": round(bpr, 3)}}
+            "roofline": roofline(kname, n * bpr, kms, n)}
 
 
-def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
+def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
     """Real TPC-H Q6 (DFMI_FLAG_EXT_AGGREGATE): SELECT SUM(l_extendedprice *
     l_discount) FROM lineitem WHERE <Q6 predicate>, one fused predicate +
     exact-sum pass per step over the C4 table; with --gpus N every rank's exact
@@ -301,7 +432,9 @@ def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
     def step():
         st.reset()
         st.add(pred, batch, flags)
-        if dist:
+        if comm is not None:  # C-ABI: RCCL all_gather of the exact partials + merge
+            v = comm.agg_finish(st)[0]
+        elif dist:
             mine = torch.frombuffer(bytearray(st.partial()), dtype=torch.uint8).to(coll_device(dev))
             parts = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(parts, mine)
@@ -311,7 +444,8 @@ def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
         res["v"] = v
         return v.count
 
-    el, kms, selected = timed_steps(step, steps, warmup, dist, eng, dev)
+    el, kms, selected = timed_steps(step, steps, warmup, dist, eng, dev, py_exchange=False)
+    kname = kernel_name(eng)
     # gate: 4M-row prefix against the oracle
     m = min(n, 1 << 22)
     pre = RecordBatch(schema, [Array(DataType.Float64, m, c[:m].view(torch.uint8)) for c in cols])
@@ -322,14 +456,12 @@ def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows):
     gate = {"rows": m, "sum_bits_equal": bool(dv.bits == rv.bits and dv.count == rv.count), "count": int(rv.count)}
     s = selected / (n * world)  # the merged count covers every rank's rows
     bpr = 32.0  # 4 Float64 inputs; the output is one value
-    ach = n * bpr / (kms * 1e-3) / 1e9
     v = res["v"]
     return {"workload": "C4 real Q6: SELECT SUM(l_extendedprice*l_discount) FROM lineitem WHERE <Q6>, 600037902 "
                         "rows per GPU, exact Float64 sum", "rows_per_s": n * world * steps / el,
             "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4), "selectivity": round(s, 5),
             "sum": float(np.array([v.bits], dtype=np.uint64).view(np.float64)[0]), "parity_gate": gate,
-            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_row": bpr}}
+            "roofline": roofline(kname, n * bpr, kms, n)}
 
 
 def q6_table(dev, n, seed):
@@ -476,20 +608,20 @@ def c3_line(eng, dev, rank, world, steps, warmup, dist):
             return r
 
         el, _, selected = timed_steps(timed, steps, warmup, dist, eng, dev)
+        kname = kernel_name(eng)
         kms = float(np.mean(kms_all[warmup:]))
         gate = prefix_gate(eng, schema, batches[0], 1 << 22, pe, [Column(0), Column(1)], flags)
         n = C3_ROWS
         s = selected / n
         # v 8 B + validity 1/8 B, s offsets 4 B + its bytes; out s*(8 + 4) + selected bytes
         alg = n * (8.0 + 0.125 + 4.0) + nbytes + selected * 12.0 + acc["sel_bytes"]
-        ach = alg / (kms * 1e-3) / 1e9
+        # kms sums the step's C3_BATCHES launches: roofline() gets the per-launch mean
+        rl = roofline(kname, alg / C3_BATCHES, kms / C3_BATCHES, n, launches=C3_BATCHES)
+        rl["kernel_ms_per_step"] = round(kms, 4)
         res[qn] = {"query": "SELECT s, v WHERE " + ("s = '%s'" % w17 if qn == "eq" else "v < 0.5"),
                    "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3,
                    "kernel_ms": round(kms, 4), "selectivity": round(s, 5), "selected": selected,
-                   "parity_gate": gate,
-                   "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(ach / HBM_PEAK_GBS, 4),
-                                "algorithmic_bytes_per_row": round(alg / n, 3)}}
+                   "parity_gate": gate, "roofline": rl}
     return {"workload": "C3: 5e8 rows per GPU (4 batches of 1.25e8), nullable Float64 v (10%% nulls) + "
                         "Utf8 s (1000-word dictionary, avg %.2f B)" % (nbytes / C3_ROWS), **res}
 
@@ -598,7 +730,7 @@ def csv_line(eng, steps, warmup):
     batch = 1 << 20
 
     def parse_only():
-        src = NativeCsvDataSource(schema, path, True, batch)
+        src = NativeCsvDataSource(schema, path, True, batch, copy=False)
         rows = 0
         while True:
             b = src.next()
@@ -607,7 +739,7 @@ def csv_line(eng, steps, warmup):
             rows += b.num_rows()
 
     def end_to_end():
-        src = NativeCsvDataSource(schema, path, True, batch)
+        src = NativeCsvDataSource(schema, path, True, batch, copy=False)
         rows = sel = 0
         while True:
             b = src.next()
@@ -654,6 +786,10 @@ def main():
     ap.add_argument("--extra", default="c4,q6,c3,batches",
                     help="extra config lines (comma list: c4,q6,c3,batches,host,csv; empty = none)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange", choices=("abi", "torch"), default=None,
+                    help="N>1 exchange: the C-ABI RCCL path (dfmi_shard_filter_project, default under nccl) or "
+                         "torch.distributed (default for the gloo rehearsal)")
+    ap.add_argument("--gather", type=int, default=1, help="time dfmi_shard_gather_to_root of the C2 outputs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -683,17 +819,27 @@ def main():
     torch.cuda.synchronize(dev)
     schema = Schema([Field(c, DataType.Float64, False) for c in "abc"])
 
+    exchange = args.exchange or ("abi" if BACKEND == "nccl" else "torch")
+    comm = None
+    if (world > 1 and exchange == "abi") or (args.gather and (BACKEND == "nccl" or world == 1)):
+        comm = abi_comm(eng, dist, rank, world, dev)
+    step_comm = comm if (world > 1 and exchange == "abi") else None
     sels = [args.sel] + [float(x) for x in args.sweep.split(",") if x and float(x) != args.sel]
     results = {}
     for sel in sels:
-        step = FusedStep(eng, schema, cols, n, *query(sel), outs)
-        el, kms, selected = timed_steps(step, args.steps, args.warmup, dist, eng, dev)
+        step = FusedStep(eng, schema, cols, n, *query(sel), outs, comm=step_comm)
+        el, kms, selected = timed_steps(step, args.steps, args.warmup, dist, eng, dev, py_exchange=step_comm is None)
         s_real = selected / n
         bytes_per_row = 24.0 + 24.0 * s_real  # a,b,c read; s*(a,b,a*b+c) written
-        achieved = n * bytes_per_row / (kms * 1e-3) / 1e9
-        results[sel] = dict(el=el, kms=kms, selected=selected, s=s_real, achieved=achieved, bpr=bytes_per_row)
+        kname = kernel_name(eng)
+        rl = roofline(kname, n * bytes_per_row, kms, n, run="main" if sel == 0.5 else "c2_s%.2f" % sel)
+        results[sel] = dict(el=el, kms=kms, selected=selected, s=s_real, rl=rl, bpr=bytes_per_row)
     del outs, step
     torch.cuda.empty_cache()
+    gather = None
+    if args.gather and comm is not None:
+        gather = gather_line(eng, comm, schema, cols, n, args.sel, dist, rank, world, dev)
+        torch.cuda.empty_cache()
     from datafusion_amd.arrow import Array
     gate = prefix_gate(eng, schema, [Array(DataType.Float64, n, c.view(torch.uint8)) for c in cols],
                        min(n, 1 << 22), *query(args.sel))
@@ -708,9 +854,9 @@ def main():
         if name == "batches":
             continue
         if name == "c4":
-            extra["c4"] = q6_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS)
+            extra["c4"] = q6_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS, comm=step_comm)
         elif name == "q6":
-            extra["q6"] = q6_agg_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS)
+            extra["q6"] = q6_agg_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS, comm=step_comm)
         elif name == "host":
             if world == 1:
                 extra["host"] = host_line(eng, min(args.steps, 3), 1)
@@ -725,7 +871,6 @@ def main():
 
     h = results[args.sel]
     total_rows = n * world * args.steps
-    traffic = pmc_traffic(n, args.sel)
     out = {
         "metric": "filter+project rows/s (1e9-row Float64 table per GPU, SELECT a, b, a*b+c WHERE a > k AND b < m)",
         "value": total_rows / h["el"],
@@ -740,21 +885,21 @@ def main():
         "dtype": "f64",
         "data": "synthetic (splitmix64 seed 42, generated in HBM)",
         "config": {"workload": "C2: 1e9-row Float64 a,b,c per GPU; s=%.2f" % args.sel, "rows_per_gpu": n,
-                   "selectivity": round(h["s"], 4), "parallelism": "row-range shards, RCCL count all_gather"
-                   if BACKEND == "nccl" else "row-range shards, %s rehearsal on shared GPUs" % BACKEND},
-        "roofline": {"bound": "hbm", "achieved": round(h["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(h["achieved"] / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE passes, %s/traffic.json" % PROFILE_TAG
-                     if traffic else None,
-                     "kernel": "dfmi_query (query-compiled filter+project)", "kernel_ms": round(h["kms"], 4),
-                     "algorithmic_bytes_per_row": round(h["bpr"], 3)},
+                   "selectivity": round(h["s"], 4),
+                   "parallelism": ("row-range shards, C-ABI dfmi_shard_filter_project (RCCL all_gather of "
+                                   "placement records)" if step_comm is not None else
+                                   "row-range shards, torch.distributed count all_gather" if BACKEND == "nccl" else
+                                   "row-range shards, %s rehearsal on shared GPUs" % BACKEND) if world > 1
+                   else "one GPU"},
+        "roofline": h["rl"],
         "sweep": {("%.2f" % s): {"rows_per_s": n * world * args.steps / r["el"], "kernel_ms": round(r["kms"], 4),
-                                 "hbm_gbs": round(r["achieved"], 1), "frac": round(r["achieved"] / HBM_PEAK_GBS, 4),
-                                 "selected": r["selected"]}
+                                 "hbm_gbs": r["rl"]["achieved"], "frac": r["rl"]["frac"], "selected": r["selected"],
+                                 "roofline": r["rl"]}
                   for s, r in results.items()},
         "parity_gate": gate,
     }
+    if gather is not None:
+        out["gather"] = gather
     if extra:
         out["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu:

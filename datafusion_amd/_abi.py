@@ -149,6 +149,7 @@ EXPORTED = [
     "dfmi_last_timing",
     "dfmi_last_compile_ms",
     "dfmi_last_error_order",
+    "dfmi_last_kernel_name",
     "dfmi_compile_aggregate",
     "dfmi_aggregate_name",
     "dfmi_aggregate_type",
@@ -272,6 +273,8 @@ def lib() -> C.CDLL:
     L.dfmi_last_compile_ms.restype = C.c_int32
     L.dfmi_last_error_order.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.dfmi_last_error_order.restype = C.c_int32
+    L.dfmi_last_kernel_name.argtypes = [C.c_void_p]
+    L.dfmi_last_kernel_name.restype = C.c_char_p
     L.dfmi_generate_column.argtypes = [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_void_p, C.POINTER(dfmi_error)]
     L.dfmi_generate_column.restype = C.c_int32

@@ -438,6 +438,7 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             hipFunction_t fn;
             try {
                 fn = jit::get_kernel(ctx->device, B.plan, B.X, &ctx->last_compile_ms);
+                ctx->last_kernel = B.X.kname;
             } catch (const Fail& f) {
                 if (se.set) throw Fail{se.code, se.msg};
                 throw;

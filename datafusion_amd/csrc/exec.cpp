@@ -316,6 +316,10 @@ extern "C" int32_t dfmi_last_error_order(const dfmi_context* c, uint64_t* key) {
     return DFMI_OK;
 }
 
+extern "C" const char* dfmi_last_kernel_name(const dfmi_context* c) {
+    return c ? c->last_kernel.c_str() : "";
+}
+
 extern "C" int32_t dfmi_last_compile_ms(const dfmi_context* c, double* compile_ms) {
     if (!c || !compile_ms) return DFMI_ERR_INVALID_ARGUMENT;
     *compile_ms = c->last_compile_ms;
@@ -368,6 +372,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             hipFunction_t fn;
             try {
                 fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
+                ctx->last_kernel = X.kname;
             } catch (const Fail& f) {
                 if (se.set) throw Fail{se.code, se.msg};  // the reference fails first
                 throw;

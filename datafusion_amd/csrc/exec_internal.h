@@ -44,6 +44,7 @@ struct dfmi_context {
     // evaluation-order key (ordinal << 44 | row << 4) of the error the last
     // dfmi_filter_project raised; ~0 for none / an error outside that order
     uint64_t last_err_key = ~0ull;
+    std::string last_kernel;  // name of the last launched query kernel (dfmi_last_kernel_name)
 };
 
 namespace dfmi {

@@ -343,7 +343,7 @@ std::vector<char> compile_code(const std::string& src, double* compile_ms) {
     return code;
 }
 
-static hipFunction_t compile(int device, const std::string& src, double* compile_ms) {
+static hipFunction_t compile(int device, const std::string& src, const std::string& name, double* compile_ms) {
     const std::string key = std::to_string(device) + "\n" + src;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
@@ -351,7 +351,7 @@ static hipFunction_t compile(int device, const std::string& src, double* compile
     const std::vector<char> code = compile_code(src, compile_ms);
     Compiled c;
     if (hipModuleLoadData(&c.mod, code.data()) != hipSuccess) throw Fail{DFMI_ERR_DEVICE, "hipModuleLoadData failed"};
-    if (hipModuleGetFunction(&c.fn, c.mod, "dfmi_query") != hipSuccess)
+    if (hipModuleGetFunction(&c.fn, c.mod, name.c_str()) != hipSuccess)
         throw Fail{DFMI_ERR_DEVICE, "hipModuleGetFunction failed"};
     g_cache[key] = c;
     return c.fn;
@@ -537,7 +537,7 @@ std::string generate(const Plan& P, Launch& X) {
     o << "\n// ---- generated query kernel ----\n";
     o << "extern \"C\" __global__ __launch_bounds__(" << BLOCK << ")";
     if (X.waves_per_eu > 0) o << " __attribute__((amdgpu_waves_per_eu(" << X.waves_per_eu << ")))";
-    o << " void dfmi_query(const dfmi::Args A) {\n";
+    o << " void DFMI_KNAME(const dfmi::Args A) {\n";
     o << "  constexpr int BLOCK = " << BLOCK << ", K = " << K << ", WAVES = BLOCK / 64;\n";
     o << "  const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);\n";
     o << "  dfmi::clear_previous<BLOCK>(A, blockIdx.x, tid);\n";
@@ -691,7 +691,17 @@ std::string generate(const Plan& P, Launch& X) {
                   << "]);\n";
     }
     o << "}\n";
-    return std::string(dfmi_skeleton_src) + o.str();
+    // kernel name: the plan kind and a hash of the generated body, so that
+    // rocprofv3 reports every query shape as its own kernel
+    std::string body = o.str();
+    uint64_t h = 1469598103934665603ull;  // FNV-1a
+    for (unsigned char ch : body) h = (h ^ ch) * 1099511628211ull;
+    char nm[64];
+    snprintf(nm, sizeof nm, "dfmi_%s_%08llx", !P.aggs.empty() ? "agg" : (P.pred ? "filter" : "project"),
+             (unsigned long long)(h & 0xffffffffull));
+    X.kname = nm;
+    body.replace(body.find("DFMI_KNAME"), 10, X.kname);
+    return std::string(dfmi_skeleton_src) + body;
 }
 
 // ------------------------------------------------------- shape fast path
@@ -703,6 +713,7 @@ std::string generate(const Plan& P, Launch& X) {
 namespace {
 struct ShapeHit {
     hipFunction_t fn;
+    std::string kname;
     uint64_t lits[32];
     int n_lits;
     int str_off[8], str_len[8];
@@ -770,13 +781,15 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
             memcpy(X.str, h.str, sizeof h.str);
             X.n_str = h.n_str;
             X.str_bytes = h.str_bytes;
+            X.kname = h.kname;
             return h.fn;
         }
     }
     const std::string src = generate(P, X);
     if (getenv("DFMI_JIT_PRINT")) fprintf(stderr, "%s\n", src.c_str() + strlen(dfmi_skeleton_src));
     ShapeHit h;
-    h.fn = compile(device, src, compile_ms);
+    h.fn = compile(device, src, X.kname, compile_ms);
+    h.kname = X.kname;
     memcpy(h.lits, X.args_lits, sizeof h.lits);
     h.n_lits = X.n_lits;
     memcpy(h.str_off, X.str_off, sizeof h.str_off);

@@ -74,6 +74,7 @@ struct Launch {
     int str_off[8] = {}, str_len[8] = {};
     char str[256] = {};
     int n_str = 0, str_bytes = 0;
+    std::string kname;  // generated kernel's name (dfmi_<kind>_<hash>)
 
     int col_type(int col) const { return in->columns[col].type; }
     bool col_nullable(int col) const {

@@ -5,19 +5,31 @@
 // ProjectRelation and filter() preserves row order (filter.rs:87-91), so the
 // per-rank outputs in rank order ARE the reference's output stream.
 //
-//   dfmi_shard_filter_project: the local fused pass, then ONE ncclAllGather of
-//     a fixed int64 record per rank (status, error order key, selected rows,
-//     Utf8 bytes and null count per output) -> every rank's global placement;
-//     a failure anywhere becomes the same (globally first) error on every rank.
+//   dfmi_shard_filter_project: the local fused pass, then ONE all_gather of a
+//     fixed record per rank (status, error position, selected rows, Utf8
+//     bytes and null count per output, error message) -> every rank's global
+//     placement; a failure anywhere becomes the same (globally first) error
+//     on every rank.
 //   dfmi_shard_gather_to_root: optional concatenation on one rank with grouped
-//     ncclSend / ncclRecv (RCCL has no gatherv), bound by the root's xGMI
-//     ingress; Utf8 offsets rebased and bitmaps re-aligned on the root.
+//     send / recv (RCCL has no gatherv), bound by the root's xGMI ingress;
+//     Utf8 offsets rebased and bitmaps re-aligned on the root. Every rank's
+//     argument checks are agreed on (one small all_gather) BEFORE the
+//     transfers, so a caller mistake on one rank fails every rank instead of
+//     leaving the others blocked in a send.
 //   dfmi_shard_agg_finish: the aggregate extension's exact partials,
-//     ncclAllGather'ed and merged -- bit-identical to one GPU over all rows.
+//     all_gathered and merged -- bit-identical to one GPU over all rows.
+//
+// The collectives go through a Transport: RCCL (the product path, one
+// process or thread per GPU) or, for tests only, a loopback group of threads
+// sharing one device (dfmi_internal_* hooks at the end of this file), so the
+// placement, error agreement and gather code runs at world sizes > 1 on a
+// one-GPU box.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -33,24 +45,217 @@ hipError_t launch_place_bits(const uint8_t* src, long long n, uint8_t* dst, long
 
 namespace {
 constexpr int kMaxOut = 16;
-constexpr int kRec = 3 + 2 * kMaxOut;  // status, error key, rows, utf8 bytes[16], nulls[16]
+// record per rank: status, error position (evaluation-order key >> 44), rows,
+// utf8 bytes[16], nulls[16]; then the error message
+constexpr int kRec = 3 + 2 * kMaxOut;
 constexpr int kMsg = 512;
+constexpr size_t kRecBytes = kRec * 8 + kMsg;
 
 #define NCCL_TRY(x)                                                                                         \
     do {                                                                                                    \
         ncclResult_t r_ = (x);                                                                              \
         if (r_ != ncclSuccess) throw Fail{DFMI_ERR_DEVICE, std::string(#x ": ") + ncclGetErrorString(r_)}; \
     } while (0)
+
+// The collectives of the shard path. all_gather works on host buffers (the
+// records are a few hundred bytes); send / recv move device buffers and
+// complete at group_end (the context stream is synchronised there).
+struct Transport {
+    virtual ~Transport() = default;
+    virtual void all_gather(dfmi_context* ctx, const void* mine, void* all, size_t bytes) = 0;
+    virtual void group_start() = 0;
+    virtual void send(dfmi_context* ctx, const void* buf, size_t nb, int peer) = 0;
+    virtual void recv(dfmi_context* ctx, void* buf, size_t nb, int peer) = 0;
+    virtual void group_end(dfmi_context* ctx) = 0;
+};
+
+struct RcclTransport : Transport {
+    int world, rank;
+    ncclComm_t comm = nullptr;
+    uint8_t* d = nullptr;  // all_gather staging, world x bytes
+    size_t cap = 0;
+    RcclTransport(int w, int r) : world(w), rank(r) {}
+    ~RcclTransport() override {
+        if (comm) ncclCommDestroy(comm);
+        if (d) (void)hipFree(d);
+    }
+    void all_gather(dfmi_context* ctx, const void* mine, void* all, size_t bytes) override {
+        hipStream_t st = ctx->stream;
+        if (cap < bytes * world) {
+            if (d) HIP_TRY(hipFree(d));
+            d = nullptr;
+            cap = 0;
+            HIP_TRY(hipMalloc((void**)&d, bytes * world));
+            cap = bytes * world;
+        }
+        uint8_t* send = d + (size_t)rank * bytes;
+        HIP_TRY(hipMemcpyAsync(send, mine, bytes, hipMemcpyHostToDevice, st));
+        NCCL_TRY(ncclAllGather(send, d, bytes, ncclUint8, comm, st));  // in place
+        HIP_TRY(hipMemcpyAsync(all, d, bytes * world, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    void group_start() override { NCCL_TRY(ncclGroupStart()); }
+    void send(dfmi_context* ctx, const void* buf, size_t nb, int peer) override {
+        NCCL_TRY(ncclSend(buf, nb, ncclUint8, peer, comm, ctx->stream));
+    }
+    void recv(dfmi_context* ctx, void* buf, size_t nb, int peer) override {
+        NCCL_TRY(ncclRecv(buf, nb, ncclUint8, peer, comm, ctx->stream));
+    }
+    void group_end(dfmi_context* ctx) override {
+        NCCL_TRY(ncclGroupEnd());
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+};
+
+// ---- loopback transport (tests): `world` host threads in one process, each
+// with its own context on the same device; the collectives are host
+// rendezvous + device-to-device copies.
+struct LoopGroup {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long generation = 0;
+    std::vector<uint8_t> buf;
+    struct Post {
+        int src, dst;
+        const void* p;
+        size_t nb;
+    };
+    std::vector<Post> posts;
+    explicit LoopGroup(int w) : world(w) {}
+    void barrier(std::unique_lock<std::mutex>& lk) {
+        const long g = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != g; });
+        }
+    }
+};
+
+struct LoopTransport : Transport {
+    LoopGroup* g;
+    int rank;
+    std::vector<LoopGroup::Post> sends, recvs;
+    LoopTransport(LoopGroup* grp, int r) : g(grp), rank(r) {}
+    void all_gather(dfmi_context*, const void* mine, void* all, size_t bytes) override {
+        std::unique_lock<std::mutex> lk(g->mu);
+        if (g->buf.size() < bytes * g->world) g->buf.resize(bytes * g->world);
+        memcpy(g->buf.data() + (size_t)rank * bytes, mine, bytes);
+        g->barrier(lk);
+        memcpy(all, g->buf.data(), bytes * g->world);
+        g->barrier(lk);
+    }
+    void group_start() override {
+        sends.clear();
+        recvs.clear();
+    }
+    void send(dfmi_context*, const void* buf, size_t nb, int peer) override { sends.push_back({rank, peer, buf, nb}); }
+    void recv(dfmi_context*, void* buf, size_t nb, int peer) override { recvs.push_back({peer, rank, buf, nb}); }
+    void group_end(dfmi_context* ctx) override {
+        hipStream_t st = ctx->stream;
+        HIP_TRY(hipStreamSynchronize(st));  // this rank's send buffers are final
+        std::unique_lock<std::mutex> lk(g->mu);
+        for (const auto& s : sends) g->posts.push_back(s);
+        g->barrier(lk);
+        std::vector<int> taken(g->posts.size(), 0);
+        bool ok = true;
+        for (const auto& r : recvs) {  // k-th recv from src <- k-th send from src to us (RCCL's matching)
+            bool found = false;
+            for (size_t i = 0; i < g->posts.size(); ++i) {
+                const auto& s = g->posts[i];
+                if (taken[i] || s.src != r.src || s.dst != rank) continue;
+                taken[i] = 1;
+                found = true;
+                if (s.nb != r.nb) ok = false;
+                else if (hipMemcpyAsync((void*)r.p, s.p, r.nb, hipMemcpyDeviceToDevice, st) != hipSuccess) ok = false;
+                break;
+            }
+            if (!found) ok = false;
+        }
+        lk.unlock();
+        const hipError_t e = hipStreamSynchronize(st);
+        lk.lock();
+        g->barrier(lk);  // every receiver done reading the posts
+        if (rank == 0) g->posts.clear();
+        g->barrier(lk);
+        if (!ok) throw Fail{DFMI_ERR_DEVICE, "loopback transport: unmatched send/recv"};
+        if (e != hipSuccess) throw Fail{DFMI_ERR_DEVICE, std::string("loopback copy: ") + hipGetErrorString(e)};
+    }
+};
+
+// ---- placement / error agreement over the exchanged records (pure)
+int first_failed_rank(const int64_t* recs, int world, size_t stride_words) {
+    int first = -1;
+    for (int r = 0; r < world; ++r) {
+        const int64_t* rr = recs + (size_t)r * stride_words;
+        if (!rr[0]) continue;
+        // smallest evaluation position, then the lowest rank (= earliest rows)
+        if (first < 0 || (uint64_t)rr[1] < (uint64_t)recs[(size_t)first * stride_words + 1]) first = r;
+    }
+    return first;
+}
+
+void placement_of(const int64_t* recs, int world, int rank, int nout, size_t stride_words, dfmi_shard_placement* p) {
+    memset(p, 0, sizeof *p);
+    p->world = world;
+    p->rank = rank;
+    for (int r = 0; r < world; ++r) {
+        const int64_t* rr = recs + (size_t)r * stride_words;
+        if (r < rank) p->row_offset += rr[2];
+        p->total_rows += rr[2];
+        for (int o = 0; o < nout; ++o) {
+            if (r < rank) p->utf8_base[o] += rr[3 + o];
+            p->utf8_total[o] += rr[3 + o];
+            p->null_total[o] += rr[3 + kMaxOut + o];
+        }
+    }
+}
 }  // namespace
 
 struct dfmi_shard_comm {
     int world = 1, rank = 0, device = 0;
-    ncclComm_t comm = nullptr;
-    int64_t* d_rec = nullptr;  // [world][kRec] device exchange buffer
-    char* d_msg = nullptr;     // [world][kMsg]
-    std::vector<int64_t> rec;  // the last exchange, host copy
+    Transport* tp = nullptr;
+    std::vector<int64_t> rec;  // the last exchange: world x kRec
     int nout = 0;              // outputs of the last exchanged pass
 };
+
+namespace {
+// One all_gather of every rank's record + message; on a failure anywhere,
+// every rank throws the globally first error with the failing rank's message.
+void exchange(dfmi_context* ctx, dfmi_shard_comm* c, const int64_t* mine, const char* msg) {
+    std::vector<uint8_t> me(kRecBytes, 0), all(kRecBytes * c->world);
+    memcpy(me.data(), mine, kRec * 8);
+    snprintf((char*)me.data() + kRec * 8, kMsg, "%s", msg ? msg : "");
+    c->tp->all_gather(ctx, me.data(), all.data(), kRecBytes);
+    c->rec.assign((size_t)c->world * kRec, 0);
+    for (int r = 0; r < c->world; ++r) memcpy(&c->rec[(size_t)r * kRec], &all[(size_t)r * kRecBytes], kRec * 8);
+    const int first = first_failed_rank(c->rec.data(), c->world, kRec);
+    if (first < 0) return;
+    all[(size_t)first * kRecBytes + kRecBytes - 1] = 0;
+    throw Fail{(int32_t)c->rec[(size_t)first * kRec], std::string((const char*)&all[(size_t)first * kRecBytes + kRec * 8])};
+}
+
+// Agreement on a local outcome (collective): every rank throws the error of
+// the lowest failing rank, or all go on.
+void agree(dfmi_context* ctx, dfmi_shard_comm* c, int32_t code, const std::string& msg) {
+    std::vector<uint8_t> me(kMsg + 8, 0), all((size_t)(kMsg + 8) * c->world);
+    memcpy(me.data(), &code, 4);
+    snprintf((char*)me.data() + 8, kMsg, "%s", msg.c_str());
+    c->tp->all_gather(ctx, me.data(), all.data(), me.size());
+    for (int r = 0; r < c->world; ++r) {
+        int32_t rc;
+        memcpy(&rc, &all[(size_t)r * (kMsg + 8)], 4);
+        if (rc) {
+            all[(size_t)(r + 1) * (kMsg + 8) - 1] = 0;
+            throw Fail{rc, std::string((const char*)&all[(size_t)r * (kMsg + 8) + 8])};
+        }
+    }
+}
+}  // namespace
 
 extern "C" int32_t dfmi_shard_unique_id(uint8_t* id, dfmi_error* err) {
     set_err(err, DFMI_OK, "");
@@ -77,20 +282,18 @@ extern "C" int32_t dfmi_shard_comm_init(dfmi_context* ctx, int32_t world, int32_
         c->world = world;
         c->rank = rank;
         c->device = ctx->device;
-        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipSetDevice(c->device));
+        auto* t = new RcclTransport(world, rank);
+        c->tp = t;
         ncclUniqueId u;
         memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
-        NCCL_TRY(ncclCommInitRank(&c->comm, world, u, rank));
-        HIP_TRY(hipMalloc((void**)&c->d_rec, (size_t)world * kRec * 8));
-        HIP_TRY(hipMalloc((void**)&c->d_msg, (size_t)world * kMsg));
+        NCCL_TRY(ncclCommInitRank(&t->comm, world, u, rank));
         c->rec.assign((size_t)world * kRec, 0);
         *out = c;
         return DFMI_OK;
     } catch (const Fail& f) {
         if (c) {
-            if (c->comm) ncclCommDestroy(c->comm);
-            if (c->d_rec) (void)hipFree(c->d_rec);
-            if (c->d_msg) (void)hipFree(c->d_msg);
+            delete c->tp;
             delete c;
         }
         set_err(err, f.code, f.msg);
@@ -101,43 +304,9 @@ extern "C" int32_t dfmi_shard_comm_init(dfmi_context* ctx, int32_t world, int32_
 extern "C" void dfmi_shard_comm_destroy(dfmi_shard_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->comm) ncclCommDestroy(c->comm);
-    if (c->d_rec) (void)hipFree(c->d_rec);
-    if (c->d_msg) (void)hipFree(c->d_msg);
+    delete c->tp;
     delete c;
 }
-
-namespace {
-// One all_gather of every rank's record; on a failure anywhere, every rank
-// throws the globally first error -- the smallest evaluation ordinal, then
-// the lowest rank (= earliest rows), as the reference over the whole table
-// would raise it -- with the failing rank's message.
-void exchange(dfmi_context* ctx, dfmi_shard_comm* c, const int64_t* mine, const dfmi_error& local) {
-    hipStream_t st = ctx->stream;
-    int64_t* send = c->d_rec + (size_t)c->rank * kRec;
-    HIP_TRY(hipMemcpyAsync(send, mine, kRec * 8, hipMemcpyHostToDevice, st));
-    NCCL_TRY(ncclAllGather(send, c->d_rec, kRec, ncclInt64, c->comm, st));
-    HIP_TRY(hipMemcpyAsync(c->rec.data(), c->d_rec, c->rec.size() * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    int first = -1;
-    for (int r = 0; r < c->world; ++r) {
-        const int64_t* rr = &c->rec[(size_t)r * kRec];
-        if (!rr[0]) continue;
-        if (first < 0 || ((uint64_t)rr[1] >> 44) < ((uint64_t)c->rec[(size_t)first * kRec + 1] >> 44)) first = r;
-    }
-    if (first < 0) return;
-    char msg[kMsg] = {};
-    snprintf(msg, sizeof msg, "%s", local.message);
-    char* msend = c->d_msg + (size_t)c->rank * kMsg;
-    HIP_TRY(hipMemcpyAsync(msend, msg, kMsg, hipMemcpyHostToDevice, st));
-    NCCL_TRY(ncclAllGather(msend, c->d_msg, kMsg, ncclChar, c->comm, st));
-    std::vector<char> all((size_t)c->world * kMsg);
-    HIP_TRY(hipMemcpyAsync(all.data(), c->d_msg, all.size(), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    all[(size_t)(first + 1) * kMsg - 1] = 0;
-    throw Fail{(int32_t)c->rec[(size_t)first * kRec], std::string(&all[(size_t)first * kMsg])};
-}
-}  // namespace
 
 extern "C" int32_t dfmi_shard_filter_project(dfmi_context* ctx, dfmi_shard_comm* c, const dfmi_program* pred,
                                              const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
@@ -149,32 +318,37 @@ extern "C" int32_t dfmi_shard_filter_project(dfmi_context* ctx, dfmi_shard_comm*
         const int nout = np > 0 ? np : in->num_columns;
         if (nout > kMaxOut) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many output columns"};
         dfmi_error local;
-        const int32_t rc = dfmi_filter_project(ctx, pred, projs, np, in, outs, flags, &local);
+        int32_t rc = dfmi_filter_project(ctx, pred, projs, np, in, outs, flags, &local);
         int64_t mine[kRec] = {};
-        mine[0] = rc;
-        mine[1] = rc ? (int64_t)ctx->last_err_key : 0;
         if (rc == DFMI_OK) {
-            mine[2] = nout ? outs[0].length : 0;
-            for (int o = 0; o < nout; ++o) {
-                mine[3 + o] = outs[o].type == DFMI_TYPE_UTF8 ? outs[o].data_length : 0;
-                mine[3 + kMaxOut + o] = outs[o].null_count;
+            try {
+                mine[2] = nout ? outs[0].length : 0;
+                for (int o = 0; o < nout; ++o) {
+                    int64_t nb = outs[o].type == DFMI_TYPE_UTF8 ? outs[o].data_length : 0;
+                    if (outs[o].type == DFMI_TYPE_UTF8 && outs[o].passthrough_column >= 0 && outs[o].length > 0) {
+                        // passthrough (Arc clone): the input column's byte span
+                        const int32_t* of = in->columns[outs[o].passthrough_column].offsets;
+                        int32_t ends[2];
+                        HIP_TRY(hipMemcpy(&ends[0], of, 4, hipMemcpyDeviceToHost));
+                        HIP_TRY(hipMemcpy(&ends[1], of + outs[o].length, 4, hipMemcpyDeviceToHost));
+                        nb = ends[1] - ends[0];
+                    }
+                    mine[3 + o] = nb;
+                    mine[3 + kMaxOut + o] = outs[o].null_count;
+                }
+            } catch (const Fail& f) {
+                rc = f.code;
+                set_err(&local, f.code, f.msg);
             }
         }
-        exchange(ctx, c, mine, local);  // throws the globally first error on every rank
+        if (rc != DFMI_OK) {
+            memset(mine, 0, sizeof mine);
+            mine[0] = rc;
+            mine[1] = (int64_t)(ctx->last_err_key >> 44);  // ~0 (no position) sorts last
+        }
+        exchange(ctx, c, mine, rc ? local.message : "");  // throws the globally first error on every rank
         c->nout = nout;
-        memset(place, 0, sizeof *place);
-        place->world = c->world;
-        place->rank = c->rank;
-        for (int r = 0; r < c->world; ++r) {
-            const int64_t* rr = &c->rec[(size_t)r * kRec];
-            if (r < c->rank) place->row_offset += rr[2];
-            place->total_rows += rr[2];
-            for (int o = 0; o < nout; ++o) {
-                if (r < c->rank) place->utf8_base[o] += rr[3 + o];
-                place->utf8_total[o] += rr[3 + o];
-                place->null_total[o] += rr[3 + kMaxOut + o];
-            }
-        }
+        placement_of(c->rec.data(), c->world, c->rank, nout, kRec, place);
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -185,143 +359,145 @@ extern "C" int32_t dfmi_shard_filter_project(dfmi_context* ctx, dfmi_shard_comm*
 extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm* c, const dfmi_out_column* local,
                                              const dfmi_out_column* root_outs, int32_t root, dfmi_error* err) {
     set_err(err, DFMI_OK, "");
+    if (!ctx || !c) {
+        set_err(err, DFMI_ERR_INVALID_ARGUMENT, "bad argument");
+        return DFMI_ERR_INVALID_ARGUMENT;
+    }
+    std::vector<uint8_t*> stage;
     try {
-        if (!ctx || !c || !local || root < 0 || root >= c->world) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
-        if (c->rank == root && !root_outs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "root outputs are NULL"};
-        hipStream_t st = ctx->stream;
         HIP_TRY(hipSetDevice(ctx->device));
+        hipStream_t st = ctx->stream;
         const int nout = c->nout, world = c->world;
         auto rec = [&](int r, int i) { return c->rec[(size_t)r * kRec + i]; };
-        for (int o = 0; o < nout; ++o)
-            if (local[o].type == DFMI_TYPE_UTF8) {
-                int64_t tot = 0;
-                for (int r = 0; r < world; ++r) tot += rec(r, 3 + o);
-                // i32 offsets address < 2^31 bytes (arrow BinaryArray)
-                if (tot >= ((int64_t)1 << 31)) throw Fail{DFMI_ERR_CAPACITY, "gathered Utf8 column exceeds 2^31 bytes"};
-                if (c->rank == root && root_outs[o].data_capacity < tot)
-                    throw Fail{DFMI_ERR_CAPACITY, "root Utf8 data_capacity too small"};
-            }
-        // staging on the root for pieces that need re-alignment (offsets, bitmaps)
-        std::vector<uint8_t*> stage;
-        auto stage_buf = [&](size_t nb) {
-            uint8_t* p = nullptr;
-            HIP_TRY(hipMalloc((void**)&p, nb ? nb : 8));
-            stage.push_back(p);
-            return p;
-        };
-        for (int o = 0; o < nout; ++o)
-            if (local[o].passthrough_column >= 0)
-                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output is a passthrough input column: gather the input"};
         int64_t total_rows = 0;
         for (int r = 0; r < world; ++r) total_rows += rec(r, 2);
-        if (c->rank == root)  // bitmaps are ORed in: start from zero
-            for (int o = 0; o < nout; ++o) {
-                int64_t nulls = 0;
-                for (int r = 0; r < world; ++r) nulls += rec(r, 3 + kMaxOut + o);
-                if (local[o].type == DFMI_TYPE_BOOLEAN)
-                    HIP_TRY(hipMemsetAsync(root_outs[o].values, 0, (size_t)((total_rows + 63) / 64 * 8), st));
-                if (nulls) {
-                    if (!root_outs[o].validity) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "root validity is NULL"};
-                    HIP_TRY(hipMemsetAsync(root_outs[o].validity, 0, (size_t)((total_rows + 63) / 64 * 8), st));
-                }
-            }
-        struct Fix {
-            int kind;  // 0 offsets rebase, 1 value bits, 2 validity bits
-            int o, r;
-            uint8_t* buf;
+        auto nulls_of = [&](int o) {
+            int64_t x = 0;
+            for (int r = 0; r < world; ++r) x += rec(r, 3 + kMaxOut + o);
+            return x;
         };
-        std::vector<Fix> fixes;
+
+        // ---- phase 1: this rank's checks and allocations, then agreement
+        struct Piece {
+            const void* src;
+            void* dst;  // root: final place (nullptr: staged for a fix-up)
+            size_t nb;
+            int fix;    // -1 none, 0 offsets rebase, 1 value bits, 2 validity bits
+            int o, r;
+        };
+        std::vector<Piece> pieces;  // (o, r) order, the same on every rank
+        int32_t code = DFMI_OK;
+        std::string msg;
         try {
-            NCCL_TRY(ncclGroupStart());
+            if (!local || root < 0 || root >= world) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+            if (c->rank == root && !root_outs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "root outputs are NULL"};
+            for (int o = 0; o < nout; ++o) {
+                if (local[o].passthrough_column >= 0)
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output is a passthrough input column: gather the input"};
+                if (local[o].type == DFMI_TYPE_UTF8) {
+                    int64_t tot = 0;
+                    for (int r = 0; r < world; ++r) tot += rec(r, 3 + o);
+                    // i32 offsets address < 2^31 bytes (arrow BinaryArray)
+                    if (tot >= ((int64_t)1 << 31)) throw Fail{DFMI_ERR_CAPACITY, "gathered Utf8 column exceeds 2^31 bytes"};
+                    if (c->rank == root && root_outs[o].data_capacity < tot)
+                        throw Fail{DFMI_ERR_CAPACITY, "root Utf8 data_capacity too small"};
+                }
+                if (c->rank == root && nulls_of(o) && !root_outs[o].validity)
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "root validity is NULL"};
+            }
             for (int o = 0; o < nout; ++o) {
                 const int t = local[o].type;
-                const bool bits = t == DFMI_TYPE_BOOLEAN;
                 const int w = jit::type_width(t);
-                int64_t nulls = 0;
-                for (int r = 0; r < world; ++r) nulls += rec(r, 3 + kMaxOut + o);
+                const bool has_nulls = nulls_of(o) > 0;
+                int64_t row0 = 0, b0 = 0;
                 for (int r = 0; r < world; ++r) {
                     const int64_t n = rec(r, 2);
-                    if (!n) continue;
-                    int64_t row0 = 0, b0 = 0;
-                    for (int q = 0; q < r; ++q) {
-                        row0 += rec(q, 2);
-                        b0 += rec(q, 3 + o);
-                    }
-                    // (pointer, bytes) of rank r's buffers, in an order both sides agree on
-                    struct Piece {
-                        const void* src;
-                        void* dst;  // root: final place, or nullptr = staged
-                        size_t nb;
-                        int fix;
-                    };
-                    std::vector<Piece> pieces;
-                    if (t == DFMI_TYPE_UTF8) {
-                        pieces.push_back({local[o].data, c->rank == root ? root_outs[o].data + b0 : nullptr,
-                                          (size_t)rec(r, 3 + o), -1});
-                        pieces.push_back({local[o].offsets, nullptr, (size_t)(n + 1) * 4, 0});
-                    } else if (bits) {
-                        pieces.push_back({local[o].values, nullptr, (size_t)((n + 7) / 8), 1});
-                    } else {
-                        pieces.push_back({local[o].values,
+                    const bool mine = c->rank == root || r == c->rank;
+                    if (n && mine) {
+                        std::vector<Piece> pc;
+                        if (t == DFMI_TYPE_UTF8) {
+                            pc.push_back({local[o].data, c->rank == root ? root_outs[o].data + b0 : nullptr,
+                                          (size_t)rec(r, 3 + o), -1, o, r});
+                            pc.push_back({local[o].offsets, nullptr, (size_t)(n + 1) * 4, 0, o, r});
+                        } else if (t == DFMI_TYPE_BOOLEAN) {
+                            pc.push_back({local[o].values, nullptr, (size_t)((n + 7) / 8), 1, o, r});
+                        } else {
+                            pc.push_back({local[o].values,
                                           c->rank == root ? (uint8_t*)root_outs[o].values + row0 * w : nullptr,
-                                          (size_t)(n * w), -1});
-                    }
-                    if (nulls) pieces.push_back({local[o].validity, nullptr, (size_t)((n + 7) / 8), 2});
-                    for (const Piece& p : pieces) {
-                        if (!p.nb) continue;
-                        if (c->rank == root) {
-                            uint8_t* dst = (uint8_t*)p.dst;
-                            if (p.fix >= 0) {
-                                dst = stage_buf(p.nb);
-                                fixes.push_back({p.fix, o, r, dst});
+                                          (size_t)(n * w), -1, o, r});
+                        }
+                        if (has_nulls) pc.push_back({local[o].validity, nullptr, (size_t)((n + 7) / 8), 2, o, r});
+                        for (Piece& p : pc) {
+                            if (!p.nb) continue;
+                            if (r == c->rank && !p.src && p.fix != 2)
+                                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "local output buffer is NULL"};
+                            if (c->rank == root && p.fix >= 0) {  // staged on the root, fixed up after
+                                uint8_t* s = nullptr;
+                                HIP_TRY(hipMalloc((void**)&s, p.nb));
+                                stage.push_back(s);
+                                p.dst = s;
                             }
-                            if (r == root) {
-                                if (p.fix == 2 && !p.src) {  // this rank has no validity: all valid
-                                    HIP_TRY(hipMemsetAsync(dst, 0xff, p.nb, st));
-                                } else {
-                                    HIP_TRY(hipMemcpyAsync(dst, p.src, p.nb, hipMemcpyDeviceToDevice, st));
-                                }
-                            } else {
-                                NCCL_TRY(ncclRecv(dst, p.nb, ncclUint8, r, c->comm, st));
-                            }
-                        } else if (r == c->rank) {
-                            const void* src = p.src;
-                            if (p.fix == 2 && !src) {  // all valid
-                                uint8_t* ones = stage_buf(p.nb);
+                            if (r == c->rank && p.fix == 2 && !p.src) {  // no validity here: all valid
+                                uint8_t* ones = nullptr;
+                                HIP_TRY(hipMalloc((void**)&ones, p.nb));
+                                stage.push_back(ones);
                                 HIP_TRY(hipMemsetAsync(ones, 0xff, p.nb, st));
-                                src = ones;
+                                p.src = ones;
                             }
-                            NCCL_TRY(ncclSend(src, p.nb, ncclUint8, root, c->comm, st));
+                            pieces.push_back(p);
                         }
                     }
+                    row0 += n;
+                    b0 += rec(r, 3 + o);
                 }
             }
-            NCCL_TRY(ncclGroupEnd());
-            // root: rebase offsets / place bitmaps at the global row offset
-            if (c->rank == root) {
-                for (const Fix& f : fixes) {
-                    int64_t row0 = 0, b0 = 0;
-                    for (int q = 0; q < f.r; ++q) {
-                        row0 += rec(q, 2);
-                        b0 += rec(q, 3 + f.o);
-                    }
-                    const int64_t n = rec(f.r, 2);
-                    if (f.kind == 0)
-                        HIP_TRY(launch_rebase_offsets((const int32_t*)f.buf, n, b0, root_outs[f.o].offsets + row0, st));
-                    else
-                        HIP_TRY(launch_place_bits(f.buf, n, f.kind == 1 ? (uint8_t*)root_outs[f.o].values
-                                                                        : root_outs[f.o].validity,
-                                                  row0, st));
+            if (c->rank == root)  // bitmaps are ORed in: start from zero
+                for (int o = 0; o < nout; ++o) {
+                    if (local[o].type == DFMI_TYPE_BOOLEAN)
+                        HIP_TRY(hipMemsetAsync(root_outs[o].values, 0, (size_t)((total_rows + 63) / 64 * 8), st));
+                    if (nulls_of(o))
+                        HIP_TRY(hipMemsetAsync(root_outs[o].validity, 0, (size_t)((total_rows + 63) / 64 * 8), st));
                 }
+        } catch (const Fail& f) {
+            code = f.code;
+            msg = f.msg;
+        }
+        agree(ctx, c, code, msg);  // every rank fails, or every rank transfers
+
+        // ---- phase 2: the transfers (all posted at once), then the root's fix-ups
+        c->tp->group_start();
+        for (const Piece& p : pieces) {
+            if (c->rank == root) {
+                if (p.r == root) HIP_TRY(hipMemcpyAsync(p.dst, p.src, p.nb, hipMemcpyDeviceToDevice, st));
+                else c->tp->recv(ctx, p.dst, p.nb, p.r);
+            } else {
+                c->tp->send(ctx, p.src, p.nb, root);
+            }
+        }
+        c->tp->group_end(ctx);
+        if (c->rank == root) {
+            for (const Piece& p : pieces) {
+                if (p.fix < 0) continue;
+                int64_t row0 = 0, b0 = 0;
+                for (int q = 0; q < p.r; ++q) {
+                    row0 += rec(q, 2);
+                    b0 += rec(q, 3 + p.o);
+                }
+                const int64_t n = rec(p.r, 2);
+                if (p.fix == 0)
+                    HIP_TRY(launch_rebase_offsets((const int32_t*)p.dst, n, b0, root_outs[p.o].offsets + row0, st));
+                else
+                    HIP_TRY(launch_place_bits((const uint8_t*)p.dst, n,
+                                              p.fix == 1 ? (uint8_t*)root_outs[p.o].values : root_outs[p.o].validity,
+                                              row0, st));
             }
             HIP_TRY(hipStreamSynchronize(st));
-        } catch (...) {
-            for (uint8_t* p : stage) (void)hipFree(p);
-            throw;
         }
         for (uint8_t* p : stage) (void)hipFree(p);
         return DFMI_OK;
     } catch (const Fail& f) {
+        (void)hipStreamSynchronize(ctx->stream);
+        for (uint8_t* p : stage) (void)hipFree(p);
         set_err(err, f.code, f.msg);
         return f.code;
     }
@@ -331,37 +507,70 @@ extern "C" int32_t dfmi_shard_agg_finish(dfmi_context* ctx, dfmi_shard_comm* c, 
                                          const dfmi_aggregate* const* aggs, int32_t n, dfmi_agg_value* out,
                                          dfmi_error* err) {
     set_err(err, DFMI_OK, "");
-    uint8_t* d = nullptr;
     try {
         if (!ctx || !c || !state || !aggs || !out) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         const int64_t nb = dfmi_agg_partial_bytes(state);
-        // a failed state still takes part (all ranks must enter the collective)
-        std::vector<uint8_t> mine((size_t)nb + 8, 0), all((size_t)(nb + 8) * c->world);
+        // [status | message | partial]: a failed state still takes part (all
+        // ranks enter the collective) and every rank reports the first
+        // failing rank's error
+        const size_t rec = 8 + kMsg + (size_t)nb;
+        std::vector<uint8_t> mine(rec, 0), all(rec * c->world);
         dfmi_error local;
-        int32_t rc = dfmi_agg_state_partial(ctx, state, mine.data() + 8, &local);
+        const int32_t rc = dfmi_agg_state_partial(ctx, state, mine.data() + 8 + kMsg, &local);
         memcpy(mine.data(), &rc, 4);
-        hipStream_t st = ctx->stream;
-        HIP_TRY(hipMalloc((void**)&d, all.size()));
-        HIP_TRY(hipMemcpyAsync(d + (size_t)c->rank * (nb + 8), mine.data(), nb + 8, hipMemcpyHostToDevice, st));
-        NCCL_TRY(ncclAllGather(d + (size_t)c->rank * (nb + 8), d, nb + 8, ncclUint8, c->comm, st));
-        HIP_TRY(hipMemcpyAsync(all.data(), d, all.size(), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        (void)hipFree(d);
-        d = nullptr;
+        if (rc) snprintf((char*)mine.data() + 8, kMsg, "%s", local.message);
+        c->tp->all_gather(ctx, mine.data(), all.data(), rec);
         for (int r = 0; r < c->world; ++r) {
             int32_t rr;
-            memcpy(&rr, &all[(size_t)r * (nb + 8)], 4);
+            memcpy(&rr, &all[(size_t)r * rec], 4);
             if (rr) {
-                if (r == c->rank) throw Fail{rc, local.message};
-                throw Fail{rr, "aggregate failed on rank " + std::to_string(r)};
+                all[(size_t)r * rec + 8 + kMsg - 1] = 0;
+                throw Fail{rr, std::string((const char*)&all[(size_t)r * rec + 8])};
             }
         }
         std::vector<const void*> parts(c->world);
-        for (int r = 0; r < c->world; ++r) parts[r] = &all[(size_t)r * (nb + 8) + 8];
+        for (int r = 0; r < c->world; ++r) parts[r] = &all[(size_t)r * rec + 8 + kMsg];
         return dfmi_agg_merge_partials(aggs, n, parts.data(), c->world, out, err);
     } catch (const Fail& f) {
-        if (d) (void)hipFree(d);
         set_err(err, f.code, f.msg);
         return f.code;
     }
+}
+
+// ------------------------------------------------------------ test hooks
+// Internal (not in include/): the C++ placement / error agreement over
+// records laid out as ShardedFilterProject.exchange's (execution/shard.py) --
+// the CPU suite checks both agree at world sizes 2 and 3 -- and a loopback
+// communicator (threads sharing one device) for the GPU suite's
+// multi-rank runs of the shard entry points on a one-GPU box.
+extern "C" int32_t dfmi_internal_shard_place(int32_t world, int32_t rank, int32_t nout, const int64_t* recs,
+                                             dfmi_shard_placement* out, int32_t* first_failed) {
+    if (world < 1 || rank < 0 || rank >= world || nout < 0 || nout > kMaxOut || !recs || !out || !first_failed)
+        return DFMI_ERR_INVALID_ARGUMENT;
+    *first_failed = first_failed_rank(recs, world, kRec);
+    placement_of(recs, world, rank, nout, kRec, out);
+    return DFMI_OK;
+}
+
+extern "C" void* dfmi_internal_loopback_group_create(int32_t world) {
+    return world >= 1 ? new LoopGroup(world) : nullptr;
+}
+extern "C" void dfmi_internal_loopback_group_destroy(void* g) { delete (LoopGroup*)g; }
+
+extern "C" int32_t dfmi_internal_shard_comm_loopback(dfmi_context* ctx, void* group, int32_t rank,
+                                                     dfmi_shard_comm** out, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    LoopGroup* g = (LoopGroup*)group;
+    if (!ctx || !g || !out || rank < 0 || rank >= g->world) {
+        set_err(err, DFMI_ERR_INVALID_ARGUMENT, "bad argument");
+        return DFMI_ERR_INVALID_ARGUMENT;
+    }
+    auto* c = new dfmi_shard_comm();
+    c->world = g->world;
+    c->rank = rank;
+    c->device = ctx->device;
+    c->tp = new LoopTransport(g, rank);
+    c->rec.assign((size_t)c->world * kRec, 0);
+    *out = c;
+    return DFMI_OK;
 }

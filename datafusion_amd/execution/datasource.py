@@ -99,11 +99,15 @@ class NativeCsvDataSource(DataSource):
     """CsvDataSource over the native reader (dfmi_csv_open, include/dfmi_datasource.h):
     host threads parse straight into pinned Arrow buffers and the next batch
     is parsed while the caller works on this one. Same batches as
-    CsvDataSource; each stays valid until the next ``next()`` (the reference's
-    pull order), or pass ``copy=True`` to keep them."""
+    CsvDataSource. By default each batch is copied out of the reader's pinned
+    buffers, so it can be kept. ``copy=False`` hands out zero-copy views of
+    those buffers instead: such a batch is valid only until the next
+    ``next()`` (the reference's pull order: csv_sql.rs:60-62 consumes each
+    batch before pulling the next); it holds a reference to this source, so
+    its memory is never freed under it, but the next batch overwrites it."""
 
     def __init__(self, schema: Schema, path: str, has_header: bool = True, batch_size: int = 1024,
-                 threads: int = 0, copy: bool = False):
+                 threads: int = 0, copy: bool = True):
         import ctypes as C
         from .. import _abi
         self._schema = schema
@@ -164,7 +168,10 @@ class NativeCsvDataSource(DataSource):
             else:
                 nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
                 cols.append(Array(t, n, view(c.values, nb), vb, None, c.null_count))
-        return RecordBatch(self._schema, cols)
+        rb = RecordBatch(self._schema, cols)
+        if not self._copy:
+            rb._source = self  # the views' memory lives as long as the batch
+        return rb
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -337,6 +337,29 @@ class ShardComm:
         self.outputs = None
         self.keep = None
 
+    @classmethod
+    def loopback(cls, eng: DeviceEngine, group, rank: int) -> "ShardComm":
+        """Test-only communicator: `rank` of a loopback group of host threads
+        sharing one device (csrc/shard.cpp LoopTransport), so the shard entry
+        points run at world sizes > 1 on a one-GPU box."""
+        L = _abi.lib()
+        fn = L.dfmi_internal_shard_comm_loopback
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(_abi.dfmi_error)]
+        fn.restype = C.c_int32
+        self = cls.__new__(cls)
+        self.eng = eng
+        self.world, self.rank = None, rank
+        out = C.c_void_p()
+        err = _abi.dfmi_error()
+        rc = fn(eng.ctx, group, rank, C.byref(out), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        self.handle = out
+        self.placement = None
+        self.outputs = None
+        self.keep = None
+        return self
+
     def gather_to_root(self, cols: List[Array], root: int = 0) -> Optional[List[Array]]:
         """The last shard pass's outputs concatenated on `root` (collective)."""
         place = self.placement

@@ -92,6 +92,16 @@ class ShardedFilterProject:
         except ExecutionError as e:
             # still take part in the exchange: every rank must learn the query failed
             return self.exchange(None, e)
+        except Exception as e:
+            # any other failure (device OOM, a bad argument) also joins the
+            # exchange -- the other ranks would block in it otherwise -- then
+            # re-raises here; the other ranks raise an ExecutionError
+            try:
+                self.exchange(None, ExecutionError("ExecutionError", "shard %d failed: %s: %s" % (
+                    dist.get_rank(self.group), type(e).__name__, e)))
+            except ExecutionError:
+                pass
+            raise
         return self.exchange(cols)
 
     def exchange(self, cols: Optional[List[Array]], error: Optional[ExecutionError] = None) -> ShardResult:
@@ -103,16 +113,8 @@ class ShardedFilterProject:
         world = dist.get_world_size(self.group)
         rank = dist.get_rank(self.group)
         nout = len(cols) if cols is not None else max(1, len(self.projections))
-        if error is None:
-            rows = cols[0].length if cols else 0
-            mine = [0, 0, rows] + [c.data_bytes() if c.data_type == DataType.Utf8 else 0 for c in cols] + \
-                   [c.null_count for c in cols]
-        else:
-            pos = (getattr(error, "order_key", None) or ((1 << 64) - 1)) >> 44
-            mine = [error.code or _abi.DFMI_ERR_EXECUTION, pos, 0] + [0] * (2 * nout)
-        # every rank sends the same record length (failed ranks pad)
+        mine = shard_record(cols, error, nout)
         width = 3 + 2 * _MAX_OUT
-        mine = mine[:3] + _pad(mine[3:3 + nout], _MAX_OUT) + _pad(mine[3 + nout:], _MAX_OUT)
         allc = exchange_counts(mine, self.group)
         failed = [r for r in range(world) if allc[r][0]]
         if failed:
@@ -130,6 +132,22 @@ class ShardedFilterProject:
 
 _MAX_OUT = 16
 _MSG = 512
+
+
+def shard_record(cols: Optional[List[Array]], error: Optional[ExecutionError], nout: int) -> List[int]:
+    """This rank's exchange record, the layout csrc/shard.cpp exchanges too:
+    [status, error position (evaluation-order key >> 44; none sorts last),
+    rows, Utf8 bytes per output (16), nulls per output (16)]."""
+    if error is None:
+        rows = cols[0].length if cols else 0
+        mine = [0, 0, rows] + [c.data_bytes() if c.data_type == DataType.Utf8 else 0 for c in cols] + \
+               [c.null_count for c in cols]
+    else:
+        key = getattr(error, "order_key", None)
+        pos = (((1 << 64) - 1) if key is None else key) >> 44
+        mine = [error.code or _abi.DFMI_ERR_EXECUTION, pos, 0] + [0] * (2 * nout)
+    # every rank sends the same record length (failed ranks pad)
+    return mine[:3] + _pad(mine[3:3 + nout], _MAX_OUT) + _pad(mine[3 + nout:], _MAX_OUT)
 
 
 def _pad(xs, n):
@@ -277,4 +295,4 @@ def concat_host(shards: Sequence[ShardResult]) -> List[List]:
     return cols or []
 
 
-__all__ = ["shard_range", "exchange_counts", "ShardResult", "ShardedFilterProject", "gather_to_root", "concat_host"]
+__all__ = ["shard_range", "exchange_counts", "shard_record", "ShardResult", "ShardedFilterProject", "gather_to_root", "concat_host"]

@@ -292,6 +292,11 @@ int32_t dfmi_last_timing(const dfmi_context* ctx, double* total_ms, double* main
  * the programs and the batch's column types / nullability). */
 int32_t dfmi_last_compile_ms(const dfmi_context* ctx, double* compile_ms);
 
+/* Name of the query kernel the last dfmi_filter_project / dfmi_aggregate_batch
+ * on ctx launched: dfmi_<filter|project|agg>_<hash of the generated code>, as
+ * rocprofv3 reports it ("" before the first launch). Diagnostics. */
+const char* dfmi_last_kernel_name(const dfmi_context* ctx);
+
 /* Evaluation-order key of the error the last dfmi_filter_project on ctx
  * returned: (position of the failing operator in the reference's evaluation
  * order) << 44 | row << 4; all ones when it returned no such error. Lets a

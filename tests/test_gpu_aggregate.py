@@ -214,3 +214,29 @@ def test_q6_sum_through_sql():
     assert int(got) == ref.bits
     m = (cols[3] >= 8766) & (cols[3] < 9131) & (cols[2] >= 0.05) & (cols[2] <= 0.07) & (cols[0] < 24)
     assert abs(agg_value_py(ref) - float((cols[1] * cols[2])[m].sum())) < 1e-3
+
+
+# ---------------------------------------------------------- round-3 fixtures
+def test_sql_min_max_fixture_on_gpu():
+    """expected/test_sql_min_max.csv on the device, through ctx.sql()."""
+    from golden_cases import CITIES, MIN_MAX_SQL, agg_fixture_value, expected_rows, load_batch
+    batch = load_batch(CITIES, "uk_cities.csv", has_header=False)
+    ctx = ExecutionContext(flags=AGG)
+    ctx.register_datasource("uk_cities", MemoryDataSource(CITIES, [batch.to(engine().device)]))
+    out = ctx.sql(MIN_MAX_SQL).next()
+    got = [int(c.cpu().numpy_values().view(np.uint64)[0]) for c in out.columns]
+    want = expected_rows("test_sql_min_max.csv")[0]
+    assert got == [agg_fixture_value(w, DataType.Float64) for w in want]
+
+
+def test_csv_aggregate_all_types_fixture_on_gpu():
+    """expected/csv_aggregate_all_types.csv columns 1-10 and the counts on
+    the device, bit-identical to the oracle and to the fixture cells."""
+    from golden_cases import agg_fixture_value, all_types_typed, load_batch
+    from test_oracle_golden import _agg_plan, all_types_aggregates
+    s = all_types_typed()
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    for sql, cells, types in all_types_aggregates():
+        dev = run_agg(s, batch, None, _agg_plan(sql, s, "t"))
+        assert [d.bits for d in dev] == [agg_fixture_value(c, t) for c, t in zip(cells, types)], sql
+        dev = run_agg(s, batch, None, _agg_plan(sql, s, "t"), batch_rows=64)  # many batches

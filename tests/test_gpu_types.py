@@ -230,3 +230,26 @@ def test_is_null_every_type():
     e = BinaryExpr(Column(2), Operator.Multiply, Column(2))
     run_both(s, bt, BinaryExpr(IsNull(e), Operator.Or, BinaryExpr(Column(9), Operator.Gt, Column(9))),
              [IsNotNull(e), e], EXT)
+
+
+# ---------------------------------------------------------- round-3 fixtures
+from golden_cases import RANGE_CASES, WHOLE_F32_FILES, range_fixture_case, whole_f32_case  # noqa: E402
+
+
+@pytest.mark.parametrize("case", RANGE_CASES, ids=[c[0] for c in RANGE_CASES])
+def test_int8_range_inclusive_on_gpu(case):
+    """expected/c_int8_range_inclusive.csv (98 rows) on the device."""
+    s, pred, projs = range_fixture_case(*case)
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    assert run_both(s, batch, pred, projs) is None  # "filter not supported for Int8"
+    dev, _ = run_both(s, batch, pred, projs, GA)
+    assert dev[0].cpu().to_pylist() == fixture_values(case[0], ALL_TYPES[case[1]])
+
+
+@pytest.mark.parametrize("name", WHOLE_F32_FILES)
+def test_float32_uint32_files_on_gpu(name):
+    """expected/c_float32_*_uint32.csv: the whole c_float32 column (CAST(c9 AS UInt32) = 0)."""
+    s, pred, projs = whole_f32_case()
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    dev, _ = run_both(s, batch, pred, projs, EXT)
+    assert dev[0].cpu().to_pylist() == fixture_values(name, DataType.Float32)

@@ -97,7 +97,7 @@ def test_c2_kernel_compiles():
     pred, projs = c2_query()
     rc, code, msg, src = jit_check(F3, pred, projs, compile_=True)
     assert rc > 0, msg
-    assert 'extern "C" __global__' in src and "dfmi_query" in src
+    assert 'extern "C" __global__' in src and "void dfmi_filter_" in src
     # literals are kernel arguments: another k/m generates the same source
     rc2, _, _, src2 = jit_check(F3, *c2_query(0.1, 0.9))
     assert src2 == src

@@ -109,3 +109,171 @@ def test_two_contexts_two_threads_host_path():
     for t in th:
         t.join(100)
     assert not errors, errors[0]
+
+
+# ---- world sizes > 1 on one device: the loopback transport (csrc/shard.cpp
+# LoopTransport: host threads, one context each, device-to-device copies)
+# runs the same C++ placement, error agreement, grouped send/recv gather and
+# root fix-ups (offset rebase, bit placement) that RCCL drives across GPUs.
+def loop_world(world, fn, timeout=120):
+    import ctypes as C
+
+    import torch
+    L = _abi.lib()
+    L.dfmi_internal_loopback_group_create.argtypes = [C.c_int32]
+    L.dfmi_internal_loopback_group_create.restype = C.c_void_p
+    L.dfmi_internal_loopback_group_destroy.argtypes = [C.c_void_p]
+    g = L.dfmi_internal_loopback_group_create(world)
+    out, errors = [None] * world, []
+
+    def work(rank):
+        try:
+            torch.cuda.set_device(0)
+            with torch.cuda.stream(torch.cuda.Stream()):
+                eng = DeviceEngine(0)
+                comm = ShardComm.loopback(eng, g, rank)
+                out[rank] = fn(rank, eng, comm)
+                torch.cuda.current_stream().synchronize()
+        except Exception as e:  # noqa: BLE001
+            out[rank] = e
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in th), "a rank is blocked in a collective"
+    L.dfmi_internal_loopback_group_destroy(g)
+    return out
+
+
+def shard_of(b, rank, world):
+    from datafusion_amd.execution.shard import shard_range
+    lo, hi = shard_range(b.num_rows(), rank, world)
+    cols = []
+    for a in b.columns:
+        h = a.cpu()
+        if a.data_type == DataType.Utf8:
+            vals = h.to_pylist()[lo:hi]
+            cols.append(Array.from_strings([v.encode() for v in vals]))
+        else:
+            v = np.asarray(h.numpy_values())[lo:hi]
+            valid = None
+            if h.validity is not None:
+                from datafusion_amd.arrow import unpack_bits
+                valid = unpack_bits(h.validity.numpy(), b.num_rows())[lo:hi].astype(bool)
+            cols.append(Array.from_numpy(a.data_type, v, valid))
+    return RecordBatch(b.schema, cols)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_loopback_shards_place_and_gather(world):
+    s, b = table(100_003)
+    pred_e = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.4)))
+    proj_e = [Column(2), BinaryExpr(Column(0), Operator.Multiply, Column(1)), Column(0)]
+    ref = oracle_filter_project(s, b, pred_e, proj_e)
+    nsel = ref[0][1].length
+
+    def fn(rank, eng, comm):
+        pred = compile_scalar_expr(None, pred_e, s)
+        projs = [compile_scalar_expr(None, e, s) for e in proj_e]
+        cols = eng.filter_project(pred, projs, shard_of(b, rank, world), 0, comm=comm)
+        p = comm.placement
+        full = comm.gather_to_root(cols, root=world - 1)  # a root that is not rank 0
+        return (p.row_offset, p.total_rows, p.utf8_base[0], p.utf8_total[0],
+                [c.cpu() for c in cols], None if full is None else [c.cpu() for c in full])
+
+    out = loop_world(world, fn)
+    assert not [o for o in out if isinstance(o, Exception)], out
+    off = 0
+    for rank, (row_off, tot, ubase, utot, cols, full) in enumerate(out):
+        assert (row_off, tot) == (off, nsel)
+        assert utot == ref[0][1].data_bytes()
+        assert ubase == sum(len(x.encode()) for x in ref[0][1].to_pylist()[:off])
+        for d, (_, r) in zip(cols, ref):
+            assert d.to_pylist() == r.to_pylist()[off:off + cols[0].length]
+        off += cols[0].length
+        assert (full is not None) == (rank == world - 1)
+    for d, (_, r) in zip(out[-1][5], ref):
+        assert_same(d, r)
+
+
+def test_loopback_dense_bits_and_validity_gather():
+    """Projection only (no predicate): a nullable Float64 sum and a Boolean
+    comparison -- validity and value bitmaps placed at row offsets that are
+    not multiples of 8 on the root."""
+    s, b = table(50_001)
+    proj_e = [BinaryExpr(Column(0), Operator.Plus, Column(1)), BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5)))]
+    ref = oracle_filter_project(s, b, None, proj_e)
+
+    def fn(rank, eng, comm):
+        projs = [compile_scalar_expr(None, e, s) for e in proj_e]
+        cols = eng.filter_project(None, projs, shard_of(b, rank, 3), 0, comm=comm)
+        full = comm.gather_to_root(cols, root=0)
+        return None if full is None else [c.cpu() for c in full]
+
+    out = loop_world(3, fn)
+    assert not [o for o in out if isinstance(o, Exception)], out
+    for d, (_, r) in zip(out[0], ref):
+        assert_same(d, r)
+
+
+def test_loopback_first_error_everywhere():
+    """Rank 1 alone divides by zero: every rank raises the same error (none blocks)."""
+    s, b = table(30_000)
+    e = BinaryExpr(Column(0), Operator.Divide, BinaryExpr(Column(0), Operator.Minus, Column(0)))
+    pred_e = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.5)))
+
+    def fn(rank, eng, comm):
+        pred = compile_scalar_expr(None, pred_e, s)
+        pe = BinaryExpr(Column(0), Operator.Plus, Column(0)) if rank != 1 else e
+        projs = [compile_scalar_expr(None, pe, s)]
+        try:
+            eng.filter_project(pred, projs, shard_of(b, rank, 3), 0, comm=comm)
+        except ExecutionError as x:
+            return (x.kind, x.message)
+        return None
+
+    out = loop_world(3, fn)
+    assert out == [("ArrowError(DivideByZero)", "DivideByZero")] * 3, out
+
+
+def test_loopback_gather_checks_are_collective():
+    """the root's Utf8 data_capacity too small fails EVERY rank
+    with the root's error before any transfer (no rank left in a send)."""
+    import ctypes as C
+    s, b = table(40_000)
+    pred_e = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.5)))
+
+    def fn(rank, eng, comm):
+        pred = compile_scalar_expr(None, pred_e, s)
+        projs = [compile_scalar_expr(None, Column(2), s)]
+        cols = eng.filter_project(pred, projs, shard_of(b, rank, 2), 0, comm=comm)
+        routs = (_abi.dfmi_out_column * 1)()
+        keep = None
+        if rank == 0:
+            oc, keep = eng._alloc_out(DataType.Utf8, comm.placement.total_rows, False, 16)  # far too small
+            routs[0] = oc
+        err = _abi.dfmi_error()
+        rc = _abi.lib().dfmi_shard_gather_to_root(eng.ctx, comm.handle, comm.outputs, routs, 0, C.byref(err))
+        del keep, cols
+        return rc, err.message.decode()
+
+    out = loop_world(2, fn)
+    assert out == [(_abi.DFMI_ERR_CAPACITY, "root Utf8 data_capacity too small")] * 2, out
+
+
+def test_loopback_aggregate_finish():
+    s, b = table(90_000)
+    fl = _abi.DFMI_FLAG_EXT_AGGREGATE
+    aggs_e = [agg("SUM", Column(1), s), agg("MIN", Column(0), s), agg("COUNT", Column(2), s)]
+    ref = oracle_aggregate(s, b, None, aggs_e, fl)
+
+    def fn(rank, eng, comm):
+        aggs = [compile_expr(None, a, s, fl) for a in aggs_e]
+        st = eng.agg_state(aggs)
+        st.add(None, shard_of(b, rank, 3), fl)
+        return [(v.bits, v.count, v.is_null) for v in comm.agg_finish(st)]
+
+    out = loop_world(3, fn)
+    for got in out:
+        assert got == [(r.bits, r.count, r.is_null) for r in ref], got

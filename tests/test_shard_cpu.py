@@ -192,3 +192,99 @@ def test_failing_shard_raises_the_first_error_everywhere(plan, want):
     errs = [o for o in out if o[0] == "error"]
     assert not errs, errs[0][1]
     assert all((o[1], o[2]) == want for o in out), out
+
+
+def _place_worker(rank, world, port, dense, plan, q):
+    """The C++ placement / error agreement (csrc/shard.cpp, through the internal
+    hook dfmi_internal_shard_place) over the records this rank's Python
+    exchange all_gathers, against ShardedFilterProject.exchange's outcome."""
+    try:
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        from datafusion_amd import _abi
+        from datafusion_amd.execution.error import ExecutionError
+        from datafusion_amd.execution.shard import ShardedFilterProject, exchange_counts, shard_record
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = shard_range(N, rank, world)
+        batch, raw = table(lo, hi, nullable=dense)
+        failure = plan[rank] if plan else None
+
+        def run(p, e, bt, f):
+            if failure is None:
+                return numpy_pass(raw, dense)
+            code, msg, pos = failure
+            err = ExecutionError.from_status(code, msg)
+            err.order_key = None if pos is None else (pos << 44) | (5 << 4)
+            raise err
+
+        step = ShardedFilterProject(None if dense else PRED, DENSE if dense else PROJS, run_shard=run)
+        py = None
+        try:
+            res = step(batch)
+            py = ("ok", res.row_offset, res.total_rows, res.utf8_base,
+                  [sum(c[1 + o] for c in res.counts) for o in range(len(res.columns))],
+                  [sum(c[1 + len(res.columns) + o] for c in res.counts) for o in range(len(res.columns))])
+            cols, e = res.columns, None
+            nout = len(cols)
+        except ExecutionError as ex:
+            py = ("error", ex.code, ex.message)
+            cols, e = None, ex
+            nout = len(DENSE if dense else PROJS)
+        if failure is not None:  # this rank's own error, as its pass raised it
+            e = ExecutionError.from_status(failure[0], failure[1])
+            e.order_key = None if failure[2] is None else (failure[2] << 44) | (5 << 4)
+            mine = shard_record(None, e, nout)
+        else:
+            mine = shard_record(numpy_pass(raw, dense), None, nout)
+        recs = exchange_counts(mine)
+        L = _abi.lib()
+        fn = L.dfmi_internal_shard_place
+        fn.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int64), C.POINTER(_abi.dfmi_shard_placement),
+                       C.POINTER(C.c_int32)]
+        fn.restype = C.c_int32
+        flat = (C.c_int64 * (world * len(recs[0])))(*[v for r in recs for v in r])
+        place = _abi.dfmi_shard_placement()
+        first = C.c_int32()
+        assert fn(world, rank, nout, flat, C.byref(place), C.byref(first)) == 0
+        cpp = ("ok", place.row_offset, place.total_rows, list(place.utf8_base[:nout]), list(place.utf8_total[:nout]),
+               list(place.null_total[:nout])) if first.value < 0 else ("error", recs[first.value][0], first.value)
+        q.put((rank, py, cpp))
+        dist.destroy_process_group()
+    except Exception as ex:  # noqa: BLE001
+        import traceback
+        q.put(("error", traceback.format_exc(), str(ex)))
+
+
+@pytest.mark.parametrize("world,dense,plan", [
+    (2, False, None), (3, False, None), (2, True, None),
+    (3, False, [None, (5, "DivideByZero", 3), None]),
+    (3, False, [(7, "attempt to divide with overflow", 9), None, (5, "DivideByZero", 4)]),
+    (3, False, [None, (7, "attempt to divide with overflow", 4), (5, "DivideByZero", 4)]),
+    (2, False, [(10, "device look-back timed out", None), (5, "DivideByZero", 0)]),  # unkeyed sorts last
+    (2, False, [(5, "DivideByZero", 0), None]),  # position 0 is the first, not "none"
+])
+def test_cpp_placement_agrees_with_python_exchange(world, dense, plan):
+    """the C-ABI path's placement / error agreement
+    (csrc/shard.cpp first_failed_rank + placement_of) and the Python
+    ShardedFilterProject.exchange give the same outcome for the same records."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_place_worker, args=(r, world, port, dense, plan, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    errs = [o for o in out if o[0] == "error"]
+    assert not errs, errs[0][1]
+    for rank, py, cpp in out:
+        if py[0] == "ok":
+            assert cpp == py, (rank, py, cpp)
+        else:
+            # the same failing rank's code (and so its message) on every rank
+            assert cpp[0] == "error" and cpp[1] == py[1], (rank, py, cpp)
+            assert plan[cpp[2]] is not None and plan[cpp[2]][1] == py[2]
