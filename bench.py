@@ -296,6 +296,11 @@ def batches_line(eng, schema, cols, sel, dev):
     for m, calls in ((1024, 4000), (1 << 20, 400)):
         outs = [torch.empty(m, dtype=torch.float64, device=dev) for _ in range(3)]
         step = FusedStep(eng, schema, cols, m, *query(sel), outs)
+        if m == 1024:  # right after the 1e9-row launches: the workspace-clearing cliff
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            step()
+            out["first_1024_call_after_large_us"] = round((time.perf_counter() - t0) * 1e6, 1)
         for _ in range(50):
             step()
         torch.cuda.synchronize(dev)
@@ -315,6 +320,8 @@ def batches_line(eng, schema, cols, sel, dev):
                               "kernel_us": round(kern / 200 * 1e3, 2),
                               "host_overhead_us": round(us - kern / 200 * 1e3, 2), "calls": calls,
                               "rows_per_s": m / (us * 1e-6)}
+    out["1024_rows_x256_coalesced"] = coalesced_batches(eng, schema, cols, sel, dev, 1024, 256)
+    out["1024_rows_host"] = host_small_batches(eng, schema, sel, 1024)
     # a new query shape: generate + hipRTC compile on the first call, cached after
     pred, projs = query(sel)
     pred = BinaryExpr(pred, Operator.And, BinaryExpr(Column(2), Operator.GtEq, Literal(Float64(0.0))))
@@ -330,6 +337,103 @@ def batches_line(eng, schema, cols, sel, dev):
     out["first_call"] = {"compile_ms": round(cm.value, 1), "first_call_ms": round(first_ms, 1),
                          "second_call_ms": round((time.perf_counter() - t0) * 1e3, 3)}
     return out
+
+
+def coalesced_batches(eng, schema, cols, sel, dev, m, nb, calls=300):
+    """dfmi_filter_project_batches: `nb` consecutive m-row batches of the
+    resident table (each with its own buffers and outputs, one output batch
+    per input batch) in one launch per call. Gate: every batch's outputs
+    equal dfmi_filter_project's on that batch alone."""
+    pred_e, proj_e = query(sel)
+    pred = compile_scalar_expr(None, pred_e, schema)
+    projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+    progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
+    carrs = []
+    cb = (_abi.dfmi_batch * nb)()
+    for i in range(nb):
+        carr = (_abi.dfmi_column * 3)()
+        for j, t in enumerate(cols):
+            carr[j].type = int(DataType.Float64)
+            carr[j].length = m
+            carr[j].values = t.data_ptr() + i * m * 8
+        carrs.append(carr)
+        cb[i].num_columns, cb[i].num_rows, cb[i].columns = 3, m, carr
+    obuf = torch.empty((nb, 3, m), dtype=torch.float64, device=dev)
+    outs = (_abi.dfmi_out_column * (nb * 3))()
+    for i in range(nb):
+        for j in range(3):
+            outs[i * 3 + j].values = obuf[i, j].data_ptr()
+    L = _abi.lib()
+    err = _abi.dfmi_error()
+    failed = C.c_int32()
+
+    def call():
+        rc = L.dfmi_filter_project_batches(eng.ctx, pred.handle, progs, 3, cb, nb, outs, 0, C.byref(failed),
+                                           C.byref(err))
+        if rc != 0:
+            raise RuntimeError(err.message.decode())
+    for _ in range(20):
+        call()
+    L.dfmi_context_set_timing(eng.ctx, 0)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        call()
+    el = (time.perf_counter() - t0) / calls
+    L.dfmi_context_set_timing(eng.ctx, 1)
+    kern = 0.0
+    for _ in range(50):
+        call()
+        kern += eng.last_timing()[1]
+    kname = kernel_name(eng)
+    # gate against the single-batch entry point, batch by batch
+    lens = [outs[i * 3].length for i in range(nb)]
+    ok = True
+    single = [torch.empty(m, dtype=torch.float64, device=dev) for _ in range(3)]
+    for i in range(0, nb, max(1, nb // 16)):
+        st = FusedStep(eng, schema, [c[i * m:(i + 1) * m] for c in cols], m, pred_e, proj_e, single)
+        k = st()
+        ok = ok and k == lens[i] and all(torch.equal(single[j][:k].view(torch.int64), obuf[i, j, :k].view(torch.int64))
+                                         for j in range(3))
+    return {"kernel": kname, "batches_per_call": nb, "rows_per_batch": m, "us_per_call": round(el * 1e6, 2),
+            "us_per_batch": round(el * 1e6 / nb, 3), "kernel_us_per_call": round(kern / 50 * 1e3, 2),
+            "rows_per_s": nb * m / el, "selected_last_call": int(sum(lens)),
+            "matches_single_batch_calls": bool(ok)}
+
+
+def host_small_batches(eng, schema, sel, m, calls=2000):
+    """dfmi_filter_project_host (what the Rust binding calls with arrow 0.12
+    host buffers) on one m-row host batch per call."""
+    from oracle_ffi import gen_unit_f64
+    host = [gen_unit_f64(SEED, j, 0, m) for j in range(3)]
+    pred_e, proj_e = query(sel)
+    pred = compile_scalar_expr(None, pred_e, schema)
+    projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+    progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
+    carr = (_abi.dfmi_column * 3)()
+    for j, h in enumerate(host):
+        carr[j].type = int(DataType.Float64)
+        carr[j].length = m
+        carr[j].values = h.ctypes.data
+    cb = _abi.dfmi_batch(3, 0, m, carr)
+    L = _abi.lib()
+    err = _abi.dfmi_error()
+
+    def call():
+        res = C.c_void_p()
+        rc = L.dfmi_filter_project_host(eng.ctx, pred.handle, progs, 3, C.byref(cb), 0, C.byref(res), C.byref(err))
+        if rc != 0:
+            raise RuntimeError(err.message.decode())
+        L.dfmi_host_result_free(res)
+    for _ in range(50):
+        call()
+    L.dfmi_context_set_timing(eng.ctx, 0)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        call()
+    el = (time.perf_counter() - t0) / calls
+    L.dfmi_context_set_timing(eng.ctx, 1)
+    return {"us_per_batch": round(el * 1e6, 2), "rows_per_s": m / el, "calls": calls,
+            "note": "host buffers in, host results out (PCIe both ways), one synchronous call per batch"}
 
 
 def prefix_gate(eng, schema, dev_cols, m, pred_e, proj_e, flags=0):
@@ -769,7 +873,10 @@ def csv_line(eng, steps, warmup):
         out[name] = {"ms": round(el * 1e3, 1), "rows_per_s": n / el, "csv_gbs": round(size / el / 1e9, 2)}
         if name == "csv_sql_c2":
             out[name]["selected"] = r[1]
-    out["host_threads"] = int(os.environ.get("DFMI_CSV_THREADS", "0")) or min(8, os.cpu_count() or 1)
+    share = len(os.sched_getaffinity(0))
+    if int(os.environ.get("OMP_NUM_THREADS", "0") or 0) > 0:
+        share = min(share, int(os.environ["OMP_NUM_THREADS"]))
+    out["host_threads"] = int(os.environ.get("DFMI_CSV_THREADS", "0")) or max(1, min(share, 64))
     os.remove(path)
     os.rmdir(d)
     return out

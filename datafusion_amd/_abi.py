@@ -137,6 +137,7 @@ EXPORTED = [
     "dfmi_context_destroy",
     "dfmi_context_set_stream",
     "dfmi_filter_project",
+    "dfmi_filter_project_batches",
     "dfmi_filter_project_host",
     "dfmi_host_result_num_columns",
     "dfmi_host_result_column",
@@ -247,6 +248,10 @@ def lib() -> C.CDLL:
                                       C.POINTER(dfmi_batch), C.POINTER(dfmi_out_column), C.c_uint32,
                                       C.POINTER(dfmi_error)]
     L.dfmi_filter_project.restype = C.c_int32
+    L.dfmi_filter_project_batches.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                              C.POINTER(dfmi_batch), C.c_int32, C.POINTER(dfmi_out_column), C.c_uint32,
+                                              C.POINTER(C.c_int32), C.POINTER(dfmi_error)]
+    L.dfmi_filter_project_batches.restype = C.c_int32
     L.dfmi_filter_project_host.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
                                            C.POINTER(dfmi_batch), C.c_uint32, C.POINTER(C.c_void_p),
                                            C.POINTER(dfmi_error)]

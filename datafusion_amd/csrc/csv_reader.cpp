@@ -19,6 +19,7 @@
 // is ArrowError(ParseError) "Error while parsing value <field>".
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -539,6 +540,18 @@ struct dfmi_csv_reader {
     }
 };
 
+// Parse threads when the caller names none: the CPUs this process may run
+// on (its affinity mask, not the machine's count), capped by
+// OMP_NUM_THREADS when the host sets one (a shared box's CPU share) and at 64.
+static int default_parse_threads() {
+    int n = (int)std::thread::hardware_concurrency();
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (const char* e = getenv("OMP_NUM_THREADS"))
+        if (atoi(e) > 0) n = std::min(n, atoi(e));
+    return std::max(1, std::min(n, 64));
+}
+
 extern "C" int32_t dfmi_csv_open(const char* path, const dfmi_schema* schema, int32_t has_header, int64_t batch_size,
                                  int32_t threads, dfmi_csv_reader** out, dfmi_error* err) {
     set_err(err, DFMI_OK, "");
@@ -560,8 +573,7 @@ extern "C" int32_t dfmi_csv_open(const char* path, const dfmi_schema* schema, in
     R->batch_size = batch_size;
     if (threads <= 0)
         if (const char* e = getenv("DFMI_CSV_THREADS")) threads = atoi(e);
-    R->threads = threads > 0 ? std::min(threads, 64)
-                             : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    R->threads = threads > 0 ? std::min(threads, 64) : default_parse_threads();
     R->fd = open(path, O_RDONLY);
     if (R->fd < 0) {
         const std::string m = std::string(path) + ": " + strerror(errno);

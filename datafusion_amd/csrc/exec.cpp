@@ -285,6 +285,11 @@ extern "C" void dfmi_context_destroy(dfmi_context* c) {
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->utf8_src) (void)hipFree(c->utf8_src);
     if (c->host_hdr) (void)hipHostFree(c->host_hdr);
+    if (c->bmeta) (void)hipFree(c->bmeta);
+    if (c->bhdr) (void)hipFree(c->bhdr);
+    if (c->ones) (void)hipFree(c->ones);
+    if (c->host_bmeta) (void)hipHostFree(c->host_bmeta);
+    if (c->host_bhdr) (void)hipHostFree(c->host_bhdr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -315,6 +320,9 @@ extern "C" int32_t dfmi_last_error_order(const dfmi_context* c, uint64_t* key) {
     *key = c->last_err_key;
     return DFMI_OK;
 }
+
+// Internal test hook: look-back timeouts relaunched on this context.
+extern "C" long dfmi_internal_relaunches(const dfmi_context* c) { return c ? c->relaunches : -1; }
 
 extern "C" const char* dfmi_last_kernel_name(const dfmi_context* c) {
     return c ? c->last_kernel.c_str() : "";
@@ -436,75 +444,92 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             memcpy(A.str_off, X.str_off, sizeof A.str_off);
             memcpy(A.str_len, X.str_len, sizeof A.str_len);
             memcpy(A.str, X.str, sizeof A.str);
-            const WsLease ws = ws_acquire(ctx, status_bytes, st);
-            uint8_t* hdr = ws.hdr;
-            A.ticket = (unsigned*)(hdr + kHdrTicket);
-            A.err = (unsigned long long*)(hdr + kHdrErr);
-            A.totals = (unsigned long long*)(hdr + kHdrTotals);
-            A.status = (unsigned long long*)ws.status;
-            A.stats = (unsigned long long*)(hdr + kHdrStats);
-            A.clear_status = (unsigned long long*)ws.clear_status;
-            A.clear_words = ws.clear_words;
-            A.clear_hdr = (unsigned long long*)ws.clear_hdr;
-            A.mode = 0;
-            if (getenv("DFMI_DIAG"))
-                if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
-            const unsigned grid = (unsigned)n_tiles;  // one block per tile
-            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
-            size_t asz = sizeof A;
-            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
-            HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
-            ws_commit(ctx, ws);
-            if (two_pass && !(A.mode & 8))
-                for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
-                    const int o = X.utf8_outs[j].first;
-                    HIP_TRY(launch_utf8_copy_rows(A.out_offs[o], A.out_src[o], A.bytes[X.utf8_outs[j].second],
-                                                  A.out_data[o], A.totals, 1 + (int)j, A.out_cap[o], n, st));
+            // A look-back that made no progress for 2 s (ERRK_LOOKBACK_TIMEOUT:
+            // e.g. the GPU time-sliced away from this queue for that long) is
+            // relaunched once over a freshly zeroed workspace before it is
+            // reported as a device error; the relaunch rewrites every output.
+            for (int attempt = 0;; ++attempt) {
+                const WsLease ws = ws_acquire(ctx, status_bytes, st);
+                uint8_t* hdr = ws.hdr;
+                A.ticket = (unsigned*)(hdr + kHdrTicket);
+                A.err = (unsigned long long*)(hdr + kHdrErr);
+                A.totals = (unsigned long long*)(hdr + kHdrTotals);
+                A.status = (unsigned long long*)ws.status;
+                A.stats = (unsigned long long*)(hdr + kHdrStats);
+                A.clear_status = (unsigned long long*)ws.clear_status;
+                A.clear_words = ws.clear_words;
+                A.clear_hdr = (unsigned long long*)ws.clear_hdr;
+                if (attempt == 0) {
+                    A.mode = 0;
+                    if (getenv("DFMI_DIAG"))
+                        if (const char* m = getenv("DFMI_DEBUG_MODE")) A.mode = atoi(m);  // diagnostics only
                 }
-            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
-            for (int o = 0; o < nout; ++o)
-                if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
-            for (int o : valid_out)
-                HIP_TRY(launch_pack_bools(A.out_valid[o], outs[o].validity, A.totals, n, st));
-            auto t_d = tnow();
-            if (prof) ph[2] += tms(t_c, t_d);
-            auto t_e = tnow();
-            if (prof) ph[3] += tms(t_d, t_e);
-            HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
-            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev2, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            auto t_f = tnow();
-            if (prof) ph[4] += tms(t_e, t_f);
-            uint64_t ew;
-            memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
-            if (ew) {
-                dev_key = ~ew;
-                dev_kind = (int)(dev_key & 15);
-                dev_key &= ~15ull;
-            }
-            if (A.mode & 4) {
-                uint64_t st3[3];
-                memcpy(st3, ctx->host_hdr + kHdrStats, sizeof st3);
-                fprintf(stderr, "dfmi look-back: tiles %lld polls %llu sleeps %llu wait %.3f ms (summed over tiles)\n",
-                        (long long)n_tiles, (unsigned long long)st3[0], (unsigned long long)st3[1], st3[2] * 1e-5);
-            }
-            if (ctx->timing) {
-                float m1 = 0, m2 = 0;
-                (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
-                (void)hipEventElapsedTime(&m2, ctx->ev0, ctx->ev2);
-                ctx->last_main_ms = m1;
-                ctx->last_total_ms = m2;
-                ctx->timed = true;
-            }
-            if (prof) {
-                ph[5] += tms(t_f, tnow());
-                if (++ncalls % 1000 == 0)
-                    fprintf(stderr,
-                            "dfmi call (us, mean of 1000): plan %.2f, kernel lookup %.2f, launch %.2f, header "
-                            "copy %.2f, sync %.2f, timing %.2f\n",
-                            ph[0] / 1000, ph[1] / 1000, ph[2] / 1000, ph[3] / 1000, ph[4] / 1000, ph[5] / 1000);
-                if (ncalls % 1000 == 0)
-                    for (double& x : ph) x = 0;
+                const unsigned grid = (unsigned)n_tiles;  // one block per tile
+                if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
+                size_t asz = sizeof A;
+                void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+                HIP_TRY(hipModuleLaunchKernel(fn, grid, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
+                ws_commit(ctx, ws);
+                if (two_pass && !(A.mode & 8))
+                    for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+                        const int o = X.utf8_outs[j].first;
+                        HIP_TRY(launch_utf8_copy_rows(A.out_offs[o], A.out_src[o], A.bytes[X.utf8_outs[j].second],
+                                                      A.out_data[o], A.totals, 1 + (int)j, A.out_cap[o], n, st));
+                    }
+                if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
+                for (int o = 0; o < nout; ++o)
+                    if (bool_dst[o]) HIP_TRY(launch_pack_bools((const uint8_t*)A.out[o], bool_dst[o], A.totals, n, st));
+                for (int o : valid_out)
+                    HIP_TRY(launch_pack_bools(A.out_valid[o], outs[o].validity, A.totals, n, st));
+                auto t_d = tnow();
+                if (prof) ph[2] += tms(t_c, t_d);
+                auto t_e = tnow();
+                if (prof) ph[3] += tms(t_d, t_e);
+                HIP_TRY(hipMemcpyAsync(ctx->host_hdr, hdr, kHdrAlloc, hipMemcpyDeviceToHost, st));
+                if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev2, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                auto t_f = tnow();
+                if (prof) ph[4] += tms(t_e, t_f);
+                uint64_t ew;
+                memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
+                if (ew) {
+                    dev_key = ~ew;
+                    dev_kind = (int)(dev_key & 15);
+                    dev_key &= ~15ull;
+                }
+                if (A.mode & 4) {
+                    uint64_t st3[3];
+                    memcpy(st3, ctx->host_hdr + kHdrStats, sizeof st3);
+                    fprintf(stderr, "dfmi look-back: tiles %lld polls %llu sleeps %llu wait %.3f ms (summed over tiles)\n",
+                            (long long)n_tiles, (unsigned long long)st3[0], (unsigned long long)st3[1], st3[2] * 1e-5);
+                }
+                if (ctx->timing) {
+                    float m1 = 0, m2 = 0;
+                    (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
+                    (void)hipEventElapsedTime(&m2, ctx->ev0, ctx->ev2);
+                    ctx->last_main_ms = m1;
+                    ctx->last_total_ms = m2;
+                    ctx->timed = true;
+                }
+                if (prof) {
+                    ph[5] += tms(t_f, tnow());
+                    if (++ncalls % 1000 == 0)
+                        fprintf(stderr,
+                                "dfmi call (us, mean of 1000): plan %.2f, kernel lookup %.2f, launch %.2f, header "
+                                "copy %.2f, sync %.2f, timing %.2f\n",
+                                ph[0] / 1000, ph[1] / 1000, ph[2] / 1000, ph[3] / 1000, ph[4] / 1000, ph[5] / 1000);
+                    if (ncalls % 1000 == 0)
+                        for (double& x : ph) x = 0;
+                }
+                if (dev_kind == ERRK_LOOKBACK_TIMEOUT && attempt == 0) {
+                    ctx->ws_valid = false;  // status words in an unknown state: re-zero all
+                    ++ctx->relaunches;
+                    A.mode &= ~16;          // (diagnostic forced timeout: once)
+                    dev_kind = 0;
+                    dev_key = ~0ull;
+                    continue;
+                }
+                break;
             }
         }
 
@@ -549,6 +574,262 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
     }
 }
 
+// ------------------------------------------------------- coalesced batches
+// dfmi_filter_project over many batches in ONE launch (include/dfmi.h). Each
+// batch keeps its own outputs, row counts and errors: tiles never straddle
+// batches, a batch's tiles run the single-pass look-back over their own
+// status segment, and every batch has its own header (totals, null counts,
+// error word). The plan is built once from a "shape" batch -- the shared
+// column types, a column nullable when any batch has nulls in it.
+namespace {
+constexpr size_t kBHdr = 256;  // per-batch header: [0..8) totals, [8..24) nulls, [24] error word
+
+int32_t batches_one_by_one(dfmi_context* ctx, const dfmi_program* pred, const dfmi_program* const* projs, int32_t np,
+                           const dfmi_batch* ins, int32_t nb, dfmi_out_column* outs, int nout, uint32_t flags,
+                           int32_t* failed, dfmi_error* err) {
+    for (int32_t b = 0; b < nb; ++b) {
+        const int32_t rc = dfmi_filter_project(ctx, pred, projs, np, &ins[b], outs + (size_t)b * nout, flags, err);
+        if (rc != DFMI_OK) {
+            *failed = b;
+            return rc;
+        }
+    }
+    return DFMI_OK;
+}
+}  // namespace
+
+extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_program* pred,
+                                               const dfmi_program* const* projs, int32_t np, const dfmi_batch* ins,
+                                               int32_t nb, dfmi_out_column* outs, uint32_t flags,
+                                               int32_t* failed, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    int32_t dummy_failed;
+    if (!failed) failed = &dummy_failed;
+    *failed = -1;
+    if (ctx) ctx->last_err_key = ~0ull;
+    try {
+        if (!ctx || nb < 0 || (nb > 0 && (!ins || !outs)) || (np > 0 && !projs))
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        if (nb == 0) return DFMI_OK;
+        const int ncols = ins[0].num_columns;
+        const int nout = np > 0 ? np : ncols;
+        int64_t maxn = 0;
+        for (int32_t b = 0; b < nb; ++b) {
+            if (ins[b].num_columns != ncols || (ncols > 0 && !ins[b].columns))
+                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
+            for (int i = 0; i < ncols; ++i)
+                if (ins[b].columns[i].type != ins[0].columns[i].type)
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
+            maxn = std::max<int64_t>(maxn, ins[b].num_rows);
+        }
+        // the shape batch: shared types, nullable where any batch has nulls;
+        // the pointers only need to be non-NULL here (the plan reads types
+        // and nullability)
+        static const uint64_t kDummy[2] = {0, 0};
+        std::vector<dfmi_column> shape(ncols);
+        std::vector<char> nullable(ncols, 0);
+        for (int i = 0; i < ncols; ++i) {
+            for (int32_t b = 0; b < nb; ++b)
+                if (ins[b].columns[i].validity && ins[b].columns[i].null_count > 0) nullable[i] = 1;
+            dfmi_column& c = shape[i];
+            c = ins[0].columns[i];
+            c.length = maxn;
+            c.validity = nullable[i] ? (const uint8_t*)kDummy : nullptr;
+            c.null_count = nullable[i] ? 1 : 0;
+            c.values = kDummy;
+            c.offsets = (const int32_t*)kDummy;
+        }
+        const dfmi_batch shape_batch{ncols, 0, maxn, shape.data()};
+        Built B;
+        build_plan(pred, projs, np, &shape_batch, outs, flags, B);
+        jit::Plan& plan = B.plan;
+        jit::Launch& X = B.X;
+        bool one_by_one = B.se.set || X.gather == 3 || !(pred || B.any_kernel_out);
+        if (pred)  // filtered Boolean / nullable outputs are packed per batch after the kernel
+            for (const jit::OutSpec& os : plan.outs)
+                if (os.kind != jit::OutSpec::SKIP && os.kind != jit::OutSpec::UTF8 &&
+                    (os.out_type == DFMI_TYPE_BOOLEAN || os.nullable))
+                    one_by_one = true;
+        if (one_by_one) return batches_one_by_one(ctx, pred, projs, np, ins, nb, outs, nout, flags, failed, err);
+
+        X.batched = true;
+        HIP_TRY(hipSetDevice(ctx->device));
+        hipStream_t st = ctx->stream;
+        ctx->timed = false;
+        ctx->last_compile_ms = 0;
+        const hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
+        ctx->last_kernel = X.kname;
+
+        // ---- batch table
+        const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
+        std::vector<int64_t> first(nb), tiles(nb);
+        int64_t T = 0;
+        for (int32_t b = 0; b < nb; ++b) {
+            tiles[b] = (ins[b].num_rows + tile_rows - 1) / tile_rows;
+            first[b] = T;
+            T += tiles[b];
+        }
+        if (T > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
+        const int NPW = jit::batch_words(X, nout);
+        const size_t table_bytes = (size_t)nb * NPW * 8, meta_bytes = table_bytes + (size_t)T * 4;
+        ensure_host(&ctx->host_bmeta, &ctx->host_bmeta_bytes, meta_bytes);
+        ensure(ctx, &ctx->bmeta, &ctx->bmeta_bytes, meta_bytes);
+        ensure_host(&ctx->host_bhdr, &ctx->host_bhdr_bytes, (size_t)nb * kBHdr);
+        ensure(ctx, &ctx->bhdr, &ctx->bhdr_bytes, (size_t)nb * kBHdr);
+        bool need_ones = false;
+        for (int i = 0; i < ncols && !need_ones; ++i)
+            if (nullable[i])
+                for (int32_t b = 0; b < nb; ++b)
+                    if (!(ins[b].columns[i].validity && ins[b].columns[i].null_count > 0)) need_ones = true;
+        if (need_ones) {
+            const size_t nbm = (size_t)((maxn + 63) / 64 * 8 + 64);
+            if (ctx->ones_bytes < nbm) {
+                ensure(ctx, &ctx->ones, &ctx->ones_bytes, nbm);
+                HIP_TRY(hipMemsetAsync(ctx->ones, 0xff, ctx->ones_bytes, st));
+            }
+        }
+        uint64_t* tab = (uint64_t*)ctx->host_bmeta;
+        int32_t* tile_batch = (int32_t*)(ctx->host_bmeta + table_bytes);
+        auto valid_of = [&](const dfmi_column& c, int col) -> uint64_t {
+            if (!nullable[col]) return 0;
+            return (uint64_t)((c.validity && c.null_count > 0) ? c.validity : ctx->ones);
+        };
+        for (int32_t b = 0; b < nb; ++b) {
+            const dfmi_batch& in = ins[b];
+            for (int i = 0; i < ncols; ++i)
+                if (in.columns[i].length != in.num_rows) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
+            uint64_t* row = tab + (size_t)b * NPW;
+            memset(row, 0, (size_t)NPW * 8);
+            row[0] = (uint64_t)in.num_rows;
+            row[1] = (uint64_t)tiles[b] | ((uint64_t)first[b] << 32);
+            row[2] = (uint64_t)(ctx->bhdr + (size_t)b * kBHdr);
+            row[3] = (uint64_t)(ctx->bhdr + (size_t)b * kBHdr + 24 * 8);
+            for (size_t sl = 0; sl < X.num_cols.size(); ++sl) {
+                const dfmi_column& c = in.columns[X.num_cols[sl]];
+                const int w = jit::type_width(c.type);
+                if (in.num_rows > 0 && !c.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
+                if (w && ((uintptr_t)c.values & (w - 1)))
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values must be aligned to their width"};
+                row[jit::batch_slot_col((int)sl)] = (uint64_t)c.values;
+                row[jit::batch_slot_col((int)sl) + 1] = valid_of(c, X.num_cols[sl]);
+            }
+            for (size_t u = 0; u < X.utf8_cols.size(); ++u) {
+                const dfmi_column& c = in.columns[X.utf8_cols[u]];
+                if (in.num_rows > 0 && (!c.values || !c.offsets))
+                    throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 column buffers are NULL"};
+                const int sl = jit::batch_slot_utf8(X, (int)u);
+                row[sl] = (uint64_t)c.offsets;
+                row[sl + 1] = (uint64_t)c.values;
+                row[sl + 2] = valid_of(c, X.utf8_cols[u]);
+            }
+            for (int o = 0; o < nout; ++o) {
+                dfmi_out_column& oc = outs[(size_t)b * nout + o];
+                const jit::OutSpec& os = plan.outs[o];
+                const int sl = jit::batch_slot_out(X, o);
+                if (os.kind == jit::OutSpec::UTF8) {
+                    if (!oc.offsets || !oc.data) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 output buffers are NULL"};
+                } else if (os.kind != jit::OutSpec::SKIP) {
+                    if (!oc.values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output values pointer is NULL"};
+                    if (!pred && !oc.validity)
+                        throw Fail{DFMI_ERR_INVALID_ARGUMENT, "output validity pointer is NULL"};
+                }
+                row[sl] = (uint64_t)oc.values;
+                row[sl + 1] = pred ? 0 : (uint64_t)oc.validity;
+                row[sl + 2] = (uint64_t)oc.offsets;
+                row[sl + 3] = (uint64_t)oc.data;
+                row[sl + 4] = (uint64_t)oc.data_capacity;
+            }
+            for (int64_t t = 0; t < tiles[b]; ++t) tile_batch[first[b] + t] = b;
+        }
+        // ---- launch
+        if (T > 0) {
+            HIP_TRY(hipMemcpyAsync(ctx->bmeta, ctx->host_bmeta, meta_bytes, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemsetAsync(ctx->bhdr, 0, (size_t)nb * kBHdr, st));
+            const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
+            const size_t status_bytes = (size_t)n_chan * T * 8 * X.spread;
+            Args A;
+            memset(&A, 0, sizeof A);
+            A.n_rows = maxn;
+            A.n_tiles = (int)T;
+            memcpy(A.lits, X.args_lits, sizeof A.lits);
+            memcpy(A.str_off, X.str_off, sizeof A.str_off);
+            memcpy(A.str_len, X.str_len, sizeof A.str_len);
+            memcpy(A.str, X.str, sizeof A.str);
+            const WsLease ws = ws_acquire(ctx, status_bytes, st);
+            A.ticket = (unsigned*)(ws.hdr + kHdrTicket);
+            A.err = (unsigned long long*)(ws.hdr + kHdrErr);
+            A.totals = (unsigned long long*)(ws.hdr + kHdrTotals);
+            A.status = (unsigned long long*)ws.status;
+            A.stats = (unsigned long long*)(ws.hdr + kHdrStats);
+            A.clear_status = (unsigned long long*)ws.clear_status;
+            A.clear_words = ws.clear_words;
+            A.clear_hdr = (unsigned long long*)ws.clear_hdr;
+            A.tile_batch = (const int*)(ctx->bmeta + table_bytes);
+            A.batch_ptrs = (void* const*)ctx->bmeta;
+            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
+            size_t asz = sizeof A;
+            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+            HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)T, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
+            ws_commit(ctx, ws);
+            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
+            HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
+        }
+        for (int32_t b = 0; b < nb; ++b)  // empty batches: Utf8 offsets = [0]
+            if (ins[b].num_rows == 0)
+                for (int o = 0; o < nout; ++o)
+                    if (plan.outs[o].kind == jit::OutSpec::UTF8 && outs[(size_t)b * nout + o].offsets)
+                        HIP_TRY(hipMemsetAsync(outs[(size_t)b * nout + o].offsets, 0, 4, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (T > 0 && ctx->timing) {
+            float m1 = 0;
+            (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);
+            ctx->last_main_ms = ctx->last_total_ms = m1;
+            ctx->timed = true;
+        }
+        // ---- per batch, in order: results, or the first batch's error
+        for (int32_t b = 0; b < nb; ++b) {
+            const uint64_t* h = (const uint64_t*)(ctx->host_bhdr + (size_t)b * kBHdr);
+            const bool ran = ins[b].num_rows > 0;
+            const uint64_t ew = ran ? h[24] : 0;
+            if (ew) {
+                const uint64_t key = ~ew;
+                const int kind = (int)(key & 15);
+                *failed = b;
+                if (kind == ERRK_LOOKBACK_TIMEOUT) throw Fail{DFMI_ERR_DEVICE, "device look-back timed out"};
+                if (kind == ERRK_CAPACITY) throw Fail{DFMI_ERR_CAPACITY, "Utf8 output data_capacity too small"};
+                ctx->last_err_key = key & ~15ull;
+                if (kind == ERRK_DIV_ZERO) throw Fail{DFMI_ERR_DIVIDE_BY_ZERO, "DivideByZero"};
+                throw Fail{DFMI_ERR_PANIC, "attempt to divide with overflow"};
+            }
+            const int64_t n = ins[b].num_rows;
+            const int64_t out_rows = pred ? (ran ? (int64_t)h[0] : 0) : n;
+            for (int o = 0; o < nout; ++o) {
+                dfmi_out_column& oc = outs[(size_t)b * nout + o];
+                const dfmi_out_column& tmpl = outs[o];
+                oc.type = tmpl.type;
+                oc.passthrough_column = tmpl.passthrough_column;
+                oc.data_length = 0;
+                if (oc.passthrough_column >= 0) {  // Arc clone of this batch's column
+                    const dfmi_column& c = ins[b].columns[oc.passthrough_column];
+                    oc.length = n;
+                    oc.null_count = c.validity ? c.null_count : 0;
+                    continue;
+                }
+                oc.length = out_rows;
+                oc.null_count = (!pred && ran) ? (int64_t)h[8 + o] : 0;
+                if (plan.outs[o].kind == jit::OutSpec::UTF8 && ran)
+                    for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                        if (X.utf8_outs[j].first == o) oc.data_length = (int64_t)h[1 + j];
+            }
+        }
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
 // Internal test hook (not part of the C ABI, not declared in include/):
 // generates the query kernel a dfmi_filter_project call would launch and, if
 // compile != 0, compiles it with hipRTC -- no device needed, so the CPU test
@@ -561,7 +842,8 @@ extern "C" int64_t dfmi_internal_jit_check(const dfmi_program* pred, const dfmi_
     try {
         if (!in || (np > 0 && !projs) || !outs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         Built B;
-        build_plan(pred, projs, np, in, outs, flags, B);
+        build_plan(pred, projs, np, in, outs, flags & ~0x40000000u, B);
+        B.X.batched = (flags & 0x40000000u) != 0;  // the coalesced-batches form of the kernel
         const std::string src = jit::generate(B.plan, B.X);
         if (compile) (void)jit::compile_code(src, nullptr);
         if (buf && cap > 0) snprintf(buf, (size_t)cap, "%s", src.c_str());

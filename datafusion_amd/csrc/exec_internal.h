@@ -22,14 +22,19 @@ struct dfmi_context {
     int device = 0;
     hipStream_t stream = nullptr;
     // Look-back workspace, double-buffered: [hdr 0 | hdr 1 | status 0 | status 1].
-    // Launch i uses pair (i & 1), which is zero on entry, and its blocks zero
-    // pair (i+1) & 1 -- what launch i-1 dirtied -- for launch i+1 (stream
-    // order makes launch i-1 complete first). No memset on the steady path.
+    // Launch i uses pair (i & 1), whose first `need` status bytes must be
+    // zero on entry; its blocks zero what launch i-1 dirtied in the other
+    // pair, for launch i+1 (stream order makes launch i-1 complete first) --
+    // no memset per call. Bytes [dirty_lo[b], dirty_hi[b]) of status buffer b
+    // may be non-zero. A launch clears the other pair only up to a few times
+    // its own status size (a 1024-row call after a 1e9-row call must not
+    // zero 31 MB from one block); a larger leftover is cleared by memset of
+    // just the prefix a later launch needs (ws_acquire).
     uint8_t* ws = nullptr;
     size_t ws_bytes = 0;
     size_t status_cap = 0;       // bytes per status buffer
     int parity = 0;              // pair the next launch uses
-    size_t dirty[2] = {0, 0};    // status bytes [0, dirty[b]) of buffer b may be non-zero
+    size_t dirty_lo[2] = {0, 0}, dirty_hi[2] = {0, 0};
     bool ws_valid = false;       // the invariant above holds (else re-zero everything)
     uint8_t* scratch = nullptr;  // Boolean output bytes (filtered)
     size_t scratch_bytes = 0;
@@ -44,7 +49,21 @@ struct dfmi_context {
     // evaluation-order key (ordinal << 44 | row << 4) of the error the last
     // dfmi_filter_project raised; ~0 for none / an error outside that order
     uint64_t last_err_key = ~0ull;
+    long relaunches = 0;      // look-back timeouts relaunched (dfmi_internal_relaunches)
     std::string last_kernel;  // name of the last launched query kernel (dfmi_last_kernel_name)
+    // coalesced batches (dfmi_filter_project_batches): per-call batch table
+    // and per-batch headers, device + pinned host mirrors; an all-valid
+    // bitmap for batches without validity in a column others have it for
+    uint8_t* bmeta = nullptr;
+    size_t bmeta_bytes = 0;
+    uint8_t* host_bmeta = nullptr;
+    size_t host_bmeta_bytes = 0;
+    uint8_t* bhdr = nullptr;
+    size_t bhdr_bytes = 0;
+    uint8_t* host_bhdr = nullptr;
+    size_t host_bhdr_bytes = 0;
+    uint8_t* ones = nullptr;
+    size_t ones_bytes = 0;
 };
 
 namespace dfmi {
@@ -85,6 +104,16 @@ struct Err {
     }
 };
 
+inline void ensure_host(uint8_t** buf, size_t* have, size_t need) {  // pinned
+    if (*have >= need) return;
+    if (*buf) HIP_TRY(hipHostFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    size_t cap = std::max(need, (size_t)1 << 16);
+    HIP_TRY(hipHostMalloc((void**)buf, cap, hipHostMallocDefault));
+    *have = cap;
+}
+
 inline void ensure(dfmi_context* ctx, uint8_t** buf, size_t* have, size_t need) {
     if (*have >= need) return;
     if (*buf) HIP_TRY(hipFree(*buf));
@@ -103,8 +132,8 @@ struct WsLease {
     size_t status_bytes = 0;
     uint8_t* hdr = nullptr;
     uint8_t* status = nullptr;
-    uint8_t* clear_status = nullptr;
-    long long clear_words = 0;
+    uint8_t* clear_status = nullptr;  // first status word the kernel zeroes ...
+    long long clear_words = 0;        // ... and how many
     uint8_t* clear_hdr = nullptr;
 };
 
@@ -117,26 +146,49 @@ inline WsLease ws_acquire(dfmi_context* ctx, size_t status_bytes, hipStream_t st
     }
     if (!ctx->ws_valid) {  // first use, growth, or an interrupted call
         HIP_TRY(hipMemsetAsync(ctx->ws, 0, 2 * kHdrAlloc + 2 * ctx->status_cap, st));
-        ctx->dirty[0] = ctx->dirty[1] = 0;
+        ctx->dirty_lo[0] = ctx->dirty_lo[1] = ctx->dirty_hi[0] = ctx->dirty_hi[1] = 0;
         ctx->ws_valid = true;
     }
     WsLease l;
-    l.par = ctx->parity;
+    const int p = ctx->parity, q = 1 - p;
+    l.par = p;
     l.status_bytes = status_bytes;
-    l.hdr = ctx->ws + l.par * kHdrAlloc;
-    l.status = ctx->ws + 2 * kHdrAlloc + l.par * ctx->status_cap;
-    l.clear_status = ctx->ws + 2 * kHdrAlloc + (1 - l.par) * ctx->status_cap;
-    l.clear_words = (long long)(ctx->dirty[1 - l.par] / 8);
-    l.clear_hdr = ctx->ws + (1 - l.par) * kHdrAlloc;
+    l.hdr = ctx->ws + p * kHdrAlloc;
+    l.status = ctx->ws + 2 * kHdrAlloc + p * ctx->status_cap;
+    // the prefix this launch needs must be zero: clear what is left dirty in it
+    size_t& lo = ctx->dirty_lo[p];
+    size_t& hi = ctx->dirty_hi[p];
+    if (hi > lo && lo < status_bytes) {
+        const size_t end = std::min(hi, status_bytes);
+        HIP_TRY(hipMemsetAsync(l.status + lo, 0, end - lo, st));
+        lo = end;
+        if (lo >= hi) lo = hi = 0;
+    }
+    // what this launch's blocks zero in the other pair (bounded by its size)
+    uint8_t* other = ctx->ws + 2 * kHdrAlloc + q * ctx->status_cap;
+    const size_t qd = ctx->dirty_hi[q] - ctx->dirty_lo[q];
+    if (qd > 0 && qd <= std::max<size_t>(4 * status_bytes, (size_t)64 << 10)) {
+        l.clear_status = other + ctx->dirty_lo[q];
+        l.clear_words = (long long)(qd / 8);
+    } else {
+        l.clear_status = other;
+        l.clear_words = 0;
+    }
+    l.clear_hdr = ctx->ws + q * kHdrAlloc;
     ctx->ws_valid = false;  // until the launch is enqueued (ws_commit)
     return l;
 }
 
-// The launch using `l` is enqueued: the other pair is clean for the next one.
+// The launch using `l` is enqueued: its status prefix is dirty, and the
+// other pair's range it zeroes is clean for the next launch.
 inline void ws_commit(dfmi_context* ctx, const WsLease& l) {
-    ctx->dirty[l.par] = l.status_bytes;
-    ctx->dirty[1 - l.par] = 0;
-    ctx->parity = 1 - l.par;
+    const int p = l.par, q = 1 - p;
+    if (l.status_bytes) {
+        ctx->dirty_hi[p] = std::max(ctx->dirty_hi[p], l.status_bytes);
+        ctx->dirty_lo[p] = 0;
+    }
+    if (l.clear_words) ctx->dirty_lo[q] = ctx->dirty_hi[q] = 0;
+    ctx->parity = q;
     ctx->ws_valid = true;
 }
 

@@ -242,7 +242,7 @@ struct Gen {
                     o << "    const bool " << v << "_e = " << vu << " && " << arr << "[k];\n";
                 } else {
                     o << "    const bool " << v << "_e = " << vu << " && dfmi::utf8_eq_lit(A, " << u << ", row, " << sl
-                      << ");\n";
+                      << ", A0.str + A0.str_off[" << sl << "]);\n";
                 }
                 o << "    const bool " << v << " = " << (eq ? "" : "!") << v << "_e;\n";
             }
@@ -443,8 +443,8 @@ static std::vector<int> emit_predicate(Gen& g, std::ostringstream& o, const Plan
     for (const auto& pe : g.pre_eq) load_offs(std::get<1>(pe));
     for (int u : extra_offs) load_offs(u);
     for (const auto& [arr, u, sl] : g.pre_eq)
-        pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u << ", " << sl << ", us"
-            << offs_name(u) << ", ux" << offs_name(u) << ", lane, " << arr << ");\n";
+        pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile<BLOCK, K>(A, " << u << ", " << sl << ", A0.str + A0.str_off["
+            << sl << "], us" << offs_name(u) << ", ux" << offs_name(u) << ", lane, " << arr << ");\n";
     if (!pre.str().empty()) {  // splice in front of the predicate loop
         const std::string loop = o.str().substr(head.size());
         o.str(head + pre.str() + loop);
@@ -476,7 +476,7 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     }
     o << "};\n";
     o << "  if (wave == 0) dfmi::agg_lds_init<NA, NF>(S, is_min, lane);\n";
-    o << "  const unsigned t = blockIdx.x;\n";
+    o << "  const unsigned t = tile_;\n";
     emit_decls(o, X.pred_slots, X, "", true);
     emit_decls(o, X.proj_slots, X, "", !P.pred);
     emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
@@ -530,6 +530,38 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     o << "  dfmi::lds_sync();\n  dfmi::agg_block_flush<NA, NF>(A, S, fslot, is_min, tid);\n  }\n";
 }
 
+// Coalesced batches: this block's batch, its local tile index `tile_`, and a
+// local copy of the Args with the batch's rows, tiles, look-back status
+// segment, totals / error words and buffers (the copy is only ever indexed
+// with constants, so it lives in registers: no scratch).
+static void emit_batched_prologue(std::ostream& o, const Plan& P, const Launch& X) {
+    const int np = batch_words(X, (int)P.outs.size());
+    o << "  const int b_ = A0.tile_batch[blockIdx.x];\n"
+      << "  void* const* bp_ = A0.batch_ptrs + (i64)b_ * " << np << ";\n"
+      << "  dfmi::Args A = A0;\n"
+      << "  A.n_rows = (i64)(u64)bp_[0];\n"
+      << "  const u64 tt_ = (u64)bp_[1];\n"
+      << "  A.n_tiles = (int)(unsigned)tt_;\n"
+      << "  const unsigned tile_ = blockIdx.x - (unsigned)(tt_ >> 32);\n"
+      << "  A.totals = (u64*)bp_[2];\n  A.err = (u64*)bp_[3];\n";
+    if (P.pred)  // [ch][tile] status words of this batch's tiles
+        o << "  A.status = A0.status + (i64)(tt_ >> 32) * " << (1 + X.utf8_outs.size()) * (size_t)X.spread << ";\n";
+    for (size_t s = 0; s < X.num_cols.size(); ++s)
+        o << "  A.col[" << s << "] = bp_[" << batch_slot_col((int)s) << "];\n  A.valid[" << s << "] = (const u8*)bp_["
+          << batch_slot_col((int)s) + 1 << "];\n";
+    for (size_t u = 0; u < X.utf8_cols.size(); ++u) {
+        const int b = batch_slot_utf8(X, (int)u);
+        o << "  A.offs[" << u << "] = (const int*)bp_[" << b << "];\n  A.bytes[" << u << "] = (const u8*)bp_[" << b + 1
+          << "];\n  A.svalid[" << u << "] = (const u8*)bp_[" << b + 2 << "];\n";
+    }
+    for (size_t oi = 0; oi < P.outs.size(); ++oi) {
+        const int b = batch_slot_out(X, (int)oi);
+        o << "  A.out[" << oi << "] = bp_[" << b << "];\n  A.out_valid[" << oi << "] = (u8*)bp_[" << b + 1
+          << "];\n  A.out_offs[" << oi << "] = (int*)bp_[" << b + 2 << "];\n  A.out_data[" << oi << "] = (u8*)bp_["
+          << b + 3 << "];\n  A.out_cap[" << oi << "] = (i64)(u64)bp_[" << b + 4 << "];\n";
+    }
+}
+
 std::string generate(const Plan& P, Launch& X) {
     Gen g(P, X);
     std::ostringstream& o = g.o;
@@ -537,10 +569,16 @@ std::string generate(const Plan& P, Launch& X) {
     o << "\n// ---- generated query kernel ----\n";
     o << "extern \"C\" __global__ __launch_bounds__(" << BLOCK << ")";
     if (X.waves_per_eu > 0) o << " __attribute__((amdgpu_waves_per_eu(" << X.waves_per_eu << ")))";
-    o << " void DFMI_KNAME(const dfmi::Args A) {\n";
+    o << " void DFMI_KNAME(const dfmi::Args A0) {\n";
     o << "  constexpr int BLOCK = " << BLOCK << ", K = " << K << ", WAVES = BLOCK / 64;\n";
     o << "  const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);\n";
-    o << "  dfmi::clear_previous<BLOCK>(A, blockIdx.x, tid);\n";
+    o << "  dfmi::clear_previous<BLOCK>(A0, blockIdx.x, tid);\n";
+    if (X.batched) {
+        if (!P.aggs.empty()) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batched launch of an aggregate"};
+        emit_batched_prologue(o, P, X);
+    } else {
+        o << "  const dfmi::Args& A = A0;\n  const unsigned tile_ = blockIdx.x;\n";
+    }
     if (!P.aggs.empty()) {
         generate_agg(g, o, P, X);
     } else if (P.pred) {
@@ -649,7 +687,7 @@ std::string generate(const Plan& P, Launch& X) {
             o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
             if (!X.utf8_outs.empty() && X.gather && X.gather != 3)
                 o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA> G[WAVES];\n";
-            o << "  const unsigned t = blockIdx.x;\n";
+            o << "  const unsigned t = tile_;\n";
             emit_decls(o, X.pred_slots, X, "", true);
             emit_decls(o, X.proj_slots, X, "", false);
             emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
@@ -657,7 +695,7 @@ std::string generate(const Plan& P, Launch& X) {
         }
     } else {
         // projection only: dense rows, ballot-packed validity / Boolean bitmaps
-        o << "  const i64 base = (i64)blockIdx.x * (BLOCK * K);\n";
+        o << "  const i64 base = (i64)tile_ * (BLOCK * K);\n";
         std::vector<int> all = X.pred_slots;
         all.insert(all.end(), X.proj_slots.begin(), X.proj_slots.end());
         emit_decls(o, all, X, "", true);
@@ -746,7 +784,8 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, os.out_type);
         put(k, (char)os.nullable);
     }
-    const int tile[] = {X.K, X.BLOCK, X.waves_per_eu, X.R, X.sleep, X.spread, X.window, X.nt, X.gather, X.late_proj, X.arena};
+    const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

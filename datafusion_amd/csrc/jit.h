@@ -75,6 +75,10 @@ struct Launch {
     char str[256] = {};
     int n_str = 0, str_bytes = 0;
     std::string kname;  // generated kernel's name (dfmi_<kind>_<hash>)
+    // coalesced batches (dfmi_filter_project_batches): blocks map to batches
+    // through Args::tile_batch, and each batch's sizes and buffers come from
+    // its row of Args::batch_ptrs (layout: batch_slot_* below)
+    bool batched = false;
 
     int col_type(int col) const { return in->columns[col].type; }
     bool col_nullable(int col) const {
@@ -91,6 +95,17 @@ struct Launch {
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "query compiler: Utf8 column not registered"};
     }
 };
+
+// Row layout of Args::batch_ptrs for one batch (8-byte words):
+//   [0] rows, [1] tiles | first tile << 32, [2] totals, [3] error word,
+//   per numeric slot s: values, validity; per Utf8 slot u: offsets, bytes,
+//   validity; per output o: values, validity, offsets, data, data capacity.
+inline int batch_slot_col(int s) { return 4 + 2 * s; }
+inline int batch_slot_utf8(const Launch& X, int u) { return 4 + 2 * (int)X.num_cols.size() + 3 * u; }
+inline int batch_slot_out(const Launch& X, int o) {
+    return 4 + 2 * (int)X.num_cols.size() + 3 * (int)X.utf8_cols.size() + 5 * o;
+}
+inline int batch_words(const Launch& X, int nout) { return batch_slot_out(X, nout); }
 
 // Bytes per value of a fixed-width dfmi_type (0 otherwise) and the C++ type
 // the generated code holds it in (i8 .. u64, float, double).

@@ -61,6 +61,11 @@ struct Args {
     i64 clear_words;                   // ... [0, clear_words) to zero
     u64* clear_hdr;                    // previous launch's 512-byte header
     u64* agg;                          // aggregate extension: [copies][aggs][kAggWords] accumulators
+    // coalesced batches (dfmi_filter_project_batches): block -> batch, and
+    // per batch a row of pointers / sizes the kernel's prologue loads into a
+    // local copy of these Args (see jit.cpp "batched")
+    const int* tile_batch;
+    void* const* batch_ptrs;  // pointers and sizes (as pointer-sized integers)
 };
 
 // This block's share of zeroing the previous launch's workspace.
@@ -71,6 +76,9 @@ __device__ __forceinline__ void clear_previous(const Args& A, unsigned block, in
     const i64 w1 = w0 + per < A.clear_words ? w0 + per : A.clear_words;
     for (i64 w = w0 + tid; w < w1; w += BLOCK) A.clear_status[w] = 0;
     if (block == 0 && tid < 64) A.clear_hdr[tid] = 0;
+    // diagnostics (mode bit 4): report a look-back timeout once, to test the
+    // host's relaunch (exec.cpp)
+    if ((A.mode & 16) && block == 0 && tid == 0) atomicMax(A.err, ~(u64)3);
 }
 
 enum ErrKind : unsigned { ERRK_DIV_ZERO = 1, ERRK_DIV_OVERFLOW = 2, ERRK_LOOKBACK_TIMEOUT = 3, ERRK_CAPACITY = 4 };
@@ -272,13 +280,15 @@ __device__ __forceinline__ bool num_cast(From x, To& out) {
 }
 
 // Rows past n_rows (the tail tile) read nothing: the callers mask them out.
-__device__ __forceinline__ bool utf8_eq_lit(const Args& A, int u, i64 row, int lit) {
+// The literal's bytes `q` come from the kernel's own Args (A0.str): in the
+// coalesced-batches form `A` is a register copy, which must never be indexed
+// with a run-time value.
+__device__ __forceinline__ bool utf8_eq_lit(const Args& A, int u, i64 row, int lit, const char* q) {
     if (row >= A.n_rows) return false;
     const int s = A.offs[u][row], e = A.offs[u][row + 1];
     const int len = A.str_len[lit];
     if (e - s != len) return false;
     const u8* p = A.bytes[u] + s;
-    const char* q = A.str + A.str_off[lit];
     // early exit: most equal-length candidates differ within the first bytes
     // (filtered tiles use utf8_eq_lit_tile below)
     for (int i = 0; i < len; ++i)
@@ -325,10 +335,9 @@ __device__ __forceinline__ int utf8_end(int s, int nx, int lane) {
 // only head matches (rare) compare the rest. Only words holding bytes of the
 // candidate are read.
 template <int BLOCK, int K>
-__device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, int lit, const int (&s)[K], const int (&nx)[K],
-                                                 int lane, bool (&res)[K]) {
+__device__ __forceinline__ void utf8_eq_lit_tile(const Args& A, int u, int lit, const char* q, const int (&s)[K],
+                                                 const int (&nx)[K], int lane, bool (&res)[K]) {
     const int len = A.str_len[lit];
-    const char* q = A.str + A.str_off[lit];
     const u8* by = A.bytes[u];
     const int hn = len < 4 ? len : 4;
     const unsigned hm = hn == 4 ? ~0u : ((1u << (8 * hn)) - 1u);

@@ -26,7 +26,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     int us[K], ue[K];
     bool eq[K];
     dfmi::utf8_offs_tile<BLOCK, K>(A, 0, base, lane, wave, ~0u, us, ue);
-    dfmi::utf8_eq_lit_tile<BLOCK, K>(A, 0, 0, us, ue, lane, eq);
+    dfmi::utf8_eq_lit_tile<BLOCK, K>(A, 0, 0, A.str + A.str_off[0], us, ue, lane, eq);
     for (int k = 0; k < K; ++k) {
         selm |= (unsigned)eq[k] << k;
         wm[k] = __ballot((selm >> k) & 1);
@@ -43,7 +43,7 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     dfmi::utf8_gather_serial<BLOCK, K, NCH, dfmi::kStageChunks>(A, T, 1, 0, 1, selm, wm, dst, us, ue, G[wave], lane, wave);
     dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, 1, 0, 1, selm, dst, us, ue, lane, wave);
     dfmi::utf8_offsets_src<BLOCK, K, NCH>(A, T, 1, 1, selm, wm, dst, us, ue, lane, wave);
-    const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0) &&
+    const bool b = dfmi::cmp_opt<2>(true, false, false) && dfmi::utf8_eq_lit(A, 0, base, 0, A.str) &&
                    dfmi::utf8_eq_col(A, 0, 1, base) && dfmi::utf8_valid(A, 0, base);
     if (b) dfmi::report_err(A.err, 1, base, dfmi::ERRK_DIV_ZERO);
     if (tid == 0 && dfmi::bitmap_word(A.valid[0], 0, A.n_rows) == 7)

@@ -49,10 +49,14 @@ class Aggregate:
 
 
 class ExecutionContext:
-    def __init__(self, device=None, flags: int = 0):
+    def __init__(self, device=None, flags: int = 0, coalesce: int = 1):
+        """coalesce > 1: Selection / Projection relations run up to that many
+        input batches per device launch (dfmi_filter_project_batches) while
+        still returning one output batch per input batch."""
         self.datasources: Dict[str, object] = {}
         self.device = device
         self.flags = flags
+        self.coalesce = coalesce
 
     def register_datasource(self, name: str, ds) -> None:
         self.datasources[name] = ds
@@ -77,7 +81,7 @@ class ExecutionContext:
             input_rel = self.execute(plan.input)
             input_schema = input_rel.schema()
             rt = compile_scalar_expr(self, plan.expr, input_schema, self.flags)
-            return FilterRelation(input_rel, rt, input_schema, self.device, self.flags)
+            return FilterRelation(input_rel, rt, input_schema, self.device, self.flags, self.coalesce)
         if isinstance(plan, Projection):
             input_rel = self.execute(plan.input)
             input_schema = input_rel.schema()
@@ -93,7 +97,7 @@ class ExecutionContext:
                     fields.append(Field(name, t, True))
             project_schema = Schema(fields)
             compiled = [compile_scalar_expr(self, e, input_schema, self.flags) for e in plan.expr]
-            return ProjectRelation(input_rel, compiled, project_schema, self.device, self.flags)
+            return ProjectRelation(input_rel, compiled, project_schema, self.device, self.flags, self.coalesce)
         if isinstance(plan, Aggregate):
             return self._execute_aggregate(plan)
         raise ExecutionError("NotImplemented", "unimplemented!() plan %r" % type(plan).__name__)

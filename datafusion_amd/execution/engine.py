@@ -110,28 +110,8 @@ class DeviceEngine:
         cb.num_rows = n
         cb.columns = carr
 
-        if projections:
-            out_types = [p.get_type() for p in projections]
-            src_cols = [p.expr.index if isinstance(p.expr, Column) else None for p in projections]
-        else:
-            out_types = [c.data_type for c in cols]
-            src_cols = list(range(len(cols)))
-        outs = (_abi.dfmi_out_column * max(1, len(out_types)))()
-        keeps = []
-        for o, t in enumerate(out_types):
-            passthrough = predicate is None and src_cols[o] is not None
-            if passthrough:
-                keeps.append({})
-                continue
-            cap = 0
-            if t == DataType.Utf8 and src_cols[o] is not None:
-                cap = cols[src_cols[o]].values.numel()
-            # validity: always without a predicate; after one, a projection
-            # with a fallible CAST can still produce nulls
-            oc, keep = self._alloc_out(t, n, t != DataType.Utf8, cap)
-            outs[o] = oc
-            keeps.append(keep)
-
+        out_types, outs_list, keeps = self._prepare_outputs(predicate, projections, cols, n)
+        outs = (_abi.dfmi_out_column * max(1, len(out_types)))(*outs_list)
         progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
         err = _abi.dfmi_error()
         L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
@@ -150,6 +130,36 @@ class DeviceEngine:
             L.dfmi_last_error_order(self.ctx, C.byref(key))
             e.order_key = key.value  # evaluation-order position (sharded callers pick the first)
             raise e
+        return self._results(out_types, [outs[o] for o in range(len(out_types))], keeps, cols)
+
+    def _prepare_outputs(self, predicate, projections, cols, n):
+        """Output types, dfmi_out_column structs (worst-case buffers for n
+        rows) and the tensors behind them, for one batch."""
+        if projections:
+            out_types = [p.get_type() for p in projections]
+            src_cols = [p.expr.index if isinstance(p.expr, Column) else None for p in projections]
+        else:
+            out_types = [c.data_type for c in cols]
+            src_cols = list(range(len(cols)))
+        outs, keeps = [], []
+        for o, t in enumerate(out_types):
+            passthrough = predicate is None and src_cols[o] is not None
+            if passthrough:
+                outs.append(_abi.dfmi_out_column())
+                keeps.append({})
+                continue
+            cap = 0
+            if t == DataType.Utf8 and src_cols[o] is not None:
+                cap = cols[src_cols[o]].values.numel()
+            # validity: always without a predicate; after one, a projection
+            # with a fallible CAST can still produce nulls
+            oc, keep = self._alloc_out(t, n, t != DataType.Utf8, cap)
+            outs.append(oc)
+            keeps.append(keep)
+        return out_types, outs, keeps
+
+    @staticmethod
+    def _results(out_types, outs, keeps, cols) -> List[Array]:
         result = []
         for o, t in enumerate(out_types):
             oc = outs[o]
@@ -164,6 +174,58 @@ class DeviceEngine:
             else:
                 result.append(Array(t, length, k["values"], k.get("validity") if nulls else None, None, nulls))
         return result
+
+    def filter_project_batches(self, predicate, projections: Optional[Sequence], batches: Sequence[RecordBatch],
+                               flags: int = 0):
+        """The pull of filter_project on each batch, in order, as ONE device
+        launch (dfmi_filter_project_batches). Returns (results, error):
+        results holds one column list per batch before the first failing
+        batch (all of them when error is None) -- what a pull loop would have
+        received before the error."""
+        L = _abi.lib()
+        projections = list(projections or [])
+        batches = [self.to_device(b) for b in batches]
+        nb = len(batches)
+        if nb == 0:
+            return [], None
+        per, cstructs = [], []
+        for b in batches:
+            cols = b.columns
+            carr = (_abi.dfmi_column * max(1, len(cols)))()
+            for i, a in enumerate(cols):
+                carr[i] = column_struct(a)
+            cstructs.append(carr)
+            per.append(self._prepare_outputs(predicate, projections, cols, b.num_rows()))
+        nout = len(per[0][0])
+        cb = (_abi.dfmi_batch * nb)()
+        for i, b in enumerate(batches):
+            cb[i].num_columns = len(b.columns)
+            cb[i].num_rows = b.num_rows()
+            cb[i].columns = cstructs[i]
+        outs = (_abi.dfmi_out_column * max(1, nb * nout))()
+        for i in range(nb):
+            for o in range(nout):
+                outs[i * nout + o] = per[i][1][o]
+        progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
+        err = _abi.dfmi_error()
+        failed = C.c_int32(-1)
+        L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        rc = L.dfmi_filter_project_batches(self.ctx, predicate.handle if predicate is not None else None, progs,
+                                           len(projections), cb, nb, outs, flags, C.byref(failed), C.byref(err))
+        error = None
+        done = nb
+        if rc != _abi.DFMI_OK:
+            error = ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+            key = C.c_uint64()
+            L.dfmi_last_error_order(self.ctx, C.byref(key))
+            error.order_key = key.value
+            done = max(failed.value, 0)
+            error.failed_batch = failed.value
+        results = []
+        for i in range(done):
+            results.append(self._results(per[i][0], [outs[i * nout + o] for o in range(nout)], per[i][2],
+                                         batches[i].columns))
+        return results, error
 
     def filter_project_host(self, predicate, projections: Optional[Sequence], batch: RecordBatch,
                             flags: int = 0) -> List[Array]:

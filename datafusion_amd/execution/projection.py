@@ -12,17 +12,19 @@ from typing import List, Optional
 from ..arrow import Field, RecordBatch, Schema
 from .engine import engine
 from .expression import RuntimeExpr
-from .filter import FilterRelation
+from .filter import Coalescer, FilterRelation
 from .relation import Relation
 
 
 class ProjectRelation(Relation):
     def __init__(self, input: Relation, expr: List[RuntimeExpr], schema: Schema, device=None,
-                 flags: int = None):
+                 flags: int = None, coalesce: int = 1):
         self.input = input
         self.expr = list(expr)
         self._schema = schema
         self.device = device
+        self.coalesce = coalesce
+        self._co = None
         if flags is None:
             flags = 0
             for e in self.expr:
@@ -31,24 +33,37 @@ class ProjectRelation(Relation):
                 flags |= input.flags
         self.flags = flags
 
-    def next(self) -> Optional[RecordBatch]:
+    def _source_and_predicate(self):
         if isinstance(self.input, FilterRelation):
-            batch = self.input.input.next()
-            pred = self.input.expr
-        else:
-            batch = self.input.next()
-            pred = None
-        if batch is None:
-            return None
+            return self.input.input, self.input.expr
+        return self.input, None
+
+    def _wrap(self, cols) -> RecordBatch:
+        schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
+        return RecordBatch(schema, cols)
+
+    def run_batch(self, batch: RecordBatch):
+        _, pred = self._source_and_predicate()
         eng = engine(self.device)
         if all(c.values.device.type == "cpu" for c in batch.columns):
             # a host batch (e.g. a CSV source's pinned buffers): the pipelined
             # host entry point, host results -- what a Rust caller gets
-            cols = eng.filter_project_host(pred, self.expr, batch, self.flags)
-        else:
-            cols = eng.filter_project(pred, self.expr, batch, self.flags)
-        schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
-        return RecordBatch(schema, cols)
+            return eng.filter_project_host(pred, self.expr, batch, self.flags)
+        return eng.filter_project(pred, self.expr, batch, self.flags)
+
+    def next(self) -> Optional[RecordBatch]:
+        source, pred = self._source_and_predicate()
+        if self.coalesce > 1:  # up to `coalesce` input batches per device launch
+            if self._co is None:
+                self._co = Coalescer(self.coalesce, source, self.run_batch,
+                                     lambda bs: engine(self.device).filter_project_batches(pred, self.expr, bs,
+                                                                                           self.flags),
+                                     self._wrap)
+            return self._co.next()
+        batch = source.next()
+        if batch is None:
+            return None
+        return self._wrap(self.run_batch(batch))
 
     def schema(self) -> Schema:
         return self._schema

@@ -243,6 +243,27 @@ int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* predicate,
                             uint32_t flags, dfmi_error* err);
 
 /* ---------------------------------------------------------------------------
+ * Coalesced form for small batches: the pull of dfmi_filter_project on each
+ * of `num_batches` device batches IN ORDER, as the reference's pull loop
+ * runs them one next() at a time (csv_sql.rs:49 reads 1024-row batches and
+ * pulls them in csv_sql.rs:60-62; relation.rs:27-32), but as ONE kernel
+ * launch for all of them. Batches share the schema (column types); each has
+ * its own rows, buffers and outputs: `outputs` holds num_batches x n
+ * columns, batch-major (n = num_projections, or num_columns without a
+ * projection), each sized for its own batch as in dfmi_filter_project. Every
+ * batch gets exactly the output dfmi_filter_project would give it (one
+ * output batch per input batch, 0-row batches included).
+ * Errors: the call returns the error of the first batch that raises one;
+ * *failed_batch names it and the batches before it are complete -- the
+ * caller hands those out first, as the pull loop would have seen them. A
+ * plan error the reference raises on every batch fails batch 0.
+ * ------------------------------------------------------------------------- */
+int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_program* predicate,
+                                    const dfmi_program* const* projections, int32_t num_projections,
+                                    const dfmi_batch* inputs, int32_t num_batches, dfmi_out_column* outputs,
+                                    uint32_t flags, int32_t* failed_batch, dfmi_error* err);
+
+/* ---------------------------------------------------------------------------
  * Host-buffer form, for callers whose batches live in host memory (the Rust
  * reference's arrow 0.12 buffers from csv::Reader, csv_sql.rs:49): the same
  * pull as dfmi_filter_project -- FilterRelation::next (filter.rs:46-72) +

@@ -1,0 +1,148 @@
+"""GPU parity of the coalesced-batches entry point (dfmi_filter_project_batches,
+include/dfmi.h): many small batches -- the reference pulls 1024-row batches
+(csv_sql.rs:49, :60-62) -- in ONE launch, each batch's output exactly the
+oracle's for that batch alone (one output batch per input batch, 0-row
+batches included), and on an error the batches before the failing one
+complete, the failing one reporting the oracle's error for it."""
+import numpy as np
+import pytest
+
+from datafusion_amd._abi import DFMI_FLAG_EXT_GATHER_ALL, DFMI_FLAG_EXT_UTF8_COMPARE
+from datafusion_amd.arrow import Array, Field, RecordBatch, Schema
+from datafusion_amd.execution import ExecutionContext, MemoryDataSource
+from datafusion_amd.execution.engine import engine
+from datafusion_amd.execution.error import ExecutionError
+from datafusion_amd.execution.expression import compile_scalar_expr
+from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Float64, Literal, Operator, Utf8
+from oracle_ffi import oracle_filter_project
+from test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1024] * 40 + [0, 1, 63, 64, 65, 1023, 1025, 4095, 4096, 4097, 20_000, 100_003, 0, 7] + [1024] * 30
+
+
+def make_batches(sizes, seed=1, nullable_every=3, utf8=True):
+    """Batches of a (Float64, nullable in every `nullable_every`-th batch),
+    b, c (Float64) and s (Utf8)."""
+    rng = np.random.default_rng(seed)
+    fields = [Field("a", DataType.Float64, True), Field("b", DataType.Float64, False),
+              Field("c", DataType.Float64, False)]
+    if utf8:
+        fields.append(Field("s", DataType.Utf8, False))
+    s = Schema(fields)
+    words = [b"", b"w17", b"alpha", b"\xe2\x82\xac", b"x" * 40] + [b"w%d" % i for i in range(30)]
+    out = []
+    for i, n in enumerate(sizes):
+        valid = (rng.random(n) >= 0.2) if (nullable_every and i % nullable_every == 0) else None
+        cols = [Array.from_numpy(DataType.Float64, rng.random(n), valid),
+                Array.from_numpy(DataType.Float64, rng.random(n)),
+                Array.from_numpy(DataType.Float64, rng.random(n))]
+        if utf8:
+            cols.append(Array.from_strings([words[j] for j in rng.integers(0, len(words), n)]))
+        out.append(RecordBatch(s, cols))
+    return s, out
+
+
+def check(schema, batches, pred_e, proj_e, flags=0):
+    """Device batched results == the oracle batch by batch, or the first
+    failing batch with the oracle's error (batches before it complete)."""
+    p = compile_scalar_expr(None, pred_e, schema, flags) if pred_e is not None else None
+    cp = [compile_scalar_expr(None, e, schema, flags) for e in proj_e]
+    dbs = [b.to(engine().device) for b in batches]
+    got, err = engine().filter_project_batches(p, cp, dbs, flags)
+    for i, b in enumerate(batches):
+        try:
+            ref = oracle_filter_project(schema, b, pred_e, proj_e, flags)
+        except ExecutionError as e:
+            assert err is not None and err.failed_batch == i, (i, e, err)
+            assert (err.kind, err.message) == (e.kind, e.message)
+            assert len(got) == i
+            return i
+        assert i < len(got), (i, err)
+        assert len(got[i]) == len(ref)
+        for d, (name, r) in zip(got[i], ref):
+            assert_same(d.cpu(), r, "batch %d %s" % (i, name))
+    assert err is None, err
+    return None
+
+
+def test_c2_query_many_batches():
+    s, bs = make_batches(SIZES)
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.3))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.7))))
+    projs = [Column(0), Column(1), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus,
+                                              Column(2))]
+    assert check(s, bs, pred, projs) is None
+    # FilterRelation output (every column, Utf8 gathered)
+    assert check(s, bs, pred, []) is None
+
+
+def test_utf8_equality_and_gather_many_batches():
+    s, bs = make_batches(SIZES, seed=2)
+    pred = BinaryExpr(Column(3), Operator.Eq, Literal(Utf8("w17")))
+    assert check(s, bs, pred, [Column(3), Column(0)], DFMI_FLAG_EXT_UTF8_COMPARE) is None
+    pred = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.5)))
+    assert check(s, bs, pred, [Column(3), Column(2)]) is None
+
+
+def test_projection_only_many_batches():
+    """No predicate: dense kernel per batch, null propagation, passthrough."""
+    s, bs = make_batches(SIZES, seed=3)
+    projs = [BinaryExpr(Column(0), Operator.Plus, Column(1)), Column(2), Column(3),
+             BinaryExpr(Column(0), Operator.Lt, Column(1))]
+    assert check(s, bs, None, projs) is None
+
+
+def test_error_in_a_middle_batch():
+    """DivideByZero in batch 57 only: batches 0..56 are returned, batch 57
+    raises the oracle's error."""
+    s, bs = make_batches([1024] * 80, seed=4, utf8=False)
+    b = bs[57].columns[1].cpu()
+    v = np.array(b.numpy_values())
+    v[500] = 0.0
+    bs[57] = RecordBatch(s, [bs[57].columns[0], Array.from_numpy(DataType.Float64, v), bs[57].columns[2]])
+    pred = BinaryExpr(Column(2), Operator.GtEq, Literal(Float64(0.0)))
+    projs = [BinaryExpr(Column(0), Operator.Divide, Column(1))]
+    assert check(s, bs, pred, projs) == 57
+    # not selected in batch 57 -> no error at all
+    v2 = np.array(bs[57].columns[2].cpu().numpy_values())
+    v2[500] = -1.0
+    bs[57] = RecordBatch(s, [bs[57].columns[0], bs[57].columns[1], Array.from_numpy(DataType.Float64, v2)])
+    assert check(s, bs, pred, projs) is None
+
+
+def test_static_error_fails_batch_zero():
+    """A plan error the reference raises on every pull ("filter not supported
+    for Int64", filter.rs:106-110) fails the first batch."""
+    s = Schema([Field("a", DataType.Float64, False), Field("i", DataType.Int64, False)])
+    rng = np.random.default_rng(5)
+    bs = [RecordBatch(s, [Array.from_numpy(DataType.Float64, rng.random(n)),
+                          Array.from_numpy(DataType.Int64, rng.integers(-5, 5, n))]) for n in (0, 100, 1024)]
+    pred = BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.5)))
+    assert check(s, bs, pred, []) == 0
+    assert check(s, bs, pred, [], DFMI_FLAG_EXT_GATHER_ALL) is None  # the extension gathers Int64
+
+
+def test_boolean_outputs_fall_back_to_per_batch():
+    s, bs = make_batches([1024] * 10 + [77, 0, 3000], seed=6)
+    pred = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.8)))
+    assert check(s, bs, pred, [BinaryExpr(Column(1), Operator.Gt, Column(2)), Column(1)]) is None
+
+
+def test_relation_coalesces_batches():
+    """ExecutionContext(coalesce=M): ProjectRelation pulls up to M batches
+    from its input and runs them as one launch, still returning one output
+    batch per input batch in order -- the same stream as without it."""
+    s, bs = make_batches([1024] * 100 + [10, 0, 5000], seed=7)
+    dbs = [b.to(engine().device) for b in bs]
+    sql = "SELECT a, b, a * b + c FROM t WHERE a > 0.25 AND b < 0.75"
+    streams = []
+    for m in (1, 32):
+        ctx = ExecutionContext(coalesce=m)
+        ctx.register_datasource("t", MemoryDataSource(s, dbs))
+        streams.append([[c.cpu() for c in rb.columns] for rb in ctx.sql(sql)])
+    assert len(streams[0]) == len(streams[1]) == len(bs)
+    for a, b in zip(*streams):
+        for x, y in zip(a, b):
+            assert_same(x, y)

@@ -57,3 +57,37 @@ def test_two_processes_share_one_gpu(tmp_path):
         outs.append(json.loads(o.strip().splitlines()[-1]))
     for r in outs:
         assert r["counts"] == [r["expect"]], r
+
+
+@pytest.mark.gpu
+def test_relaunch_after_lookback_timeout(monkeypatch):
+    """exec.cpp relaunches a launch whose look-back timed out once (over a
+    re-zeroed workspace) before reporting DFMI_ERR_DEVICE: a forced timeout
+    (diagnostic mode bit 4) still returns the oracle's result."""
+    import ctypes as C
+
+    import numpy as np
+    from datafusion_amd import _abi
+    from datafusion_amd.arrow import Array, Field, RecordBatch, Schema
+    from datafusion_amd.execution.engine import engine
+    from datafusion_amd.execution.expression import compile_scalar_expr
+    from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Float64, Literal, Operator
+    from oracle_ffi import gen_unit_f64, oracle_filter_project
+    from test_gpu_parity import assert_same
+    n = 300_001
+    s = Schema([Field(c, DataType.Float64, False) for c in "ab"])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, gen_unit_f64(9, j, 0, n)) for j in range(2)])
+    pred_e = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.5)))
+    proj_e = [Column(1), BinaryExpr(Column(0), Operator.Plus, Column(1))]
+    ref = oracle_filter_project(s, b, pred_e, proj_e)
+    eng = engine()
+    L = _abi.lib()
+    L.dfmi_internal_relaunches.argtypes = [C.c_void_p]
+    L.dfmi_internal_relaunches.restype = C.c_long
+    before = L.dfmi_internal_relaunches(eng.ctx)
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_DEBUG_MODE", "16")
+    out = eng.filter_project(compile_scalar_expr(None, pred_e, s), [compile_scalar_expr(None, e, s) for e in proj_e], b)
+    assert L.dfmi_internal_relaunches(eng.ctx) == before + 1
+    for d, (_, r) in zip(out, ref):
+        assert_same(d.cpu(), r)

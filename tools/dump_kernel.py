@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Write the generated query kernel of a bench configuration to a .hip file
 (for hipcc -Rpass-analysis=kernel-resource-usage / ISA inspection).
-usage: tools/dump_kernel.py c2|c3eq|c3lt out.hip"""
+usage: tools/dump_kernel.py c2|c3eq|c3lt[b] out.hip  (suffix b: the coalesced-batches form)"""
 import os
 import sys
 
@@ -18,13 +18,15 @@ C3 = Schema([Field("s", DataType.Utf8, False), Field("v", DataType.Float64, True
 
 def main():
     which, out = sys.argv[1], sys.argv[2]
+    bflag = 0x40000000 if which.endswith("b") else 0
+    which = which.rstrip("b")
     if which == "c2":
         pred, projs = c2_query()
-        rc, code, msg, src = jit_check(F3, pred, projs)
+        rc, code, msg, src = jit_check(F3, pred, projs, flags=bflag)
     elif which in ("c3eq", "c3lt"):
         pred = (BinaryExpr(Column(0), Operator.Eq, Literal(Utf8("w17dizjxms"))) if which == "c3eq"
                 else BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5))))
-        rc, code, msg, src = jit_check(C3, pred, [Column(0), Column(1)], flags=2)
+        rc, code, msg, src = jit_check(C3, pred, [Column(0), Column(1)], flags=2 | bflag)
     else:
         raise SystemExit("unknown config")
     assert rc > 0, msg
