@@ -206,6 +206,16 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         // (C3 equality 0.826 -> 0.675 ms per 1.25e8-row batch)
         X.window = 16;
         X.waves_per_eu = 8;
+        // ... and M sub-tiles share one look-back, their output pass two
+        // slices per wave at a time: 60 VGPRs, no spills at 8 waves/SIMD
+        // (DESIGN.md §4 "Sub-tiles")
+        X.M = 8;
+        X.KO = 2;
+    } else {
+        // Utf8 outputs of a numeric predicate: the LDS-image gather (the
+        // binary-search emitter's smaller LDS footprint only pays where few
+        // rows are selected)
+        X.gather = 4;
     }
     // diagnostic knobs (tools/*): read only when DFMI_DIAG is set -- a dozen
     // getenv scans per call would cost the 1024-row batch path microseconds
@@ -220,17 +230,24 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;
-        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 4;  // 2 = serial, 3 = two-pass
+        if (const char* e = getenv("DFMI_UTF8_PRESTAGE")) X.prestage = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 6;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_SUBTILES"))
+            if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
+        if (const char* e = getenv("DFMI_OUT_SLICES")) X.KO = atoi(e);
+        if (const char* e = getenv("DFMI_SUBTILE_PREFETCH")) X.prefetch = atoi(e) & 1;
     }
     // a numeric predicate's tiles are VGPR-limited (3 blocks/CU): LDS has room
     // for a 4 KiB staging arena per wave, which stages ~4 slices per round trip
     if (!X.utf8_outs.empty() && !X.pred_slots.empty()) X.arena = 256;
     if (diag)
         if (const char* e = getenv("DFMI_UTF8_ARENA")) X.arena = std::max(128, std::min(1024, atoi(e)));
-    if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.BLOCK / 64 > 256)
+    if (X.M == 1 || X.KO == 0) X.KO = X.K;
+    if (X.KO < 1 || X.KO > X.K || X.K % X.KO) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
+    if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.M * X.BLOCK / 64 > 256)
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
-    const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
+    const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
     const int64_t n_tiles = (n + tile_rows - 1) / tile_rows;
     if (n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
     // a filtered batch with one Utf8 output packs rows and bytes into one
@@ -662,7 +679,7 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
         ctx->last_kernel = X.kname;
 
         // ---- batch table
-        const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
+        const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
         std::vector<int64_t> first(nb), tiles(nb);
         int64_t T = 0;
         for (int32_t b = 0; b < nb; ++b) {

@@ -419,7 +419,7 @@ static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Lau
 // counts are needed before the look-back, so they share the first memory
 // round trip). Returns the Utf8 slots whose offsets are in registers.
 static std::vector<int> emit_predicate(Gen& g, std::ostringstream& o, const Plan& P, Launch& X, const std::string& cur,
-                                       const std::vector<int>& extra_offs) {
+                                       const std::vector<int>& extra_offs, bool preloaded = false) {
     const std::string head = o.str();
     g.tile_pre = true;
     g.pre_eq.clear();
@@ -436,6 +436,7 @@ static std::vector<int> emit_predicate(Gen& g, std::ostringstream& o, const Plan
     auto load_offs = [&](int u) {
         if (std::find(offs_loaded.begin(), offs_loaded.end(), u) != offs_loaded.end()) return;
         offs_loaded.push_back(u);
+        if (preloaded) return;  // us<u> / ux<u> already in scope (sub-tile prefetch)
         pre << "  int us" << offs_name(u) << "[K], ux" << offs_name(u)
             << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u << ", base, lane, wave, ~0u, us" << offs_name(u)
             << ", ux" << offs_name(u) << ");\n";
@@ -586,18 +587,16 @@ std::string generate(const Plan& P, Launch& X) {
         o << "  constexpr int NCH = " << nch << ";\n";
         const std::string tparams = std::to_string(X.R) + ", " + std::to_string(X.sleep) + ", " +
                                     std::to_string(X.spread) + ", " + std::to_string(X.window);
-        // One tile: predicate, projection-only loads, scan + look-back,
-        // compacted stores; `cur` names the tile's register set.
-        auto tile_body = [&](const std::string& cur, const std::string& T) {
-            o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
-            g.sfx = cur;
+        std::vector<int> utf8_out_cols;
+        for (const auto& uo : X.utf8_outs) utf8_out_cols.push_back(uo.second);
+        auto offs_name = [&](int u) { return std::to_string(u); };
+        // The predicate over the rows at `base`: selm, the projection-only
+        // loads (unless late), the selection ballots wm and counts cnt.
+        auto emit_select = [&]() {
             g.filtered_cols = false;
-            std::vector<int> utf8_out_cols;
-            for (const auto& uo : X.utf8_outs) utf8_out_cols.push_back(uo.second);
-            const std::vector<int> offs_loaded = emit_predicate(g, o, P, X, cur, utf8_out_cols);
-            auto offs_name = [&](int u) { return std::to_string(u) + cur; };
+            emit_predicate(g, o, P, X, "", utf8_out_cols);
             // projection-only columns, loaded only where selected
-            if (!X.late_proj) emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
+            if (!X.late_proj && X.M == 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
             // compaction offsets (rows + Utf8 bytes)
             o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
               << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
@@ -607,15 +606,17 @@ std::string generate(const Plan& P, Launch& X) {
                   << "[k], ux" << offs_name(u) << "[k], lane); cnt[" << (j + 1) << "][k] = ((selm >> k) & 1) ? "
                   << "(unsigned)(e_ - us" << offs_name(u) << "[k]) : 0u; }\n";
             }
-            {
-                o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << tparams << ">(A, " << T << ", t, cnt, lane, wave);\n";
-            }
+        };
+        // Compacted stores of the selected rows at `base` (selm, wm, the
+        // Utf8 offsets and the column registers in scope; the tile's offsets
+        // resolved in T); `kb`: the rows' first word of the tile.
+        auto emit_outputs = [&](const std::string& kb, bool prestaged) {
             // byte-light predicates: projection-only columns after the look-back
             // (fewer registers held across it; few rows are selected)
-            if (X.late_proj) emit_loads(o, X.proj_slots, X, cur, "base", "(selm >> k) & 1", false);
-            o << "  const i64 obase = (i64)" << T << ".prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
-              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)" << T
-              << ".excl[0][k * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
+            if (X.late_proj || X.M > 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
+              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][(" << kb
+              << " + k) * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
             // projections over the selected rows (filtered batch: no validity)
             g.filtered_cols = true;
             for (size_t oi = 0; oi < P.outs.size(); ++oi)
@@ -655,43 +656,115 @@ std::string generate(const Plan& P, Launch& X) {
             if (!X.utf8_outs.empty()) o << "  if (!(A.mode & 8)) {  // mode bit 3: skip the byte copies (diagnostics)\n";
             for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
                 const int u = X.utf8_outs[j].second;
+                const std::string tail = ", us" + offs_name(u) + ", ux" + offs_name(u) + ", ";
                 if (X.gather == 3)
-                    o << "  dfmi::utf8_offsets_src<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", "
-                      << X.utf8_outs[j].first << ", selm, wm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
-                      << ", lane, wave);\n";
+                    o << "  dfmi::utf8_offsets_src<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << X.utf8_outs[j].first
+                      << ", selm, wm, dst" << tail << "lane, wave, " << kb << ");\n";
                 else if (X.gather == 0)
-                    o << "  dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, " << T << ", " << (j + 1) << ", " << u << ", "
-                      << X.utf8_outs[j].first << ", selm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
-                      << ", lane, wave);\n";
+                    o << "  dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << u << ", "
+                      << X.utf8_outs[j].first << ", selm, dst" << tail << "lane, wave, " << kb << ");\n";
                 else
-                    o << "  dfmi::utf8_gather" << (X.gather == 2 ? "_serial" : "") << "<BLOCK, K, NCH, ARENA>(A, " << T
-                      << ", " << (j + 1) << ", " << u << ", "
-                      << X.utf8_outs[j].first << ", selm, wm, dst, us" << offs_name(u) << ", ux" << offs_name(u)
-                      << ", G[wave], lane, wave);\n";
+                    o << "  dfmi::utf8_gather" << (X.gather == 2 ? "_serial" : "") << "<BLOCK, K, NCH, ARENA>(A, T, "
+                      << (j + 1) << ", " << u << ", " << X.utf8_outs[j].first << ", selm, wm, dst" << tail
+                      << "G[wave], lane, wave, " << kb
+                      << (X.gather == 2 ? "" : X.gather == 4 ? ", 1" : X.gather == 5 ? ", 2" : ", 0")
+                      << (prestaged && j == 0 ? ", pre_" : "") << ");\n";
             }
             if (!X.utf8_outs.empty()) o << "  }\n";
-            if (!X.utf8_outs.empty()) {
-                o << "  if (tid == 0 && t == (unsigned)A.n_tiles - 1) {\n";
-                for (size_t j = 0; j < X.utf8_outs.size(); ++j)
-                    o << "    A.out_offs[" << X.utf8_outs[j].first << "][" << T << ".prefix[0] + " << T
-                      << ".agg[0]] = (int)(" << T << ".prefix[" << (j + 1) << "] + " << T << ".agg[" << (j + 1)
-                      << "]);\n";
-                o << "  }\n";
-            }
-            o << "  }\n";
-            g.sfx.clear();
         };
-        {
-            // one tile per block in dispatch order (in order per XCD, so every
-            // tile a block waits on in the look-back is running or done)
+        // The last tile writes every Utf8 output's final offset.
+        auto emit_last_offsets = [&]() {
+            if (X.utf8_outs.empty()) return;
+            o << "  if (tid == 0 && t == (unsigned)A.n_tiles - 1) {\n";
+            for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                o << "    A.out_offs[" << X.utf8_outs[j].first << "][T.prefix[0] + T.agg[0]] = (int)(T.prefix[" << (j + 1)
+                  << "] + T.agg[" << (j + 1) << "]);\n";
+            o << "  }\n";
+        };
+        // one tile per block in dispatch order (in order per XCD, so every
+        // tile a block waits on in the look-back is running or done)
+        if (!X.utf8_outs.empty() && X.gather && X.gather != 3)
+            o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA, "
+              << (X.gather == 1 ? "32" : X.gather == 5 ? "72" : "dfmi::kStageChunks + 1") << "> G[WAVES];\n";
+        o << "  const unsigned t = tile_;\n";
+        if (X.M == 1) {
+            // One tile: predicate, projection-only loads, scan + look-back,
+            // compacted stores.
             o << "  __shared__ dfmi::Tile<BLOCK, K, NCH> T;\n";
-            if (!X.utf8_outs.empty() && X.gather && X.gather != 3)
-                o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA> G[WAVES];\n";
-            o << "  const unsigned t = tile_;\n";
             emit_decls(o, X.pred_slots, X, "", true);
             emit_decls(o, X.proj_slots, X, "", false);
             emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
-            tile_body("", "T");
+            o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
+            emit_select();
+            // the first Utf8 output's first staging round goes out before the
+            // look-back, whose wait then hides it
+            const bool pre = !X.utf8_outs.empty() && (X.gather == 1 || X.gather >= 4) && X.prestage;
+            if (pre)
+                o << "  const int pre_ = dfmi::utf8_gather_prestage<K, ARENA>(A, " << X.utf8_outs[0].second
+                  << ", wm, us" << offs_name(X.utf8_outs[0].second) << ", ux" << offs_name(X.utf8_outs[0].second)
+                  << ", G[wave], lane);\n";
+            o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << tparams << ">(A, T, t, cnt, lane, wave);\n";
+            emit_outputs("0", pre);
+            emit_last_offsets();
+            o << "  }\n";
+        } else {
+            // M sub-tiles: the predicate pass keeps only each sub-tile's
+            // ballots and counts (LDS), one scan + look-back covers all of
+            // them, and the output pass revisits the sub-tiles with selected
+            // rows, reloading the Utf8 offsets and column values they need.
+            if (!X.pred_slots.empty()) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "sub-tiles need a Utf8-only predicate"};
+            o << "  constexpr int M = " << X.M << ";\n"
+              << "  __shared__ dfmi::Tile<BLOCK, K * M, NCH> T;\n  __shared__ u64 WS[K * M * WAVES];\n";
+            // software pipeline: sub-tile m+1's Utf8 offsets are loaded while
+            // sub-tile m's dependent loads (equality heads) are in flight
+            const size_t nu = X.utf8_cols.size();
+            for (size_t u = 0; u < nu && X.prefetch; ++u)
+                o << "  int usN" << u << "[K], uxN" << u << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u
+                  << ", (i64)t * M * (BLOCK * K), lane, wave, ~0u, usN" << u << ", uxN" << u << ");\n";
+
+            o << "  for (int m_ = 0; m_ < M; ++m_) {\n  const i64 base = ((i64)t * M + m_) * (BLOCK * K);\n"
+              << "  if (base >= A.n_rows) { if (tid < K * WAVES) { WS[m_ * K * WAVES + tid] = 0; }\n"
+              << "    for (int c_ = tid; c_ < NCH * K * WAVES; c_ += BLOCK) T.cnt[c_ / (K * WAVES)][m_ * K * WAVES + c_ % (K * WAVES)] = 0;\n"
+              << "    continue; }\n";
+            for (size_t u = 0; u < nu; ++u)
+                if (X.prefetch)
+                    o << "  int us" << u << "[K], ux" << u << "[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) { us" << u
+                      << "[k] = usN" << u << "[k]; ux" << u << "[k] = uxN" << u << "[k]; }\n"
+                      << "  if (m_ + 1 < M) dfmi::utf8_offs_tile<BLOCK, K>(A, " << u
+                      << ", base + BLOCK * K, lane, wave, ~0u, usN" << u << ", uxN" << u << ");\n";
+                else  // (diagnostics: each sub-tile loads its own offsets when it starts)
+                    o << "  int us" << u << "[K], ux" << u << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u
+                      << ", base, lane, wave, ~0u, us" << u << ", ux" << u << ");\n";
+            g.filtered_cols = false;
+            emit_predicate(g, o, P, X, "", utf8_out_cols, true);
+            o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+              << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
+            for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+                const int u = X.utf8_outs[j].second;
+                o << "#pragma unroll\n  for (int k = 0; k < K; ++k) { const int e_ = dfmi::utf8_end(us" << offs_name(u)
+                  << "[k], ux" << offs_name(u) << "[k], lane); cnt[" << (j + 1) << "][k] = ((selm >> k) & 1) ? "
+                  << "(unsigned)(e_ - us" << offs_name(u) << "[k]) : 0u; }\n";
+            }
+            o << "  dfmi::subtile_counts<BLOCK, K, NCH>(T, WS, m_ * K, cnt, wm, lane, wave);\n  }\n";
+            const std::string sp = std::to_string(X.spread);
+            o << "  dfmi::tile_scan_lds<BLOCK, K * M, NCH, " << sp << ">(A, T, t, lane, wave);\n"
+              << "  dfmi::tile_resolve<BLOCK, K * M, NCH, " << tparams << ">(A, T, t, lane, wave);\n"
+              << "  dfmi::lds_sync();\n";
+            // output pass in steps of KO slices (fewer registers than K)
+            o << "  {\n  constexpr int KS = K, K = " << X.KO << ";  // slices per sub-tile / per output step\n"
+              << "  for (int q_ = 0; q_ < M * KS; q_ += K) {\n"
+              << "  const i64 base = ((i64)t * M + q_ / KS) * (BLOCK * KS) + (i64)(q_ % KS) * BLOCK;\n"
+              << "  u64 wm[K];\n  unsigned selm = 0, need_ = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+              << "    wm[k] = dfmi::lds_uniform_u64(&WS[(q_ + k) * WAVES + wave]);\n"
+              << "    selm |= (unsigned)((wm[k] >> lane) & 1) << k;\n    need_ |= (unsigned)(wm[k] != 0) << k;\n  }\n"
+              << "  if (!need_) continue;\n";
+            for (int u : utf8_out_cols)
+                o << "  int us" << offs_name(u) << "[K], ux" << offs_name(u) << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, "
+                  << u << ", base, lane, wave, need_, us" << offs_name(u) << ", ux" << offs_name(u) << ");\n";
+            emit_decls(o, X.proj_slots, X, "", false);
+            emit_outputs("q_", false);
+            o << "  }\n  }\n";
+            emit_last_offsets();
         }
     } else {
         // projection only: dense rows, ballot-packed validity / Boolean bitmaps
@@ -785,7 +858,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

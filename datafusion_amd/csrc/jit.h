@@ -57,10 +57,21 @@ struct Launch {
     // (64 cost ~9% of the C2 kernel in polling traffic)
     int window = 8;
     int late_proj = 0;  // projection-only columns loaded after the look-back (byte-light predicates)
-    int gather = 1;  // Utf8 gather: 1 = wave-cooperative, consecutive slices staged together;
+    // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
+    // predicate over M sub-tiles of BLOCK * K rows, keeping only their
+    // selection ballots (LDS), then one scan + look-back for all of them and
+    // an output pass that reloads what the selected rows need
+    int M = 1;
+    int prefetch = 1;  // ... and load sub-tile m+1's Utf8 offsets while sub-tile m's heads are in flight
+    int KO = 0;  // ... whose output pass handles KO slices per wave at a time (divides K; 0 = K)
+    int gather = 1;  // Utf8 gather: 1 = wave-cooperative, consecutive slices staged together,
+                     //     lanes on output words found by binary search (utf8_emit_slice);
                      // 2 = one slice per round trip, 0 = per-lane copy (diagnostics);
                      // 3 = two passes: offsets + source starts, then k_utf8_copy_rows
+                     // 4 = as 1, but each slice assembled in an LDS image (round 2's form);
+                     // 5 = as 1, output words' strings found by a marker max-scan
     int arena = 128; // Utf8 gather staging arena per wave, 16-byte chunks
+    int prestage = 0;  // gather 1 / 4: the first staging round is issued before the look-back
     // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores
     int nt = 0;
     const dfmi_batch* in = nullptr;

@@ -520,29 +520,46 @@ struct Tile {
     static constexpr int WAVES = BLOCK / 64;
     static constexpr int NW = K * WAVES;  // 64-row words per tile
     static_assert(NW <= 256, "one wave scans the tile's words (up to 4 per lane)");
-    u64 cnt[NCH][NW];
+    unsigned cnt[NCH][NW];  // one slice's rows (<= 64) or Utf8 bytes (< 2^31)
     u64 excl[NCH][NW];
     u64 prefix[NCH];
     u64 agg[NCH];
 };
 
-// counts[ch][k] : per-lane value for row k (rows: 0/1 selection, Utf8: bytes)
-// First half of the tile step: per-(k, wave) counts, the one-wave scan of the
-// tile's words and the publication of the tile aggregate (no waiting).
-template <int BLOCK, int K, int NCH, int SPREAD = 1>
-__device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
-                                                  const unsigned (&cnt)[NCH][K], int lane, int wave) {
+// Sub-tile form of the counting step (multi-sub-tile tiles: M sub-tiles of K
+// slices per wave share one scan and one look-back): sub-tile words
+// [kb, kb + K) of T, and each (k, wave)'s selection ballot into `ws` (the
+// output pass reloads them instead of holding them across the look-back).
+template <int BLOCK, int K, int NCH, int KT>
+__device__ __forceinline__ void subtile_counts(Tile<BLOCK, KT, NCH>& T, u64* ws, int kb, const unsigned (&cnt)[NCH][K],
+                                               const u64 (&wm)[K], int lane, int wave) {
     constexpr int WAVES = BLOCK / 64;
-    constexpr int NW = K * WAVES;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            // Utf8 byte counts of one slice fit 32 bits (an array holds < 2^31 bytes)
-            const u64 s = ch == 0 ? (u64)__builtin_popcountll(__ballot(cnt[0][k] != 0))
-                                  : readlane_u(wave_incl_scan32(cnt[ch][k], lane), 63);
-            if (lane == 0) T.cnt[ch][k * WAVES + wave] = s;
+            const u64 s = ch == 0 ? (u64)__builtin_popcountll(wm[k]) : readlane_u(wave_incl_scan32(cnt[ch][k], lane), 63);
+            if (lane == 0) T.cnt[ch][(kb + k) * WAVES + wave] = (unsigned)s;
         }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (lane == 0) ws[(kb + k) * WAVES + wave] = wm[k];
+}
+
+// Uniform 64-bit LDS word (the same address in every lane) as a scalar.
+__device__ __forceinline__ u64 lds_uniform_u64(const u64* p) {
+    const u64 v = *p;
+    return ((u64)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
+}
+
+// The one-wave scan of the tile's words (T.cnt, written by every wave before
+// the barrier here) and the publication of the tile aggregate.
+template <int BLOCK, int K, int NCH, int SPREAD>
+__device__ __forceinline__ void tile_scan_lds(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile, int lane,
+                                              int wave) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int NW = K * WAVES;
     lds_sync();
     if (wave == 0) {
         u64 packed = 0;
@@ -553,7 +570,7 @@ __device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, 
 #pragma unroll
             for (int i = 0; i < NPL; ++i) {
                 const int w = lane * NPL + i;
-                c[i] = w < NW ? T.cnt[ch][w] : 0ull;
+                c[i] = w < NW ? (u64)T.cnt[ch][w] : 0ull;
                 tot += c[i];
             }
             const u64 incl = wave_incl_scan(tot, lane);
@@ -578,6 +595,25 @@ __device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, 
         if constexpr (NCH == 2)
             if (!(A.mode & 2)) lb_publish<SPREAD>(A.status, tile, packed, lane);
     }
+}
+
+// counts[ch][k] : per-lane value for row k (rows: 0/1 selection, Utf8: bytes)
+// First half of the tile step: per-(k, wave) counts, the one-wave scan of the
+// tile's words and the publication of the tile aggregate (no waiting).
+template <int BLOCK, int K, int NCH, int SPREAD = 1>
+__device__ __forceinline__ void tile_scan_publish(const Args& A, Tile<BLOCK, K, NCH>& T, unsigned tile,
+                                                  const unsigned (&cnt)[NCH][K], int lane, int wave) {
+    constexpr int WAVES = BLOCK / 64;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            // Utf8 byte counts of one slice fit 32 bits (an array holds < 2^31 bytes)
+            const u64 s = ch == 0 ? (u64)__builtin_popcountll(__ballot(cnt[0][k] != 0))
+                                  : readlane_u(wave_incl_scan32(cnt[ch][k], lane), 63);
+            if (lane == 0) T.cnt[ch][k * WAVES + wave] = (unsigned)s;
+        }
+    tile_scan_lds<BLOCK, K, NCH, SPREAD>(A, T, tile, lane, wave);
 }
 
 // Second half: wave 0 resolves the tile's global offsets into T.prefix; a
@@ -666,10 +702,10 @@ __device__ __forceinline__ void utf8_copy(const u8* src, u8* dst, unsigned L) {
 
 // Per-lane Utf8 gather: each selected lane copies its own string with
 // utf8_copy (diagnostic variant, DFMI_UTF8_GATHER=0).
-template <int BLOCK, int K, int NCH>
-__device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+template <int BLOCK, int K, int NCH, int KT = K>
+__device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
                                                  unsigned selm, const unsigned (&dst)[K], const int (&s)[K],
-                                                 const int (&nx)[K], int lane, int wave) {
+                                                 const int (&nx)[K], int lane, int wave, int kb = 0) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -680,7 +716,7 @@ __device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK
         const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
         const unsigned incl = wave_incl_scan32(L, lane);
         if (!sel) continue;
-        const u64 ob = bpre + T.excl[ch][k * WAVES + wave] + (incl - L);
+        const u64 ob = bpre + T.excl[ch][(kb + k) * WAVES + wave] + (incl - L);
         A.out_offs[o][obase + dst[k]] = (int)ob;
         if ((i64)(ob + L) > A.out_cap[o]) {
             report_err(A.err, 0, 0, ERRK_CAPACITY);
@@ -693,11 +729,14 @@ __device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK
 
 // LDS staging of one wave's Utf8 gather.
 constexpr int kStageChunks = 128;  // 16-byte source chunks of one slice's span: 2 KiB (longer: per-lane copy)
-template <int ARENA = kStageChunks>
+template <int ARENA = kStageChunks, int DST = kStageChunks + 1>
 struct Utf8Stage {
     static_assert(ARENA >= kStageChunks, "the arena holds at least one slice's span");
-    uint4 src[ARENA];              // source spans of consecutive slices, whole aligned 16-byte chunks
-    uint4 dst[kStageChunks + 1];   // one slice's output bytes, at their output address modulo 4
+    static_assert(DST >= 32, "room for utf8_emit_slice's lane table");
+    uint4 src[ARENA];  // source spans of consecutive slices, whole aligned 16-byte chunks
+    // one slice's output bytes at their output address modulo 4 (LDS-image
+    // variants: kStageChunks + 1 chunks), or utf8_emit_slice's lane table (32)
+    uint4 dst[DST];
 };
 
 typedef __attribute__((address_space(1))) void dfmi_gvoid;
@@ -738,11 +777,11 @@ __device__ __forceinline__ unsigned byte_mask(int lo, int hi) {
 // are whole aligned 16-byte chunks holding span bytes. One global round trip
 // per slice (diagnostic variant DFMI_UTF8_GATHER=2; utf8_gather below stages
 // consecutive slices together).
-template <int BLOCK, int K, int NCH, int ARENA>
-__device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+template <int BLOCK, int K, int NCH, int ARENA, int KT = K, int DST = kStageChunks + 1>
+__device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
                                                    unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
-                                                   const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA>& G,
-                                                   int lane, int wave) {
+                                                   const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA, DST>& G,
+                                                   int lane, int wave, int kb = 0) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -760,7 +799,7 @@ __device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLO
         const unsigned incl = wave_incl_scan32(L, lane);
         const unsigned rel = incl - L;
         const unsigned Ls = (unsigned)readlane_u(incl, 63);
-        const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
+        const u64 ob0 = bpre + T.excl[ch][(kb + k) * WAVES + wave];
         if (sel) A.out_offs[o][obase + dst[k]] = (int)(ob0 + rel);
         if ((i64)(ob0 + Ls) > A.out_cap[o]) {
             if (lane == 0) report_err(A.err, 0, 0, ERRK_CAPACITY);
@@ -852,6 +891,130 @@ __device__ __forceinline__ void utf8_place(const unsigned* sg, unsigned* gd, int
     }
 }
 
+// Output words of one slice from its staged source span sg (lanes on
+// consecutive output words, no per-string loops, no LDS image): each lane's
+// string is described by a two-entry table in LDS -- tend[l], the end of
+// lane l's output in image coordinates (image byte 0 = the aligned word
+// holding the slice's first output byte, which sits at image byte `sh`), and
+// tdel[l], source byte minus image byte for that string (lanes without a
+// string: zero length, tend = their left neighbour's). An output word finds
+// the string holding its first byte by a 6-step binary search over tend
+// (non-decreasing), takes its bytes with one v_alignbyte of two staged source
+// words, and repeats for the (rare) next string that starts inside the word:
+// at most 4 rounds. Interior words are stored whole; the two edge words the
+// slice shares with its neighbours bytewise.
+__device__ __forceinline__ int utf8_lb(const int* tend, int q) {  // first lane whose string ends after q
+    int i = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1)
+        if (tend[i + st - 1] <= q) i += st;
+    return i;
+}
+__device__ __forceinline__ void utf8_emit_slice(const unsigned* sg, int* tab, u8* w0, int sh, int iend, unsigned incl,
+                                                unsigned rel, int a, int lane) {
+    int* tend = tab;
+    int* tdel = tab + 64;
+    tend[lane] = sh + (int)incl;
+    tdel[lane] = a - (sh + (int)rel);
+    wave_lds_fence();
+    const int nw = (iend + 3) >> 2;
+    for (int j = lane; j < nw; j += 64) {
+        const int P = 4 * j;
+        const int hi = P + 4 < iend ? P + 4 : iend;
+        int lo = P > sh ? P : sh;
+        unsigned val = 0;
+#pragma unroll 1
+        while (lo < hi) {
+            const int i = utf8_lb(tend, lo);  // tend[i] > lo: string i holds image byte lo
+            const int e = tend[i] < hi ? tend[i] : hi;
+            const int sb = P + tdel[i];  // source byte of image byte P under string i's shift (>= -3)
+            const int sw = sb >> 2;      // arithmetic shift: -1 at most
+            const unsigned x = __builtin_amdgcn_alignbyte(sg[sw + 1], sg[sw < 0 ? 0 : sw], (unsigned)sb & 3u);
+            val |= x & byte_mask(lo - P, e - P);
+            lo = e;
+        }
+        if (P >= sh && P + 4 <= iend) {
+            *at<unsigned>(w0, P) = val;
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (P + b >= sh && P + b < iend) w0[P + b] = (u8)(val >> (8 * b));
+        }
+    }
+    wave_lds_fence();
+}
+
+// Inclusive max-scan over the wave (values >= 0; every lane active).
+__device__ __forceinline__ unsigned wave_incl_max32(unsigned v) {
+    v = max(v, dpp32<0x111, 0xf>(v));  // row_shr:1
+    v = max(v, dpp32<0x112, 0xf>(v));  // row_shr:2
+    v = max(v, dpp32<0x114, 0xf>(v));  // row_shr:4
+    v = max(v, dpp32<0x118, 0xf>(v));  // row_shr:8
+    v = max(v, dpp32<0x142, 0xa>(v));  // row_bcast:15
+    v = max(v, dpp32<0x143, 0xc>(v));  // row_bcast:31
+    return v;
+}
+
+// utf8_emit_slice with the string of each output word found by a marker
+// scan instead of a binary search: the last string starting in image word w
+// marks mk[w] with its lane + 1 (a string knows it is the last one starting
+// in its word when its end lies in a later word or it is the slice's last),
+// and a wave max-scan of the markers in word order gives every word the last
+// string starting before it -- where its first bytes come from. A word then
+// walks forward through the non-empty strings (`ne` ballot) that start inside
+// it: one or two rounds, at most four.
+__device__ __forceinline__ void utf8_emit_slice_mk(const unsigned* sg, int* tab, u8* mk, u8* w0, int sh, int iend,
+                                                   unsigned incl, unsigned rel, unsigned L, int a, int lane) {
+    int* tend = tab;
+    int* tdel = tab + 64;
+    const int st = sh + (int)rel, en = sh + (int)incl;
+    tend[lane] = en;
+    tdel[lane] = a - st;
+    const int nw = (iend + 3) >> 2;
+    for (int j = lane; j < nw; j += 64) mk[j] = 0;
+    wave_lds_fence();
+    const u64 ne = __ballot(L != 0);
+    if (L != 0 && ((en >> 2) != (st >> 2) || en >= iend)) mk[st >> 2] = (u8)(lane + 1);
+    wave_lds_fence();
+    unsigned carry = 0;  // last string starting before this round's first word
+    for (int j0 = 0; j0 < nw; j0 += 64) {
+        const int j = j0 + lane;
+        const unsigned m = j < nw ? (unsigned)mk[j] : 0u;
+        const unsigned incm = max(wave_incl_max32(m), carry);
+        const unsigned prev = max((unsigned)__builtin_amdgcn_update_dpp(0, (int)incm, 0x138, 0xf, 0xf, false), carry);  // wave_shr:1
+        carry = (unsigned)__builtin_amdgcn_readlane((int)incm, 63);
+        if (j >= nw) continue;
+        const int P = 4 * j;
+        const int hi = P + 4 < iend ? P + 4 : iend;
+        int lo = P > sh ? P : sh;
+        // first candidate: the last string starting before this word, else the first string
+        int i = prev ? (int)prev - 1 : __builtin_ctzll(ne);
+        unsigned val = 0;
+#pragma unroll 1
+        while (lo < hi) {
+            const int e = tend[i] < hi ? tend[i] : hi;
+            if (e > lo) {
+                const int sb = P + tdel[i];  // source byte of image byte P under string i's shift (>= -3)
+                const int sw = sb >> 2;
+                const unsigned x = __builtin_amdgcn_alignbyte(sg[sw + 1], sg[sw < 0 ? 0 : sw], (unsigned)sb & 3u);
+                val |= x & byte_mask(lo - P, e - P);
+                lo = e;
+            }
+            const u64 rest = i >= 63 ? 0ull : ne >> (i + 1);
+            if (!rest) break;
+            i += 1 + __builtin_ctzll(rest);
+        }
+        if (P >= sh && P + 4 <= iend) {
+            *at<unsigned>(w0, P) = val;
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (P + b >= sh && P + b < iend) w0[P + b] = (u8)(val >> (8 * b));
+        }
+    }
+    wave_lds_fence();
+}
+
 // The 16-byte-chunk source span of slice k (wave-uniform): chunks from the
 // one holding the first selected string's first byte to the one holding the
 // last one's last byte, as an offset from src and a count (0: no bytes).
@@ -862,19 +1025,78 @@ __device__ __forceinline__ void utf8_span(u64 m, int s, int e, i64 sm, i64& c0, 
     nch = s1 > s0 ? (int)(((s1 - 1 - c0) >> 4)) + 1 : 0;
 }
 
+// Every slice's source span (scalars): chunk offset from src and count.
+template <int K>
+__device__ __forceinline__ void utf8_spans(const u8* src, const u64 (&wm)[K], const int (&s)[K], const int (&nx)[K],
+                                           int lane, i64 (&cs)[K], int (&cn)[K]) {
+    const i64 sm = (i64)((u64)src & 15u);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        cs[k] = 0;
+        cn[k] = 0;
+        if (wm[k]) utf8_span(wm[k], s[k], utf8_end(s[k], nx[k], lane), sm, cs[k], cn[k]);
+    }
+}
+
+// Stage the spans of slice k and the following ones while they fit the
+// arena (direct global->LDS loads, no wait); returns the last slice covered
+// (slices whose span exceeds kStageChunks are copied per lane, not staged).
+template <int K, int ARENA>
+__device__ __forceinline__ int utf8_stage_group(const u8* src, const u64 (&wm)[K], const i64 (&cs)[K],
+                                                const int (&cn)[K], int k, uint4* arena, int lane) {
+    int staged_to = k - 1, used = 0;
+    bool full = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (j < k || full || !wm[j]) continue;
+        if (cn[j] > kStageChunks) {  // copied per lane when processed
+            if (j == k) staged_to = j;
+            else full = true;
+            continue;
+        }
+        if (used + cn[j] > ARENA) {
+            full = true;
+            continue;
+        }
+        stage_span(at<uint4>(src, cs[j]), arena + used, cn[j], lane);
+        used += cn[j];
+        staged_to = j;
+    }
+    return staged_to;
+}
+
+// The first staging round of utf8_gather, issued before the tile's look-back
+// so that the look-back's wait hides the staging loads; returns the `pre`
+// argument of utf8_gather (-1: nothing staged).
+template <int K, int ARENA, int DST>
+__device__ __forceinline__ int utf8_gather_prestage(const Args& A, int u, const u64 (&wm)[K], const int (&s)[K],
+                                                    const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane) {
+    const u8* src = A.bytes[u];
+    i64 cs[K];
+    int cn[K];
+    utf8_spans<K>(src, wm, s, nx, lane, cs, cn);
+    int k0 = -1;
+#pragma unroll
+    for (int k = K - 1; k >= 0; --k)
+        if (wm[k]) k0 = k;
+    return k0 < 0 ? -1 : utf8_stage_group<K, ARENA>(src, wm, cs, cn, k0, G.src, lane);
+}
+
 // Copy the selected rows of Utf8 input u into output o (rebased i32
-// offsets + bytes, filter.rs:94-105) as utf8_gather_serial does slice by
-// slice -- LDS image of each slice's output, coalesced word stores -- but
-// the source spans of consecutive slices are staged into the ARENA together
-// with direct global->LDS loads, one wait per arena-full: a tile's gather
-// pays about K * (span bytes) / (arena bytes) global round trips instead of K.
+// offsets + bytes, filter.rs:94-105), one 64-row slice at a time, the wave
+// cooperating: the source spans of consecutive slices are staged into the
+// ARENA together with direct global->LDS loads, one wait per arena-full (a
+// tile's gather pays about K * (span bytes) / (arena bytes) global round
+// trips instead of K; `pre` >= 0: the first round was staged before the
+// look-back by utf8_gather_prestage), and each slice's output words are
+// written by utf8_emit_slice (or, `image`, assembled in an LDS image first).
 // Only scalar state (where the staged round ends, the next arena offset) is
 // carried between slices.
-template <int BLOCK, int K, int NCH, int ARENA>
-__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+template <int BLOCK, int K, int NCH, int ARENA, int KT = K, int DST = kStageChunks + 1>
+__device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
                                             unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
-                                            const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA>& G, int lane,
-                                            int wave) {
+                                            const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane,
+                                            int wave, int kb = 0, int emit = 0, int pre = -1) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -882,36 +1104,21 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
     u8* out = A.out_data[o];
     const unsigned* gs = (const unsigned*)G.src;
     unsigned* gd = (unsigned*)G.dst;
-    const i64 sm = (i64)((u64)src & 15u);
-    int staged_to = -1;  // slices <= staged_to are in the arena (or need no staging)
-    int aoff = 0;        // arena chunk of the next staged slice to process
+    int staged_to = pre;  // slices <= staged_to are in the arena (or need no staging)
+    int aoff = 0;         // arena chunk of the next staged slice to process
+    i64 cs[K];
+    int cn[K];
+    utf8_spans<K>(src, wm, s, nx, lane, cs, cn);
+    if (pre >= 0) {
+        wait_vm_loads();
+        wave_lds_fence();
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const u64 m = wm[k];
         if (!m) continue;
         if (k > staged_to) {
-            // stage slice k and the following ones while their spans fit
-            int used = 0;
-            bool full = false;
-#pragma unroll
-            for (int j = k; j < K; ++j) {
-                if (full || !wm[j]) continue;
-                i64 cj;
-                int nj;
-                utf8_span(wm[j], s[j], utf8_end(s[j], nx[j], lane), sm, cj, nj);
-                if (nj > kStageChunks) {  // copied per lane when processed
-                    if (j == k) staged_to = j;
-                    else full = true;
-                    continue;
-                }
-                if (used + nj > ARENA) {
-                    full = true;
-                    continue;
-                }
-                stage_span(at<uint4>(src, cj), G.src + used, nj, lane);
-                used += nj;
-                staged_to = j;
-            }
+            staged_to = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k, G.src, lane);
             wait_vm_loads();
             wave_lds_fence();
             aoff = 0;
@@ -922,11 +1129,10 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
         const unsigned incl = wave_incl_scan32(L, lane);
         const unsigned rel = incl - L;
         const unsigned Ls = (unsigned)readlane_u(incl, 63);
-        const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
+        const u64 ob0 = bpre + T.excl[ch][(kb + k) * WAVES + wave];
         if (sel) A.out_offs[o][obase + dst[k]] = (int)(ob0 + rel);
-        i64 c0;
-        int nch;
-        utf8_span(m, s[k], e, sm, c0, nch);
+        const i64 c0 = cs[k];
+        const int nch = cn[k];
         const int my_off = aoff;
         if (nch <= kStageChunks) aoff += nch;
         if ((i64)(ob0 + Ls) > A.out_cap[o]) {
@@ -940,6 +1146,15 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
         }
         const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
         u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word holding the slice's first byte
+        if (emit == 2) {
+            utf8_emit_slice_mk(gs + 4 * my_off, (int*)gd, (u8*)(gd + 128), w0, sh, sh + (int)Ls, incl, rel, L,
+                               (int)(s[k] - c0), lane);
+            continue;
+        }
+        if (emit == 0 || DST <= kStageChunks) {  // (an LDS image needs the full dst)
+            utf8_emit_slice(gs + 4 * my_off, (int*)gd, w0, sh, sh + (int)Ls, incl, rel, (int)(s[k] - c0), lane);
+            continue;
+        }
         const int nw = (sh + (int)Ls + 3) >> 2;
         for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_fence();
@@ -965,10 +1180,10 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, K, 
 // library's k_utf8_copy_rows (kernels.hip) then copies the bytes as a dense
 // pass over the compacted rows -- lanes on consecutive output words, no
 // per-string loops in the query kernel.
-template <int BLOCK, int K, int NCH>
-__device__ __forceinline__ void utf8_offsets_src(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int o,
+template <int BLOCK, int K, int NCH, int KT = K>
+__device__ __forceinline__ void utf8_offsets_src(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int o,
                                                  unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
-                                                 const int (&s)[K], const int (&nx)[K], int lane, int wave) {
+                                                 const int (&s)[K], const int (&nx)[K], int lane, int wave, int kb = 0) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -979,7 +1194,7 @@ __device__ __forceinline__ void utf8_offsets_src(const Args& A, const Tile<BLOCK
         const int e = utf8_end(s[k], nx[k], lane);  // every lane (DPP)
         const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
         const unsigned incl = wave_incl_scan32(L, lane);
-        const u64 ob0 = bpre + T.excl[ch][k * WAVES + wave];
+        const u64 ob0 = bpre + T.excl[ch][(kb + k) * WAVES + wave];
         if (sel) {
             A.out_offs[o][obase + dst[k]] = (int)(ob0 + incl - L);
             A.out_src[o][obase + dst[k]] = s[k];
