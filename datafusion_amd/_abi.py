@@ -162,6 +162,8 @@ EXPORTED = [
     "dfmi_agg_state_partial",
     "dfmi_agg_merge_partials",
     "dfmi_agg_state_reset",
+    "dfmi_agg_state_create_grouped",
+    "dfmi_agg_state_finish_grouped",
     "dfmi_shard_unique_id",
     "dfmi_shard_comm_init",
     "dfmi_shard_comm_destroy",
@@ -307,6 +309,12 @@ def lib() -> C.CDLL:
     L.dfmi_aggregate_batch.restype = C.c_int32
     L.dfmi_agg_state_finish.argtypes = [C.c_void_p, C.c_void_p, P(dfmi_agg_value), P(dfmi_error)]
     L.dfmi_agg_state_finish.restype = C.c_int32
+    L.dfmi_agg_state_create_grouped.argtypes = [C.c_void_p, C.c_void_p, P(C.c_void_p), C.c_int32, P(C.c_void_p),
+                                                P(dfmi_error)]
+    L.dfmi_agg_state_create_grouped.restype = C.c_int32
+    L.dfmi_agg_state_finish_grouped.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, P(dfmi_agg_value), P(dfmi_agg_value),
+                                                P(C.c_int64), P(dfmi_error)]
+    L.dfmi_agg_state_finish_grouped.restype = C.c_int32
     L.dfmi_agg_partial_bytes.argtypes = [C.c_void_p]
     L.dfmi_agg_partial_bytes.restype = C.c_int64
     L.dfmi_agg_state_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(dfmi_error)]

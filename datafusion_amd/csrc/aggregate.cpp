@@ -13,6 +13,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <new>
 #include <string>
@@ -24,6 +25,13 @@
 using namespace dfmi;
 using namespace dfmi::xi;
 
+// One aggregate's merged state (host): the layout of a device copy with the
+// float digits carry-normalised (every digit but the top in [0, 2^32)).
+struct Partial_ {
+    uint64_t count = 0, flags = 0, key = 0, isum = 0;
+    int64_t limbs[dfmi::kAggLimbs] = {};
+};
+
 struct dfmi_aggregate {
     std::string name;  // as spelled in the SQL text (the Field name, sqlplanner.rs:385-389)
     int fn = 0;        // dfmi_agg_fn
@@ -34,11 +42,28 @@ struct dfmi_aggregate {
 struct dfmi_agg_state {
     int device = 0;
     std::vector<const dfmi_aggregate*> aggs;
-    uint64_t* acc = nullptr;  // [kAggCopies][n][kAggWords]
+    uint64_t* acc = nullptr;  // [kAggCopies][n][kAggWords]; grouped: [kAggCopies][gslots][n + 1][kAggWords]
     size_t acc_words = 0;
     bool failed = false;      // a batch raised an error: the query has failed
     dfmi_error failure{};
     std::vector<uint64_t> init;  // the zero state (MIN keys all ones)
+    // GROUP BY extension (dfmi_agg_state_create_grouped)
+    bool grouped = false;
+    dfmi_program key;           // the key (a copy: same uid, same kernels)
+    int gslots = 0;             // slots per accumulator copy: the key window + the null slot
+    uint64_t win_base = 0;      // the window the device accumulators hold ...
+    int win_width = -1;         // ... (-1: none yet)
+    bool dirty = false;         // the device accumulators hold rows
+    struct HKey {
+        bool null;
+        __int128 ord;
+        bool operator<(const HKey& o) const { return null != o.null ? !null : (!null && ord < o.ord); }
+    };
+    std::map<HKey, std::pair<uint64_t, std::vector<Partial_>>> groups;  // key -> (bits, partials)
+    // integer keys: the per-batch key window comes from MIN / MAX of the key
+    // over the batch's selected rows (a pre-pass through this same extension)
+    dfmi_aggregate* mm[2] = {nullptr, nullptr};
+    dfmi_agg_state* mm_state = nullptr;
 };
 
 namespace {
@@ -56,12 +81,7 @@ int agg_fn_of(const std::string& name) {
 bool is_float_type(int t) { return t == DFMI_TYPE_FLOAT32 || t == DFMI_TYPE_FLOAT64; }
 
 // ---- exact merge of accumulator copies (host)
-// One aggregate's merged state: the layout of a device copy with the float
-// digits carry-normalised (every digit but the top in [0, 2^32)).
-struct Partial {
-    uint64_t count = 0, flags = 0, key = 0, isum = 0;
-    int64_t limbs[kAggLimbs] = {};
-};
+using Partial = Partial_;
 
 void merge_into(Partial& p, const uint64_t* w, bool is_min) {
     p.count += w[0];
@@ -232,6 +252,7 @@ void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const df
                 throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batch column type does not match the schema"};
     };
     if (pred) check_schema(pred);
+    if (st->grouped) check_schema(&st->key);
     for (const dfmi_aggregate* a : st->aggs) check_schema(&a->arg);
     for (int i = 0; i < ncols; ++i)
         if (in->columns[i].length != n) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
@@ -249,6 +270,14 @@ void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const df
             }
     }
     int base = P + 2, nf = 0;
+    if (st->grouped) {  // the group key is evaluated before the aggregates
+        for (const IrNode& nd : st->key.ir)
+            if (nd.rt_code) se.offer((uint64_t)(base + nd.ordinal) << 44, nd.rt_code, nd.rt_msg);
+        B.plan.gkey = &st->key;
+        B.plan.gkey_ord = base;
+        B.plan.gslots = st->gslots;
+        base += st->key.length;
+    }
     for (const dfmi_aggregate* a : st->aggs) {
         for (const IrNode& nd : a->arg.ir)
             if (nd.rt_code) se.offer((uint64_t)(base + nd.ordinal) << 44, nd.rt_code, nd.rt_msg);
@@ -284,6 +313,7 @@ void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const df
         }
     };
     if (pred) reg_prog(pred, X.pred_slots);
+    if (st->grouped) reg_prog(&st->key, X.proj_slots);
     for (const dfmi_aggregate* a : st->aggs) reg_prog(&a->arg, X.proj_slots);
     if ((int)X.num_cols.size() > kArgCols || X.utf8_cols.size() > (size_t)kArgUtf8)
         throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many input columns"};
@@ -315,6 +345,51 @@ std::vector<uint64_t> read_acc(dfmi_context* ctx, dfmi_agg_state* st) {
     HIP_TRY(hipMemcpyAsync(h.data(), st->acc, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return h;
+}
+
+void merge_partial(Partial& into, const Partial& p, bool is_min) {
+    uint64_t w[kAggWords];
+    w[0] = p.count;
+    w[1] = p.flags;
+    w[2] = p.key;
+    w[3] = p.isum;
+    for (int i = 0; i < kAggLimbs; ++i) w[4 + i] = (uint64_t)p.limbs[i];
+    merge_into(into, w, is_min);
+}
+
+bool is_signed_type(int t) {
+    return t == DFMI_TYPE_INT8 || t == DFMI_TYPE_INT16 || t == DFMI_TYPE_INT32 || t == DFMI_TYPE_INT64;
+}
+
+// GROUP BY: the device accumulators (window win_base / win_width) merged into
+// the host's groups, and the device state reset.
+void flush_groups(dfmi_context* ctx, dfmi_agg_state* st) {
+    if (!st->dirty) return;
+    const std::vector<uint64_t> h = read_acc(ctx, st);
+    const size_t n = st->aggs.size(), na = n + 1;
+    const int kt = st->key.type;
+    for (int g = 0; g <= st->win_width; ++g) {
+        std::vector<Partial> parts(na);
+        for (size_t j = 0; j < na; ++j) {
+            const bool is_min = j < n && st->aggs[j]->fn == DFMI_AGG_MIN;
+            for (int c = 0; c < kAggCopies; ++c)
+                merge_into(parts[j], &h[(((size_t)c * st->gslots + g) * na + j) * kAggWords], is_min);
+            normalize(parts[j]);
+        }
+        if (parts[n].count == 0) continue;  // no row of this key in the window
+        dfmi_agg_state::HKey hk{g == st->win_width, 0};
+        uint64_t bits = 0;
+        if (!hk.null) {
+            bits = st->win_base + (uint64_t)g;
+            hk.ord = kt == DFMI_TYPE_BOOLEAN ? (__int128)bits
+                                             : (is_signed_type(kt) ? (__int128)(int64_t)bits : (__int128)bits);
+        }
+        auto it = st->groups.find(hk);
+        if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(n))).first;
+        for (size_t j = 0; j < n; ++j) merge_partial(it->second.second[j], parts[j], st->aggs[j]->fn == DFMI_AGG_MIN);
+    }
+    HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+    st->dirty = false;
 }
 
 }  // namespace
@@ -385,6 +460,87 @@ extern "C" int32_t dfmi_agg_state_create(dfmi_context* ctx, const dfmi_aggregate
     }
 }
 
+extern "C" int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key,
+                                                 const dfmi_aggregate* const* aggs, int32_t n, dfmi_agg_state** out,
+                                                 dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    dfmi_agg_state* st = nullptr;
+    try {
+        if (!ctx || !out || !key || n <= 0 || !aggs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        const int kt = key->type;
+        if (kt != DFMI_TYPE_BOOLEAN && !(is_numeric_type(kt) && !is_float_type(kt)))
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_debug(kt)};
+        if (n > 15) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 15 grouped aggregates"};
+        st = new dfmi_agg_state();
+        st->device = ctx->device;
+        st->grouped = true;
+        st->key = *key;
+        st->gslots = kt == DFMI_TYPE_BOOLEAN ? 3 : 17;  // false, true / 16 consecutive values; + null
+        for (int j = 0; j < n; ++j) {
+            if (!aggs[j]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL aggregate"};
+            st->aggs.push_back(aggs[j]);
+        }
+        const size_t na = (size_t)n + 1;
+        st->acc_words = (size_t)kAggCopies * st->gslots * na * kAggWords;
+        std::vector<uint64_t> init(st->acc_words, 0);
+        for (size_t cg = 0; cg < (size_t)kAggCopies * st->gslots; ++cg)
+            for (int j = 0; j < n; ++j)
+                if (aggs[j]->fn == DFMI_AGG_MIN) init[(cg * na + j) * kAggWords + 2] = ~0ull;
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipMalloc((void**)&st->acc, st->acc_words * 8));
+        HIP_TRY(hipMemcpyAsync(st->acc, init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        st->init = std::move(init);
+        if (kt != DFMI_TYPE_BOOLEAN) {
+            dfmi_error e2{};
+            for (int i = 0; i < 2; ++i)
+                if (dfmi_compile_aggregate(i ? "MAX" : "MIN", key, kt, DFMI_FLAG_EXT_AGGREGATE, &st->mm[i], &e2) != DFMI_OK)
+                    throw Fail{e2.code, e2.message};
+            const dfmi_aggregate* mm[2] = {st->mm[0], st->mm[1]};
+            if (dfmi_agg_state_create(ctx, mm, 2, &st->mm_state, &e2) != DFMI_OK) throw Fail{e2.code, e2.message};
+        }
+        *out = st;
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        dfmi_agg_state_free(st);
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_state* st, int64_t cap,
+                                                 dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups,
+                                                 dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st || !num_groups) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (!st->grouped) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return st->failure.code;
+        }
+        HIP_TRY(hipSetDevice(ctx->device));
+        flush_groups(ctx, st);
+        *num_groups = (int64_t)st->groups.size();
+        if (*num_groups > cap) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "group capacity too small"};
+        if (*num_groups > 0 && (!keys || !values)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        const size_t n = st->aggs.size();
+        int64_t g = 0;
+        for (const auto& [hk, v] : st->groups) {
+            keys[g].type = st->key.type;
+            keys[g].is_null = hk.null ? 1 : 0;
+            keys[g].bits = hk.null ? 0 : (st->key.type == DFMI_TYPE_BOOLEAN ? v.first : narrow_int(v.first, st->key.type));
+            keys[g].count = 0;
+            for (size_t j = 0; j < n; ++j) values[g * n + j] = finish_one(*st->aggs[j], v.second[j]);
+            ++g;
+        }
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
 extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, dfmi_error* err) {
     set_err(err, DFMI_OK, "");
     try {
@@ -393,6 +549,13 @@ extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, d
         HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
         st->failed = false;
         st->failure = dfmi_error{};
+        st->groups.clear();
+        st->win_width = -1;
+        st->dirty = false;
+        if (st->mm_state) {
+            dfmi_error e2{};
+            if (dfmi_agg_state_reset(ctx, st->mm_state, &e2) != DFMI_OK) throw Fail{e2.code, e2.message};
+        }
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -402,6 +565,9 @@ extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, d
 
 extern "C" void dfmi_agg_state_free(dfmi_agg_state* st) {
     if (!st) return;
+    dfmi_agg_state_free(st->mm_state);
+    dfmi_aggregate_free(st->mm[0]);
+    dfmi_aggregate_free(st->mm[1]);
     if (st->acc) {
         (void)hipSetDevice(st->device);
         (void)hipFree(st->acc);
@@ -430,6 +596,40 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
         const int64_t n = in->num_rows;
         HIP_TRY(hipSetDevice(ctx->device));
         hipStream_t stream = ctx->stream;
+        if (st->grouped && n > 0) {
+            // the batch's key window: Boolean keys always [false, true];
+            // integer keys 16 values from the batch's smallest selected key
+            uint64_t wbase = 0;
+            int wwidth = 2;
+            if (st->key.type != DFMI_TYPE_BOOLEAN) {
+                wwidth = st->gslots - 1;
+                dfmi_error e2{};
+                dfmi_agg_value mm[2];
+                if (dfmi_aggregate_batch(ctx, st->mm_state, pred, in, flags, &e2) != DFMI_OK ||
+                    dfmi_agg_state_finish(ctx, st->mm_state, mm, &e2) != DFMI_OK ||
+                    dfmi_agg_state_reset(ctx, st->mm_state, &e2) != DFMI_OK) {
+                    // the predicate or the key failed: evaluated before any aggregate
+                    st->failed = true;
+                    st->failure = e2;
+                    throw Fail{e2.code, e2.message};
+                }
+                const bool cover = st->win_width == wwidth && (mm[0].count == 0 || ((mm[0].bits - st->win_base) < (uint64_t)wwidth &&
+                                                                                   (mm[1].bits - st->win_base) < (uint64_t)wwidth));
+                if (cover) {
+                    wbase = st->win_base;
+                } else {
+                    wbase = mm[0].count ? mm[0].bits : 0;
+                    if (mm[0].count && mm[1].bits - mm[0].bits >= (uint64_t)wwidth)
+                        throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
+                                   "GROUP BY: more than 16 consecutive key values in one batch"};
+                }
+            }
+            if (st->win_width != wwidth || st->win_base != wbase) {
+                flush_groups(ctx, st);
+                st->win_base = wbase;
+                st->win_width = wwidth;
+            }
+        }
         ctx->timed = false;
         ctx->last_compile_ms = 0;
         uint64_t dev_key = ~0ull;
@@ -477,6 +677,8 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             A.clear_words = ws.clear_words;
             A.clear_hdr = (unsigned long long*)ws.clear_hdr;
             A.agg = (unsigned long long*)st->acc;
+            A.gbase = st->win_base;
+            A.gwidth = st->win_width;
             HIP_TRY(hipEventRecord(ctx->ev0, stream));
             size_t asz = sizeof A;
             void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
@@ -500,8 +702,11 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             ctx->last_total_ms = m2;
             ctx->timed = true;
         }
+        if (st->grouped && n > 0) st->dirty = true;
         Fail fail{DFMI_OK, ""};
-        if (dev_kind && (!se.set || dev_key < se.key))
+        if (dev_kind == ERRK_CAPACITY)  // a key outside the window the pre-pass found: cannot happen
+            fail = Fail{DFMI_ERR_DEVICE, "GROUP BY key outside the batch's key window"};
+        else if (dev_kind && (!se.set || dev_key < se.key))
             fail = dev_kind == ERRK_DIV_ZERO ? Fail{DFMI_ERR_DIVIDE_BY_ZERO, "DivideByZero"}
                                              : Fail{DFMI_ERR_PANIC, "attempt to divide with overflow"};
         else if (se.set)
@@ -528,6 +733,7 @@ extern "C" int32_t dfmi_agg_state_finish(dfmi_context* ctx, dfmi_agg_state* st, 
             if (err) *err = st->failure;
             return st->failure.code;
         }
+        if (st->grouped) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "a GROUP BY state: dfmi_agg_state_finish_grouped"};
         const std::vector<Partial> parts = merge_copies(st, read_acc(ctx, st));
         for (size_t j = 0; j < st->aggs.size(); ++j) out[j] = finish_one(*st->aggs[j], parts[j]);
         return DFMI_OK;
@@ -549,6 +755,7 @@ extern "C" int32_t dfmi_agg_state_partial(dfmi_context* ctx, dfmi_agg_state* st,
             if (err) *err = st->failure;
             return st->failure.code;
         }
+        if (st->grouped) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "partial state of a GROUP BY aggregate"};
         const std::vector<Partial> parts = merge_copies(st, read_acc(ctx, st));
         memcpy(host_out, parts.data(), parts.size() * sizeof(Partial));
         return DFMI_OK;
@@ -596,6 +803,32 @@ extern "C" int64_t dfmi_internal_agg_jit_check(const dfmi_program* pred, const d
     try {
         if (!in || !aggs || n <= 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
         dfmi_agg_state st;
+        for (int j = 0; j < n; ++j) st.aggs.push_back(aggs[j]);
+        AggBuilt B;
+        build_agg_plan(&st, pred, in, flags, B);
+        const std::string src = jit::generate(B.plan, B.X);
+        if (compile) (void)jit::compile_code(src, nullptr);
+        if (buf && cap > 0) snprintf(buf, (size_t)cap, "%s", src.c_str());
+        return (int64_t)src.size();
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return -(int64_t)f.code;
+    }
+}
+
+// Internal test hook: the GROUP BY form of the above (key: a Boolean or
+// integer program).
+extern "C" int64_t dfmi_internal_agg_grouped_jit_check(const dfmi_program* pred, const dfmi_program* key,
+                                                       const dfmi_aggregate* const* aggs, int32_t n,
+                                                       const dfmi_batch* in, uint32_t flags, int32_t compile, char* buf,
+                                                       int64_t cap, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!in || !aggs || !key || n <= 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        dfmi_agg_state st;
+        st.grouped = true;
+        st.key = *key;
+        st.gslots = key->type == DFMI_TYPE_BOOLEAN ? 3 : 17;
         for (int j = 0; j < n; ++j) st.aggs.push_back(aggs[j]);
         AggBuilt B;
         build_agg_plan(&st, pred, in, flags, B);

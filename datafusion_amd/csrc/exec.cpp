@@ -231,6 +231,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;
         if (const char* e = getenv("DFMI_UTF8_PRESTAGE")) X.prestage = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_GATHER_PHASES")) X.gather_phases = atoi(e) & 1;
         if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 6;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
         if (const char* e = getenv("DFMI_SUBTILES"))
@@ -513,6 +514,13 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                     dev_key = ~ew;
                     dev_kind = (int)(dev_key & 15);
                     dev_key &= ~15ull;
+                }
+                if (A.mode & 32) {
+                    uint64_t g5[5];
+                    memcpy(g5, ctx->host_hdr + kHdrStats + 64, sizeof g5);
+                    fprintf(stderr, "dfmi utf8 gather cycles (summed over waves): staging %llu setup %llu zero %llu place %llu "
+                            "store %llu\n", (unsigned long long)g5[0], (unsigned long long)g5[1], (unsigned long long)g5[2],
+                            (unsigned long long)g5[3], (unsigned long long)g5[4]);
                 }
                 if (A.mode & 4) {
                     uint64_t st3[3];

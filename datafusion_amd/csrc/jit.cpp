@@ -531,6 +531,107 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     o << "  dfmi::lds_sync();\n  dfmi::agg_block_flush<NA, NF>(A, S, fslot, is_min, tid);\n  }\n";
 }
 
+// GROUP BY form of the aggregate kernel (one Boolean / integer key): every
+// selected row's slot in the batch's key window (Args::gbase / gwidth, null
+// key: slot gwidth) is computed once; then, per slot present in the wave
+// (uniform loop), the arguments are reduced over that slot's rows exactly as
+// in generate_agg and flushed into the slot's LDS state. A hidden last
+// aggregate counts the slot's rows (so a group whose arguments are all null
+// still exists). Accumulators: [copies][GS][NA + 1][kAggWords].
+static void generate_agg_grouped(Gen& g, std::ostringstream& o, const Plan& P, Launch& X) {
+    const int NA = (int)P.aggs.size() + 1;  // + the group's row count
+    int NF = 0;
+    for (const AggSpec& a : P.aggs) NF += a.fslot >= 0;
+    o << "  constexpr int NA = " << NA << ", NF = " << NF << ", GS = " << P.gslots << ";\n";
+    o << "  __shared__ dfmi::AggLds<NA, NF> S[GS];\n  const unsigned char is_min[NA] = {";
+    for (int j = 0; j + 1 < NA; ++j) o << (P.aggs[j].fn == DFMI_AGG_MIN ? 1 : 0) << ", ";
+    o << "0};\n  const int fslot[NF > 0 ? NF : 1] = {";
+    {
+        bool any = false;
+        for (int j = 0; j + 1 < NA; ++j)
+            if (P.aggs[j].fslot >= 0) {
+                o << (any ? ", " : "") << j;
+                any = true;
+            }
+        if (!any) o << "0";
+    }
+    o << "};\n";
+    o << "  const int nslot = A.gwidth + 1;  // <= GS (host-checked)\n";
+    o << "  for (int g_ = wave; g_ < nslot; g_ += WAVES) dfmi::agg_lds_init<NA, NF>(S[g_], is_min, lane);\n";
+    o << "  const unsigned t = tile_;\n";
+    emit_decls(o, X.pred_slots, X, "", true);
+    emit_decls(o, X.proj_slots, X, "", !P.pred);
+    emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
+    o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
+    if (P.pred) {
+        g.filtered_cols = false;
+        emit_predicate(g, o, P, X, "", {});
+        emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+    } else {
+        o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) selm |= (unsigned)(base + k * BLOCK "
+             "+ tid < A.n_rows) << k;\n";
+        emit_loads(o, X.proj_slots, X, "", "base", nullptr, true);
+    }
+    g.filtered_cols = P.pred != nullptr;
+    // the key of every selected row (evaluated before the aggregates: its
+    // errors come first in evaluation order) -> its slot
+    o << "  unsigned gsl[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+      << "    const i64 row = base + k * BLOCK + tid;\n    const bool sel = (selm >> k) & 1;\n";
+    {
+        const Val kv = g.emit(P.gkey, P.gkey->root, P.gkey_ord, "sel");
+        if (P.gkey->type == DFMI_TYPE_BOOLEAN) {
+            o << "    gsl[k] = !(" << kv.n << ") ? (unsigned)A.gwidth : ((" << kv.v << ") ? 1u : 0u);\n";
+        } else {
+            o << "    { const u64 d_ = (u64)(" << (is_signed_int(P.gkey->type) ? "i64" : "u64") << ")(" << kv.v
+              << ") - A.gbase;\n"
+              << "      gsl[k] = !(" << kv.n << ") ? (unsigned)A.gwidth : (d_ < (u64)A.gwidth ? (unsigned)d_ : ~0u);\n"
+              << "      if (sel && gsl[k] == ~0u) dfmi::report_err(A.err, 0, 0, dfmi::ERRK_CAPACITY); }\n";
+        }
+    }
+    o << "  }\n  dfmi::lds_sync();\n";
+    o << "  for (int g_ = 0; g_ < nslot; ++g_) {\n"
+      << "    bool any_ = false;\n#pragma unroll\n    for (int k = 0; k < K; ++k) any_ |= ((selm >> k) & 1) && gsl[k] == (unsigned)g_;\n"
+      << "    if (!__ballot(any_)) continue;\n";
+    for (int j = 0; j < NA; ++j)
+        o << "  unsigned acnt" << j << " = 0, afl" << j << " = 0;\n  u64 asum" << j << " = 0, akey" << j << " = "
+          << (j + 1 < NA && P.aggs[j].fn == DFMI_AGG_MIN ? "~0ull" : "0ull") << ";\n";
+    o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+      << "    const i64 row = base + k * BLOCK + tid;\n    const bool sel = ((selm >> k) & 1) && gsl[k] == (unsigned)g_;\n"
+      << "    acnt" << NA - 1 << " += sel ? 1u : 0u;\n";
+    for (int j = 0; j + 1 < NA; ++j) {
+        const AggSpec& a = P.aggs[j];
+        const Val v = g.emit(a.prog, a.prog->root, a.ord_base, "sel");
+        const std::string ok = "ok" + std::to_string(j) + "_";
+        o << "    { const bool " << ok << " = sel && (" << v.n << ");\n";
+        o << "      acnt" << j << " += " << ok << " ? 1u : 0u;\n";
+        if (a.fn == DFMI_AGG_SUM && a.fslot < 0) {
+            o << "      asum" << j << " += " << ok << " ? (u64)(" << (is_signed_int(a.arg_type) ? "i64" : "u64") << ")("
+              << v.v << ") : 0ull;\n";
+        } else if (a.fn == DFMI_AGG_SUM) {
+            o << "      afl" << j << " |= " << ok << " ? dfmi::agg_sum_flags(" << v.v << ") : 0u;\n"
+              << "      const bool fin_ = " << ok << " && (dfmi::agg_sum_flags(" << v.v << ") == dfmi::AGGF_NONNEGZERO) && ("
+              << v.v << ") != 0;\n"
+              << "      dfmi::fsum_add(S[g_].limbs[" << a.fslot << "], &S[g_].dlo[" << a.fslot << "], &S[g_].dhi["
+              << a.fslot << "], (double)(" << v.v << "), fin_, lane);\n";
+        } else if (a.fn == DFMI_AGG_MIN || a.fn == DFMI_AGG_MAX) {
+            const char* cmp = a.fn == DFMI_AGG_MIN ? "<" : ">";
+            o << "      const bool nan_ = dfmi::agg_isnan(" << v.v << ");\n"
+              << "      afl" << j << " |= " << ok << " ? (nan_ ? (unsigned)dfmi::AGGF_NAN : (unsigned)dfmi::AGGF_VALUE) : 0u;\n"
+              << "      if (" << ok << " && !nan_) { const u64 k_ = dfmi::agg_key(" << v.v << "); if (k_ " << cmp << " akey" << j
+              << ") akey" << j << " = k_; }\n";
+        }
+        o << "    }\n";
+    }
+    o << "  }\n";
+    for (int j = 0; j < NA; ++j)
+        o << "  dfmi::agg_wave_flush<NA, NF>(S[g_], " << j << ", acnt" << j << ", asum" << j << ", akey" << j << ", "
+          << (j + 1 < NA && P.aggs[j].fn == DFMI_AGG_MIN ? "true" : "false") << ", afl" << j << ", lane);\n";
+    o << "  }\n  dfmi::lds_sync();\n"
+      << "  for (int g_ = 0; g_ < nslot; ++g_)\n"
+      << "    dfmi::agg_block_flush<NA, NF>(A, S[g_], fslot, is_min, tid, A.agg + ((u64)(blockIdx.x % dfmi::kAggCopies) * GS + "
+         "g_) * NA * dfmi::kAggWords);\n  }\n";
+}
+
 // Coalesced batches: this block's batch, its local tile index `tile_`, and a
 // local copy of the Args with the batch's rows, tiles, look-back status
 // segment, totals / error words and buffers (the copy is only ever indexed
@@ -580,7 +681,9 @@ std::string generate(const Plan& P, Launch& X) {
     } else {
         o << "  const dfmi::Args& A = A0;\n  const unsigned tile_ = blockIdx.x;\n";
     }
-    if (!P.aggs.empty()) {
+    if (!P.aggs.empty() && P.gkey) {
+        generate_agg_grouped(g, o, P, X);
+    } else if (!P.aggs.empty()) {
         generate_agg(g, o, P, X);
     } else if (P.pred) {
         const int nch = 1 + (int)X.utf8_outs.size();
@@ -668,7 +771,8 @@ std::string generate(const Plan& P, Launch& X) {
                       << (j + 1) << ", " << u << ", " << X.utf8_outs[j].first << ", selm, wm, dst" << tail
                       << "G[wave], lane, wave, " << kb
                       << (X.gather == 2 ? "" : X.gather == 4 ? ", 1" : X.gather == 5 ? ", 2" : ", 0")
-                      << (prestaged && j == 0 ? ", pre_" : "") << ");\n";
+                      << (X.gather == 2 ? "" : (prestaged && j == 0 ? ", pre_" : ", -1"))
+                      << (X.gather == 2 ? "" : X.gather_phases ? ", true" : ", false") << ");\n";
             }
             if (!X.utf8_outs.empty()) o << "  }\n";
         };
@@ -843,6 +947,9 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
     k.reserve(256);
     put(k, device);
     put(k, P.pred ? P.pred->uid : 0ull);
+    put(k, P.gkey ? P.gkey->uid : 0ull);
+    put(k, P.gkey_ord);
+    put(k, P.gslots);
     for (const AggSpec& a : P.aggs) {
         put(k, a.fn);
         put(k, a.prog ? a.prog->uid : 0ull);
@@ -858,7 +965,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -43,6 +43,11 @@ struct Plan {
     const dfmi_program* pred = nullptr;  // nullptr: projection only (dense kernel)
     std::vector<OutSpec> outs;
     std::vector<AggSpec> aggs;           // non-empty: the aggregate kernel (outs unused)
+    // GROUP BY extension: the key (Boolean / integer), its evaluation-order
+    // base, and the kernel's slot count (key window + the null slot)
+    const dfmi_program* gkey = nullptr;
+    int gkey_ord = 0;
+    int gslots = 0;
 };
 
 // Slot tables + literal pools of one launch.
@@ -71,7 +76,8 @@ struct Launch {
                      // 4 = as 1, but each slice assembled in an LDS image (round 2's form);
                      // 5 = as 1, output words' strings found by a marker max-scan
     int arena = 128; // Utf8 gather staging arena per wave, 16-byte chunks
-    int prestage = 0;  // gather 1 / 4: the first staging round is issued before the look-back
+    int prestage = 0;
+    int gather_phases = 0;  // diagnostics: per-phase cycle counters in utf8_gather (DFMI_DEBUG_MODE bit 5)  // gather 1 / 4: the first staging round is issued before the look-back
     // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores
     int nt = 0;
     const dfmi_batch* in = nullptr;

@@ -66,6 +66,10 @@ struct Args {
     // local copy of these Args (see jit.cpp "batched")
     const int* tile_batch;
     void* const* batch_ptrs;  // pointers and sizes (as pointer-sized integers)
+    // GROUP BY extension: the batch's key window -- key bits gbase + i for
+    // slot i < gwidth, slot gwidth for the null key (aggregate.cpp)
+    u64 gbase;
+    int gwidth;
 };
 
 // This block's share of zeroing the previous launch's workspace.
@@ -864,6 +868,30 @@ __device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLO
 __device__ __forceinline__ void utf8_place(const unsigned* sg, unsigned* gd, int a, int d, int L) {
     const int delta = a - d;  // source byte = output byte + delta
     const int wf = d >> 2, wl = (d + L - 1) >> 2;
+    if (wl - wf < 8) {
+        // up to 8 output words (strings up to 25..32 bytes): every source
+        // word read at once (one LDS round trip), output word i of the string
+        // is v_alignbyte(x[i + 1], x[i]) with one shift for the whole string
+        const int nwo = wl - wf + 1;
+        const int sw0 = (4 * wf + delta) >> 2;  // arithmetic shift: -1 at most
+        const unsigned sh = (unsigned)delta & 3u;
+        unsigned x[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) x[i] = i <= nwo ? sg[sw0 + i < 0 ? 0 : sw0 + i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i >= nwo) break;
+            const unsigned val = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
+            if (i == 0 || i == nwo - 1) {  // edge words: shared with the neighbouring strings
+                const int p = 4 * (wf + i) - d;
+                const unsigned msk = byte_mask(p < 0 ? -p : 0, p + 4 > L ? L - p : 4);
+                __hip_atomic_fetch_or(gd + wf + i, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            } else {
+                gd[wf + i] = val;
+            }
+        }
+        return;
+    }
     auto edge = [&](int w) {
         const int p = 4 * w - d;  // position of the word's first byte in the string (>= -3)
         const int sb = a + p;     // ... in the span (>= -3)
@@ -1096,7 +1124,7 @@ template <int BLOCK, int K, int NCH, int ARENA, int KT = K, int DST = kStageChun
 __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
                                             unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
                                             const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane,
-                                            int wave, int kb = 0, int emit = 0, int pre = -1) {
+                                            int wave, int kb = 0, int emit = 0, int pre = -1, bool prof = false) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -1109,6 +1137,21 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     i64 cs[K];
     int cn[K];
     utf8_spans<K>(src, wm, s, nx, lane, cs, cn);
+    // diagnostics (`prof`, compiled in by DFMI_GATHER_PHASES, and mode bit 5):
+    // shader cycles per phase summed over waves into stats[8..13): staging,
+    // slice setup, image zeroing, placing, stores. Reading the counter
+    // serialises the wave (~10x slower kernel): relative figures only.
+    const bool tp_on = prof && (A.mode & 32) != 0;
+    bool zeroed = false;  // LDS image (emit == 1) zeroed for this tile
+    u64 tacc[5] = {0, 0, 0, 0, 0};
+    u64 tcur = tp_on ? __builtin_readcyclecounter() : 0;
+    auto tick = [&](int ph) {
+        if (tp_on) {
+            const u64 n = __builtin_readcyclecounter();
+            tacc[ph] += n - tcur;
+            tcur = n;
+        }
+    };
     if (pre >= 0) {
         wait_vm_loads();
         wave_lds_fence();
@@ -1117,12 +1160,14 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     for (int k = 0; k < K; ++k) {
         const u64 m = wm[k];
         if (!m) continue;
+        tick(1);
         if (k > staged_to) {
             staged_to = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k, G.src, lane);
             wait_vm_loads();
             wave_lds_fence();
             aoff = 0;
         }
+        tick(0);
         const bool sel = (selm >> k) & 1;
         const int e = utf8_end(s[k], nx[k], lane);
         const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
@@ -1156,23 +1201,42 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             continue;
         }
         const int nw = (sh + (int)Ls + 3) >> 2;
-        for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
-        wave_lds_fence();
+        tick(1);
+        if (!zeroed) {  // the image is zero from here on: the store pass clears what it reads
+            for (int c = lane; c < DST; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
+            wave_lds_fence();
+            zeroed = true;
+        }
+        tick(2);
         if (L) utf8_place(gs + 4 * my_off, gd, (int)(s[k] - c0), sh + (int)rel, (int)L);
         wave_lds_fence();
-        for (int j = lane; j < nw; j += 64) {
-            const unsigned val = gd[j];
-            const int p = 4 * j - sh;  // output position of the word's first byte
-            if (p >= 0 && p + 4 <= (int)Ls) {
-                *at<unsigned>(w0, 4 * j) = val;
-            } else {
+        tick(3);
+        for (int j0 = 0; j0 < nw; j0 += 128) {
+            const int ja = j0 + lane, jb = ja + 64;
+            const unsigned va = ja < nw ? gd[ja] : 0u, vb = jb < nw ? gd[jb] : 0u;
+            if (ja < nw) gd[ja] = 0u;
+            if (jb < nw) gd[jb] = 0u;
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if (p + b >= 0 && p + b < (int)Ls) w0[4 * j + b] = (u8)(val >> (8 * b));
+            for (int h = 0; h < 2; ++h) {
+                const int j = h ? jb : ja;
+                const unsigned val = h ? vb : va;
+                if (j >= nw) continue;
+                const int p = 4 * j - sh;  // output position of the word's first byte
+                if (p >= 0 && p + 4 <= (int)Ls) {
+                    *at<unsigned>(w0, 4 * j) = val;
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if (p + b >= 0 && p + b < (int)Ls) w0[4 * j + b] = (u8)(val >> (8 * b));
+                }
             }
         }
         wave_lds_fence();
+        tick(4);
     }
+    if (tp_on && lane == 0)
+#pragma unroll
+        for (int i = 0; i < 5; ++i) atomicAdd(A.stats + 8 + i, tacc[i]);
 }
 
 // Two-pass Utf8 gather, first pass (Launch::gather == 3): the rebased output
@@ -1362,8 +1426,9 @@ __device__ __forceinline__ void agg_wave_flush(AggLds<NA, NF>& S, int j, unsigne
 // top one in [0, 2^32)), so a global digit absorbs 2^31 block partials.
 template <int NA, int NF>
 __device__ __forceinline__ void agg_block_flush(const Args& A, AggLds<NA, NF>& S, const int (&fslot)[NF > 0 ? NF : 1],
-                                                const unsigned char (&is_min)[NA > 0 ? NA : 1], int tid) {
-    u64* base = A.agg + (u64)(blockIdx.x % kAggCopies) * NA * kAggWords;
+                                                const unsigned char (&is_min)[NA > 0 ? NA : 1], int tid,
+                                                u64* base_ = nullptr) {
+    u64* base = base_ ? base_ : A.agg + (u64)(blockIdx.x % kAggCopies) * NA * kAggWords;
     if (tid < NA) {
         u64* w = base + tid * kAggWords;
         if (S.count[tid]) atomicAdd((unsigned long long*)&w[0], (unsigned long long)S.count[tid]);

@@ -1,9 +1,10 @@
-"""Aggregate relation (DFMI_FLAG_EXT_AGGREGATE): LogicalPlan::Aggregate with
-no GROUP BY over an optional Selection (sqlplanner.rs:91-117). The reference
-plans it and compiles its AggregateFunctions (compile_expr,
+"""Aggregate relation (DFMI_FLAG_EXT_AGGREGATE): LogicalPlan::Aggregate over
+an optional Selection (sqlplanner.rs:91-117), without or with one GROUP BY
+key. The reference plans it and compiles its AggregateFunctions (compile_expr,
 expression.rs:81-116) but its executor stops at context.rs:161
 (`unimplemented!()`); here every input batch is one fused predicate +
-aggregate pass on the GPU and next() returns the single result row."""
+aggregate pass on the GPU and next() returns the result: one row, or one row
+per group in key order (null key last)."""
 from __future__ import annotations
 
 from typing import List, Optional
@@ -31,6 +32,19 @@ def agg_value_array(v) -> Array:
     return Array.from_numpy(t, vals, np.array([not v.is_null]) if v.is_null else None)
 
 
+def agg_values_array(vals) -> Array:
+    """An Array of several aggregate / group-key values (dfmi_agg_value), one row each."""
+    if not vals:
+        return Array.from_pylist(DataType.Boolean, [])
+    t = DataType(vals[0].type)
+    valid = np.array([not v.is_null for v in vals])
+    if t == DataType.Boolean:
+        return Array.from_numpy(t, np.array([bool(v.bits) for v in vals]), None if valid.all() else valid)
+    dt = np.dtype(_NP[t])
+    raw = np.array([v.bits for v in vals], dtype=np.uint64).view(np.uint8).reshape(-1, 8)[:, : dt.itemsize].copy()
+    return Array.from_numpy(t, raw.reshape(-1).view(dt), None if valid.all() else valid)
+
+
 def agg_value_py(v):
     """The aggregate value as a Python scalar (None for null)."""
     if v.is_null:
@@ -39,13 +53,16 @@ def agg_value_py(v):
 
 
 class AggregateRelation(Relation):
-    """Aggregate(input, group_expr=[], aggr_expr) with the input's Selection
-    (if any) fused: pulls every batch of `input`, then yields one batch."""
+    """Aggregate(input, group_expr, aggr_expr) with the input's Selection (if
+    any) fused: pulls every batch of `input`, then yields one batch -- the
+    group key column (if any) followed by the aggregates."""
 
-    def __init__(self, input: Relation, predicate, aggs: List, schema: Schema, device=None, flags: int = 0):
+    def __init__(self, input: Relation, predicate, aggs: List, schema: Schema, device=None, flags: int = 0,
+                 key=None):
         self.input = input
         self.predicate = predicate
         self.aggs = aggs
+        self.key = key
         self._schema = schema
         self.device = device
         self.flags = flags
@@ -55,13 +72,20 @@ class AggregateRelation(Relation):
         if self.done:
             return None
         self.done = True
-        state = engine(self.device).agg_state(self.aggs)
+        eng = engine(self.device)
+        state = eng.agg_state(self.aggs) if self.key is None else eng.grouped_agg_state(self.key, self.aggs)
         while True:
             b = self.input.next()
             if b is None:
                 break
             state.add(self.predicate, b, self.flags)
-        return RecordBatch(self._schema, [agg_value_array(v) for v in state.finish()])
+        if self.key is None:
+            return RecordBatch(self._schema, [agg_value_array(v) for v in state.finish()])
+        keys, vals = state.finish()
+        if not keys:
+            return None
+        cols = [agg_values_array(keys)] + [agg_values_array([g[j] for g in vals]) for j in range(len(self.aggs))]
+        return RecordBatch(self._schema, cols)
 
     def schema(self) -> Schema:
         return self._schema

@@ -6,7 +6,7 @@ from __future__ import annotations
 from typing import Dict
 
 from ..arrow import Field, Schema
-from ..logicalplan import Column, Expr, PlanError, expr_to_field_name_type
+from ..logicalplan import Column, DataType, Expr, PlanError, expr_to_field_name_type
 from .error import ExecutionError
 from .aggregate import AggregateRelation
 from .expression import compile_expr, compile_scalar_expr
@@ -108,8 +108,8 @@ class ExecutionContext:
         from .. import _abi
         if not (self.flags & _abi.DFMI_FLAG_EXT_AGGREGATE):
             raise ExecutionError("panic", "not yet implemented")
-        if plan.group_expr:
-            raise ExecutionError("NotImplemented", "GROUP BY on the device path")
+        if len(plan.group_expr) > 1:
+            raise ExecutionError("NotImplemented", "GROUP BY over more than one expression")
         inp, pred = plan.input, None
         if isinstance(inp, Selection):
             source = self.execute(inp.input)
@@ -117,6 +117,11 @@ class ExecutionContext:
         else:
             source = self.execute(inp)
         input_schema = source.schema()
+        key = None
+        fields = []
+        if plan.group_expr:  # GROUP BY extension: the key column first (sqlplanner.rs:108-111)
+            key = compile_scalar_expr(self, plan.group_expr[0], input_schema, self.flags)
+            fields.append(Field(key.get_name(), DataType(key.get_type()), True))
         aggs = [compile_expr(self, e, input_schema, self.flags) for e in plan.aggr_expr]
-        schema = Schema([Field(e.name, e.return_type, True) for e in plan.aggr_expr])  # sqlplanner.rs:385-389
-        return AggregateRelation(source, pred, aggs, schema, self.device, self.flags)
+        fields += [Field(e.name, e.return_type, True) for e in plan.aggr_expr]  # sqlplanner.rs:385-389
+        return AggregateRelation(source, pred, aggs, Schema(fields), self.device, self.flags, key)

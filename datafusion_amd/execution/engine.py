@@ -295,18 +295,27 @@ class DeviceEngine:
         """Device accumulators for one Aggregate plan (dfmi_agg_state_create)."""
         return AggState(self, aggs)
 
+    def grouped_agg_state(self, key, aggs: Sequence) -> "GroupedAggState":
+        """Device accumulators for one Aggregate plan with a GROUP BY key
+        (dfmi_agg_state_create_grouped)."""
+        return GroupedAggState(self, key, aggs)
+
 
 class AggState:
     """dfmi_agg_state: accumulates batches of one Aggregate plan on one GPU."""
 
-    def __init__(self, eng: DeviceEngine, aggs: Sequence):
+    def __init__(self, eng: DeviceEngine, aggs: Sequence, key=None):
         self.eng = eng
         self.aggs = list(aggs)
+        self.key = key
         L = _abi.lib()
         arr = (C.c_void_p * len(self.aggs))(*[a.handle.value for a in self.aggs])
         out = C.c_void_p()
         err = _abi.dfmi_error()
-        rc = L.dfmi_agg_state_create(eng.ctx, arr, len(self.aggs), C.byref(out), C.byref(err))
+        if key is None:
+            rc = L.dfmi_agg_state_create(eng.ctx, arr, len(self.aggs), C.byref(out), C.byref(err))
+        else:
+            rc = L.dfmi_agg_state_create_grouped(eng.ctx, key.handle, arr, len(self.aggs), C.byref(out), C.byref(err))
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
         self.handle = out
@@ -357,6 +366,33 @@ class AggState:
             except Exception:
                 pass
             self.handle = C.c_void_p(0)
+
+
+class GroupedAggState(AggState):
+    """dfmi_agg_state with a GROUP BY key: finish() returns (keys, values)
+    -- one dfmi_agg_value key per group in key order (null last) and per group
+    the aggregate values."""
+
+    def __init__(self, eng: DeviceEngine, key, aggs: Sequence):
+        super().__init__(eng, aggs, key)
+
+    def finish(self):
+        L = _abi.lib()
+        n = len(self.aggs)
+        ng = C.c_int64()
+        err = _abi.dfmi_error()
+        cap = 64
+        while True:
+            keys = (_abi.dfmi_agg_value * cap)()
+            vals = (_abi.dfmi_agg_value * (cap * n))()
+            rc = L.dfmi_agg_state_finish_grouped(self.eng.ctx, self.handle, cap, keys, vals, C.byref(ng), C.byref(err))
+            if rc == _abi.DFMI_ERR_INVALID_ARGUMENT and ng.value > cap:
+                cap = ng.value
+                continue
+            if rc != _abi.DFMI_OK:
+                raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+            g = ng.value
+            return list(keys[:g]), [list(vals[i * n:(i + 1) * n]) for i in range(g)]
 
 
 def merge_agg_partials(aggs: Sequence, partials: Sequence[bytes]) -> List[_abi.dfmi_agg_value]:

@@ -344,7 +344,13 @@ int32_t dfmi_last_error_order(const dfmi_context* ctx, uint64_t* key);
  *   MIN/MAX(e): NaN values are skipped (a set of only NaNs gives the
  *             canonical NaN), -0.0 orders below +0.0;
  *   SUM/MIN/MAX over no non-null value is null.
- * GROUP BY is not implemented (NotImplemented).
+ * GROUP BY (dfmi_agg_state_create_grouped): one key, Boolean or integer;
+ * per group the aggregates above. Groups come out in key order (false <
+ * true, integers numerically) with the null key last -- the order of the
+ * reference's expected/csv_aggregate_by_c_bool.csv. Low-cardinality keys:
+ * the selected rows of one batch may hold at most 16 consecutive integer key
+ * values (any number of batches, any number of groups overall); a wider batch
+ * is NotImplemented.
  * ------------------------------------------------------------------------- */
 typedef enum dfmi_agg_fn {       /* AggregateType (expression.rs:33-40) */
     DFMI_AGG_MIN = 0,
@@ -396,6 +402,19 @@ int32_t dfmi_agg_state_partial(dfmi_context* ctx, dfmi_agg_state* state, void* h
 int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, int32_t num_aggs,
                                 const void* const* partials, int32_t num_partials, dfmi_agg_value* out,
                                 dfmi_error* err);
+/* GROUP BY extension: LogicalPlan::Aggregate{group_expr: [key]}
+ * (sqlplanner.rs:91-117; the reference's executor stops at context.rs:161).
+ * `key` compiled by dfmi_compile_scalar_expr over the same schema (Boolean or
+ * an integer type; otherwise NotImplemented "GROUP BY over <type>"), at most
+ * 15 aggregates. Batches go through dfmi_aggregate_batch. */
+int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key, const dfmi_aggregate* const* aggs,
+                                      int32_t num_aggs, dfmi_agg_state** out, dfmi_error* err);
+/* The groups so far, in key order: keys[g] (type = the key's type, is_null,
+ * bits: Boolean 0/1, integers sign/zero-extended; count = the group's selected
+ * rows) and values[g * num_aggs + j]. *num_groups is set even when it exceeds
+ * `capacity` (then DFMI_ERR_INVALID_ARGUMENT and nothing is written). */
+int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_state* state, int64_t capacity, dfmi_agg_value* keys,
+                                      dfmi_agg_value* values, int64_t* num_groups, dfmi_error* err);
 /* Back to the empty state (asynchronous on the context stream): re-running the query. */
 int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
 void dfmi_agg_state_free(dfmi_agg_state* state);

@@ -30,6 +30,7 @@
 #include <functional>
 #include <limits>
 #include <type_traits>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -1019,11 +1020,17 @@ T from_bits64(uint64_t b) {
     return v;
 }
 
+void agg_accumulate_row(AggState& st, const Array& a, int64_t i);
+
 void agg_accumulate(AggState& st, const Array& a) {
-    for (int64_t i = 0; i < a.len; ++i) {
-        if (a.is_null(i)) continue;
+    for (int64_t i = 0; i < a.len; ++i) agg_accumulate_row(st, a, i);
+}
+
+void agg_accumulate_row(AggState& st, const Array& a, int64_t i) {
+    {
+        if (a.is_null(i)) return;
         ++st.count;
-        if (st.fn == DFMI_AGG_COUNT) continue;
+        if (st.fn == DFMI_AGG_COUNT) return;
         dispatch_numeric(a.type, [&](auto tag) {
             using T = decltype(tag);
             const T v = a.value<T>(i);
@@ -1053,6 +1060,33 @@ void agg_accumulate(AggState& st, const Array& a) {
             st.has_key = true;
         });
     }
+}
+
+// GROUP BY key of row i of the key array: (null, order value, bits). Groups
+// are ordered by key value -- false < true, integers numerically -- with the
+// null group last (the order of expected/csv_aggregate_by_c_bool.csv).
+struct GroupKey {
+    bool null;
+    __int128 ord;
+    bool operator<(const GroupKey& o) const { return null != o.null ? !null : (!null && ord < o.ord); }
+};
+GroupKey group_key(const Array& a, int64_t i, uint64_t* bits) {
+    *bits = 0;
+    if (a.is_null(i)) return {true, 0};
+    if (a.type == DFMI_TYPE_BOOLEAN) {
+        *bits = a.bool_value(i) ? 1 : 0;
+        return {false, (__int128)*bits};
+    }
+    __int128 ord = 0;
+    dispatch_numeric(a.type, [&](auto tag) {
+        using T = decltype(tag);
+        if constexpr (std::is_integral<T>::value) {
+            const T v = a.value<T>(i);
+            *bits = to_bits64(v);
+            ord = (__int128)v;
+        }
+    });
+    return {false, ord};
 }
 
 dfmi_agg_value agg_result(const AggState& st) {
@@ -1234,6 +1268,73 @@ int32_t oracle_aggregate(const dfmi_expr_node* pred_nodes, int32_t pred_len, con
             for (int j = 0; j < n; ++j) agg_accumulate(st[j], *args[j].f(f));
         }
         for (int j = 0; j < n; ++j) out[j] = agg_result(st[j]);
+        return DFMI_OK;
+    } catch (const ExecError& e) {
+        set_err(err, e.code, e.msg);
+        return e.code;
+    }
+}
+
+// GROUP BY extension: LogicalPlan::Aggregate{group_expr: [key]} (the
+// planner's form, sqlplanner.rs:91-117) -- one Boolean or integer key; per
+// group the aggregates of the no-GROUP-BY form. keys[g] / out[g * n + j] in
+// group order (GroupKey); *num_groups is set even when cap is too small.
+int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_len, const dfmi_expr_node* key_nodes,
+                                 int32_t key_len, const char* const* names, const dfmi_expr_node* const* arg_nodes,
+                                 const int32_t* arg_lens, const int32_t* return_types, int32_t n,
+                                 const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
+                                 uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
+                                 int64_t* num_groups, dfmi_error* err) {
+    try {
+        set_err(err, DFMI_OK, "");
+        if (!(flags & DFMI_FLAG_EXT_AGGREGATE)) fail(DFMI_ERR_PANIC, "not yet implemented");  // context.rs:161
+        Plan p = make_plan(pred_nodes, pred_len, nullptr, nullptr, 0, schema, flags);
+        ExprP kt = build_tree(key_nodes, key_len);
+        Runtime key = compile(*kt, *schema, flags);
+        if (key.t != DFMI_TYPE_BOOLEAN && !(is_numeric(key.t) && key.t != DFMI_TYPE_FLOAT32 && key.t != DFMI_TYPE_FLOAT64))
+            fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_name(key.t));
+        std::vector<Runtime> args;
+        std::vector<AggState> proto(n);
+        for (int j = 0; j < n; ++j) {
+            const int fn = agg_fn_of(names[j]);
+            ExprP t = build_tree(arg_nodes[j], arg_lens[j]);
+            args.push_back(compile(*t, *schema, flags));
+            proto[j].fn = fn;
+            proto[j].arg_type = args[j].t;
+            proto[j].ret_type = return_types[j];
+            const int want = fn == DFMI_AGG_COUNT ? DFMI_TYPE_UINT64 : args[j].t;
+            if (return_types[j] != want) fail(DFMI_ERR_INVALID_ARGUMENT, "aggregate return type");
+            if (fn != DFMI_AGG_COUNT && !is_numeric(args[j].t))
+                fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("aggregate over ") + type_name(args[j].t));
+        }
+        std::map<GroupKey, std::pair<uint64_t, std::vector<AggState>>> groups;
+        if (batch_rows <= 0) batch_rows = std::max<int64_t>(1, input->num_rows);
+        for (int64_t r0 = 0; r0 < input->num_rows; r0 += batch_rows) {
+            const int64_t rows = std::min(batch_rows, input->num_rows - r0);
+            Batch in = wrap_input(input, r0, rows);
+            Batch f = run_batch(p, in, flags);  // FilterRelation::next (or the batch itself)
+            ArrayRef ka = key.f(f);             // the key first, then the aggregates in order
+            std::vector<ArrayRef> av;
+            for (int j = 0; j < n; ++j) av.push_back(args[j].f(f));
+            for (int64_t i = 0; i < f.num_rows; ++i) {
+                uint64_t bits;
+                const GroupKey gk = group_key(*ka, i, &bits);
+                auto it = groups.find(gk);
+                if (it == groups.end()) it = groups.emplace(gk, std::make_pair(bits, proto)).first;
+                for (int j = 0; j < n; ++j) agg_accumulate_row(it->second.second[j], *av[j], i);
+            }
+        }
+        *num_groups = (int64_t)groups.size();
+        if ((int64_t)groups.size() > cap) fail(DFMI_ERR_INVALID_ARGUMENT, "group capacity too small");
+        int64_t g = 0;
+        for (const auto& [gk, v] : groups) {
+            keys[g].type = key.t;
+            keys[g].is_null = gk.null ? 1 : 0;
+            keys[g].bits = v.first;
+            keys[g].count = 0;
+            for (int j = 0; j < n; ++j) out[g * n + j] = agg_result(v.second[j]);
+            ++g;
+        }
         return DFMI_OK;
     } catch (const ExecError& e) {
         set_err(err, e.code, e.msg);

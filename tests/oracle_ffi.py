@@ -48,6 +48,12 @@ def oracle_lib() -> C.CDLL:
                                    P(C.c_int32), P(C.c_int32), C.c_int32, P(_abi.dfmi_schema), P(_abi.dfmi_batch),
                                    C.c_int64, C.c_uint32, P(_abi.dfmi_agg_value), P(_abi.dfmi_error)]
     L.oracle_aggregate.restype = C.c_int32
+    L.oracle_aggregate_grouped.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(_abi.dfmi_expr_node), C.c_int32,
+                                           P(C.c_char_p), P(P(_abi.dfmi_expr_node)), P(C.c_int32), P(C.c_int32),
+                                           C.c_int32, P(_abi.dfmi_schema), P(_abi.dfmi_batch), C.c_int64, C.c_uint32,
+                                           C.c_int64, P(_abi.dfmi_agg_value), P(_abi.dfmi_agg_value), P(C.c_int64),
+                                           P(_abi.dfmi_error)]
+    L.oracle_aggregate_grouped.restype = C.c_int32
     L.oracle_gen_unit_f64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_void_p]
     L.oracle_gen_i64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_void_p]
     _L = L
@@ -201,3 +207,36 @@ def oracle_aggregate(schema: Schema, batch: RecordBatch, pred: Optional[Expr], a
     if rc != _abi.DFMI_OK:
         raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
     return list(out)
+
+
+def oracle_aggregate_grouped(schema: Schema, batch: RecordBatch, pred: Optional[Expr], key: Expr, aggs: Sequence,
+                             flags: int = None, batch_rows: int = 0, cap: int = 4096):
+    """Aggregate{group_expr: [key]}(Selection?(scan)) on the oracle: returns
+    (keys, values) -- one dfmi_agg_value key per group (key order, null
+    last) and per group the list of aggregate values -- or raises
+    ExecutionError."""
+    if flags is None:
+        flags = _abi.DFMI_FLAG_EXT_AGGREGATE
+    L = oracle_lib()
+    hb = Batched(batch)
+    sch, keep = _abi.make_schema([(f.name, f.data_type, f.nullable) for f in schema.fields])
+    pn = _abi.PostfixNodes(pred.to_postfix()) if pred is not None else None
+    kn = _abi.PostfixNodes(key.to_postfix())
+    n = len(aggs)
+    arg_nodes = [_abi.PostfixNodes(a.args[0].to_postfix()) for a in aggs]
+    names = (C.c_char_p * max(1, n))(*[a.name.encode() for a in aggs])
+    arr = (C.POINTER(_abi.dfmi_expr_node) * max(1, n))(*[C.cast(x.array, C.POINTER(_abi.dfmi_expr_node))
+                                                          for x in arg_nodes])
+    lens = (C.c_int32 * max(1, n))(*[x.length for x in arg_nodes])
+    rts = (C.c_int32 * max(1, n))(*[int(a.return_type) for a in aggs])
+    keys = (_abi.dfmi_agg_value * cap)()
+    out = (_abi.dfmi_agg_value * (cap * max(1, n)))()
+    ng = C.c_int64()
+    err = _abi.dfmi_error()
+    rc = L.oracle_aggregate_grouped(pn.array if pn else None, pn.length if pn else 0, kn.array, kn.length, names, arr,
+                                    lens, rts, n, C.byref(sch), C.byref(hb.cb), batch_rows, flags, cap, keys, out,
+                                    C.byref(ng), C.byref(err))
+    if rc != _abi.DFMI_OK:
+        raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+    g = ng.value
+    return list(keys[:g]), [list(out[i * n:(i + 1) * n]) for i in range(g)]

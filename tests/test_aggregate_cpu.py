@@ -241,3 +241,46 @@ def test_planner_builds_aggregate():
     assert [e.return_type for e in p.aggr_expr] == [DataType.Float64, DataType.UInt64, DataType.Int64]
     p = SqlToRel(ctx).sql_to_rel("SELECT MAX(a) FROM t GROUP BY b")
     assert [repr(e) for e in p.group_expr] == ["#1"]
+
+
+def _grouped_jit(schema, pred, key, aggs, flags=AGG, compile_=True):
+    L = _abi.lib()
+    fn = L.dfmi_internal_agg_grouped_jit_check
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(_abi.dfmi_batch), C.c_uint32,
+                   C.c_int32, C.c_char_p, C.c_int64, C.POINTER(_abi.dfmi_error)]
+    fn.restype = C.c_int64
+    hb = HostBatch(schema)
+    p = compile_scalar_expr(None, pred, schema, flags) if pred is not None else None
+    k = compile_scalar_expr(None, key, schema, flags)
+    cs = [compile_expr(None, a, schema, flags) for a in aggs]
+    arr = (C.c_void_p * len(cs))(*[c.handle.value for c in cs])
+    err = _abi.dfmi_error()
+    buf = C.create_string_buffer(1 << 20)
+    rc = fn(p.handle if p else None, k.handle, arr, len(cs), C.byref(hb.batch), flags, int(compile_), buf, len(buf),
+            C.byref(err))
+    return rc, err.code, err.message.decode(), buf.value.decode()
+
+
+def test_grouped_aggregate_kernels_compile():
+    """GROUP BY extension: the grouped kernel (slot per row, per-slot
+    reductions, [copies][slots][aggs + 1] accumulators) compiles for a Boolean
+    key (3 slots) and an integer key (17 slots), with exact float sums."""
+    s = Schema([Field("k", DataType.Boolean, True), Field("i", DataType.Int16, True),
+                Field("x", DataType.Float64, True), Field("f", DataType.Float32, False)])
+    pred = BinaryExpr(Column(2), Operator.Lt, Literal(Float64(0.7)))
+    aggs = [agg("SUM", Column(2), s), agg("MIN", Column(3), s), agg("COUNT", Column(1), s), agg("MAX", Column(1), s)]
+    for key, slots in ((Column(0), 3), (Column(1), 17)):
+        for p in (None, pred):
+            rc, code, msg, src = _grouped_jit(s, p, key, aggs)
+            assert rc > 0, msg
+            assert "GS = %d" % slots in src and "gsl[k]" in src and "fsum_add(S[g_]" in src
+
+
+def test_grouped_state_rejects_float_keys():
+    """GROUP BY over a float key is NotImplemented -- on the oracle too."""
+    from oracle_ffi import oracle_aggregate_grouped
+    s = Schema([Field("x", DataType.Float64, False)])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, np.zeros(3))])
+    with pytest.raises(ExecutionError) as ei:
+        oracle_aggregate_grouped(s, b, None, Column(0), [agg("COUNT", Column(0), s)])
+    assert ei.value.kind == "NotImplemented" and ei.value.message == "GROUP BY over Float64"

@@ -240,3 +240,115 @@ def test_csv_aggregate_all_types_fixture_on_gpu():
         dev = run_agg(s, batch, None, _agg_plan(sql, s, "t"))
         assert [d.bits for d in dev] == [agg_fixture_value(c, t) for c, t in zip(cells, types)], sql
         dev = run_agg(s, batch, None, _agg_plan(sql, s, "t"), batch_rows=64)  # many batches
+
+
+# ------------------------------------------------------- GROUP BY extension
+def run_grouped(schema, batch, pred, key, aggs, flags=AGG, batch_rows=0):
+    """Device groups and oracle groups (keys and values bit-identical), or
+    the same error."""
+    from oracle_ffi import oracle_aggregate_grouped
+    ref = ref_err = dev = dev_err = None
+    try:
+        ref = oracle_aggregate_grouped(schema, batch, pred, key, aggs, flags, batch_rows)
+    except ExecutionError as e:
+        ref_err = e
+    try:
+        p = compile_scalar_expr(None, pred, schema, flags) if pred is not None else None
+        k = compile_scalar_expr(None, key, schema, flags)
+        cs = [compile_expr(None, a, schema, flags) for a in aggs]
+        st = engine().grouped_agg_state(k, cs)
+        n = batch.num_rows()
+        step = batch_rows if batch_rows > 0 else max(n, 1)
+        dbatch = batch.to(engine().device)
+        for r0 in range(0, max(n, 1), step):
+            st.add(p, slice_batch(dbatch, r0, min(step, n - r0)) if n else dbatch, flags)
+        dev = st.finish()
+    except ExecutionError as e:
+        dev_err = e
+    if ref_err is not None or dev_err is not None:
+        assert ref_err is not None and dev_err is not None, (ref_err, dev_err)
+        assert (dev_err.kind, dev_err.message) == (ref_err.kind, ref_err.message)
+        return None
+    (dk, dv), (rk, rv) = dev, ref
+    assert [(k.type, k.is_null, k.bits) for k in dk] == [(k.type, k.is_null, k.bits) for k in rk]
+    for g in range(len(rk)):
+        for a, d, r in zip(aggs, dv[g], rv[g]):
+            assert (d.type, d.is_null, d.count) == (r.type, r.is_null, r.count), (g, repr(a))
+            if not r.is_null:
+                assert d.bits == r.bits, (g, repr(a), hex(d.bits), hex(r.bits))
+    return dev
+
+
+def test_group_by_c_bool_fixture_on_gpu():
+    """expected/csv_aggregate_by_c_bool.csv (MIN/MAX of every numeric column
+    per c_bool group) on the device through ctx.sql(), bit-identical to the
+    fixture cells and to the oracle; also pulled as 64-row batches."""
+    from golden_cases import agg_fixture_value, all_types_typed, load_batch
+    from test_oracle_golden import _agg_plan, by_c_bool_aggregates
+    s = all_types_typed()
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    for sql, cells, types in by_c_bool_aggregates():
+        (key,), aggs = _agg_plan(sql, s, "t", grouped=True)
+        for br in (0, 64):
+            keys, vals = run_grouped(s, batch, None, key, aggs, batch_rows=br)
+            assert [(k.is_null, k.bits) for k in keys] == [(0, 0), (0, 1)]
+            for g in range(2):
+                assert [v.bits for v in vals[g]] == [agg_fixture_value(c, t) for c, t in zip(cells[g], types)]
+        ctx = ExecutionContext(flags=AGG)
+        ctx.register_datasource("t", MemoryDataSource(s, [batch.to(engine().device)]))
+        out = ctx.sql(sql).next()
+        assert out.columns[0].cpu().to_pylist() == [False, True]
+        assert out.schema.fields[0].name == "c0" and len(out.columns) == 11
+
+
+def test_group_by_random_keys():
+    """Boolean / Int8 / UInt64 / Int64 keys with nulls over many batches whose
+    key windows differ (device flushes between windows), with a predicate,
+    exact float sums, MIN/MAX, COUNT and wrapping integer sums per group."""
+    rng = np.random.default_rng(12)
+    n = 200_003
+    s = Schema([Field("b", DataType.Boolean, True), Field("i8", DataType.Int8, True),
+                Field("u64", DataType.UInt64, False), Field("i64", DataType.Int64, True),
+                Field("x", DataType.Float64, True), Field("f", DataType.Float32, True), Field("v", DataType.Int32, True)])
+    i8 = (rng.integers(-3, 9, n) + (np.arange(n) // 50_000) * 7).astype(np.int8)  # windows move per 50k rows
+    cols = [Array.from_numpy(DataType.Boolean, rng.random(n) < 0.4, rng.random(n) >= 0.05),
+            Array.from_numpy(DataType.Int8, i8, rng.random(n) >= 0.02),
+            Array.from_numpy(DataType.UInt64, (np.uint64(2 ** 64 - 9) + rng.integers(0, 6, n).astype(np.uint64))),
+            Array.from_numpy(DataType.Int64, rng.integers(-8, 7, n).astype(np.int64), rng.random(n) >= 0.1),
+            Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.1),
+            Array.from_numpy(DataType.Float32, rng.standard_normal(n).astype(np.float32), rng.random(n) >= 0.1),
+            Array.from_numpy(DataType.Int32, rng.integers(-2 ** 31, 2 ** 31 - 1, n).astype(np.int32))]
+    b = RecordBatch(s, cols)
+    aggs = [agg("SUM", Column(4), s), agg("MIN", Column(5), s), agg("MAX", Column(5), s), agg("COUNT", Column(4), s),
+            agg("SUM", Column(6), s), agg("MAX", Column(3), s)]
+    pred = BinaryExpr(Column(4), Operator.Lt, Literal(Float64(0.8)))
+    for c in range(4):
+        for p in (None, pred):
+            for br in ((25_000,) if c == 1 else (0, 25_000)):  # Int8: 16-value windows per 50k rows
+                out = run_grouped(s, b, p, Column(c), aggs, batch_rows=br)
+                assert out is not None and len(out[0]) >= 2
+
+
+def test_group_by_errors():
+    """A batch whose selected keys span more than 16 consecutive values is
+    NotImplemented on the device (the oracle has no such limit: only the
+    device raises); an error in the key expression is raised by both, before
+    any aggregate's, in the reference's evaluation order."""
+    n = 4096
+    s = Schema([Field("k", DataType.Int64, False), Field("d", DataType.Int64, False), Field("x", DataType.Float64, False)])
+    k = np.arange(n, dtype=np.int64) % 40
+    d = np.ones(n, dtype=np.int64)
+    d[1000] = 0
+    b = RecordBatch(s, [Array.from_numpy(DataType.Int64, k), Array.from_numpy(DataType.Int64, d),
+                        Array.from_numpy(DataType.Float64, np.arange(n, dtype=np.float64))])
+    cs = [compile_expr(None, agg("SUM", Column(2), s), s, AGG)]
+    st = engine().grouped_agg_state(compile_scalar_expr(None, Column(0), s, AGG), cs)
+    with pytest.raises(ExecutionError) as e:
+        st.add(None, b.to(engine().device), AGG)
+    assert e.value.kind == "NotImplemented"
+    # key = k / d: DivideByZero at row 1000, before the aggregate's own error
+    key = BinaryExpr(Column(0), Operator.Divide, Column(1))
+    bad = [agg("SUM", BinaryExpr(Column(2), Operator.Divide, Literal(Float64(0.0))), s)]
+    pred = BinaryExpr(Column(0), Operator.Lt, Literal(Int64(10)))
+    run_grouped(s, b, pred, key, bad)
+    run_grouped(s, b, pred, Column(0), bad)

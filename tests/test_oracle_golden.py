@@ -313,11 +313,11 @@ def test_float32_uint32_files_are_the_whole_column(name):
     assert out[0][1].to_pylist() == want
 
 
-def _agg_plan(sql, schema, table):
+def _agg_plan(sql, schema, table, grouped=False):
     from datafusion_amd.execution.context import Aggregate
     p = SqlToRel(_Ctx({table: schema})).sql_to_rel(sql)
-    assert isinstance(p, Aggregate) and not p.group_expr
-    return p.aggr_expr
+    assert isinstance(p, Aggregate) and bool(p.group_expr) == grouped
+    return (p.group_expr, p.aggr_expr) if grouped else p.aggr_expr
 
 
 def test_sql_min_max_fixture():
@@ -361,3 +361,43 @@ def test_csv_aggregate_all_types_fixture():
         with pytest.raises(ExecutionError) as e:
             oracle_aggregate(s, batch, None, _agg_plan("SELECT MIN(c%d) FROM t" % c, s, "t"), AGG)
         assert e.value.kind == "NotImplemented"
+
+
+def by_c_bool_aggregates():
+    """csv_aggregate_by_c_bool.csv as (SQL, expected cells per group) pairs:
+    GROUP BY c0 (Boolean), MIN/MAX of columns 1-10 in two plans; the file's
+    Utf8 MIN/MAX (last two cells) are outside the extension."""
+    rows = expected_rows("csv_aggregate_by_c_bool.csv")
+    assert [r[0] for r in rows] == ["false", "true"] and all(len(r) == 23 for r in rows)
+    plans = []
+    for lo, hi in ((1, 6), (6, 11)):
+        sel = ", ".join("MIN(c%d), MAX(c%d)" % (c, c) for c in range(lo, hi))
+        cells = [r[1 + 2 * (lo - 1): 1 + 2 * (hi - 1)] for r in rows]
+        plans.append(("SELECT c0, %s FROM t GROUP BY c0" % sel, cells,
+                      [ALL_TYPES[c] for c in range(lo, hi) for _ in (0, 1)]))
+    return plans
+
+
+def test_csv_aggregate_by_c_bool_fixture():
+    """expected/csv_aggregate_by_c_bool.csv: MIN/MAX of every numeric column
+    per c_bool group (false, then true), through the planner's
+    Aggregate{group_expr} (sqlplanner.rs:91-117)."""
+    from datafusion_amd._abi import DFMI_FLAG_EXT_AGGREGATE as AGG
+    from oracle_ffi import oracle_aggregate_grouped
+    s = all_types_typed()
+    batch = load_batch(s, "all_types_flat.csv", has_header=False)
+    for sql, cells, types in by_c_bool_aggregates():
+        (key,), aggs = _agg_plan(sql, s, "t", grouped=True)
+        keys, vals = oracle_aggregate_grouped(s, batch, None, key, aggs, AGG)
+        assert [(k.is_null, k.bits) for k in keys] == [(0, 0), (0, 1)]
+        for g in range(2):
+            assert [v.bits for v in vals[g]] == [agg_fixture_value(c, t) for c, t in zip(cells[g], types)], (sql, g)
+    # batch-size independence and a predicate (count per group)
+    sql = "SELECT c0, COUNT(c1), SUM(c8), MIN(c9), MAX(c10) FROM t GROUP BY c0"
+    (key,), aggs = _agg_plan(sql, s, "t", grouped=True)
+    one = oracle_aggregate_grouped(s, batch, None, key, aggs, AGG)
+    for br in (8, 64, 1000):
+        again = oracle_aggregate_grouped(s, batch, None, key, aggs, AGG, batch_rows=br)
+        assert [(k.is_null, k.bits) for k in again[0]] == [(k.is_null, k.bits) for k in one[0]]
+        assert [[(v.is_null, v.bits) for v in g] for g in again[1]] == [[(v.is_null, v.bits) for v in g] for g in one[1]]
+    assert sum(v[0].bits for v in one[1]) == batch.num_rows()
