@@ -244,6 +244,8 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
     if (!X.utf8_outs.empty() && !X.pred_slots.empty()) X.arena = 256;
     if (diag)
         if (const char* e = getenv("DFMI_UTF8_ARENA")) X.arena = std::max(128, std::min(1024, atoi(e)));
+    if (diag)
+        if (const char* e = getenv("DFMI_UTF8_IMAGE")) X.image = std::max(32, std::min(129, atoi(e)));
     if (X.M == 1 || X.KO == 0) X.KO = X.K;
     if (X.KO < 1 || X.KO > X.K || X.K % X.KO) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.M * X.BLOCK / 64 > 256)

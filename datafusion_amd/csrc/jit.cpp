@@ -789,7 +789,7 @@ std::string generate(const Plan& P, Launch& X) {
         // tile a block waits on in the look-back is running or done)
         if (!X.utf8_outs.empty() && X.gather && X.gather != 3)
             o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA, "
-              << (X.gather == 1 ? "32" : X.gather == 5 ? "72" : "dfmi::kStageChunks + 1") << "> G[WAVES];\n";
+              << (X.gather == 1 ? 32 : X.gather == 5 ? 72 : X.gather == 2 ? 129 : X.image) << "> G[WAVES];\n";
         o << "  const unsigned t = tile_;\n";
         if (X.M == 1) {
             // One tile: predicate, projection-only loads, scan + look-back,
@@ -965,7 +965,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -76,6 +76,7 @@ struct Launch {
                      // 4 = as 1, but each slice assembled in an LDS image (round 2's form);
                      // 5 = as 1, output words' strings found by a marker max-scan
     int arena = 128; // Utf8 gather staging arena per wave, 16-byte chunks
+    int image = 129;   // gather 4: LDS image per wave, 16-byte chunks (a longer slice output copies per lane)
     int prestage = 0;
     int gather_phases = 0;  // diagnostics: per-phase cycle counters in utf8_gather (DFMI_DEBUG_MODE bit 5)  // gather 1 / 4: the first staging round is issued before the look-back
     // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores

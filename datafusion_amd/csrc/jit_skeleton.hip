@@ -736,10 +736,11 @@ constexpr int kStageChunks = 128;  // 16-byte source chunks of one slice's span:
 template <int ARENA = kStageChunks, int DST = kStageChunks + 1>
 struct Utf8Stage {
     static_assert(ARENA >= kStageChunks, "the arena holds at least one slice's span");
-    static_assert(DST >= 32, "room for utf8_emit_slice's lane table");
+    static_assert(DST >= 32, "room for utf8_emit_slice's lane table / a 512-byte image");
     uint4 src[ARENA];  // source spans of consecutive slices, whole aligned 16-byte chunks
     // one slice's output bytes at their output address modulo 4 (LDS-image
-    // variants: kStageChunks + 1 chunks), or utf8_emit_slice's lane table (32)
+    // variants; a slice whose output is longer copies per lane), or
+    // utf8_emit_slice's lane table (32 chunks)
     uint4 dst[DST];
 };
 
@@ -1185,18 +1186,19 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             continue;
         }
         if (Ls == 0) continue;
-        if (nch > kStageChunks) {
+        const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
+        // a span over the stage, or (LDS image) an output over the image: each lane copies its string
+        if (nch > kStageChunks || (emit == 1 && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST)) {
             if (sel && L) utf8_copy(src + s[k], out + ob0 + rel, L);
             continue;
         }
-        const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
         u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word holding the slice's first byte
         if (emit == 2) {
             utf8_emit_slice_mk(gs + 4 * my_off, (int*)gd, (u8*)(gd + 128), w0, sh, sh + (int)Ls, incl, rel, L,
                                (int)(s[k] - c0), lane);
             continue;
         }
-        if (emit == 0 || DST <= kStageChunks) {  // (an LDS image needs the full dst)
+        if (emit == 0 || DST < 32) {
             utf8_emit_slice(gs + 4 * my_off, (int*)gd, w0, sh, sh + (int)Ls, incl, rel, (int)(s[k] - c0), lane);
             continue;
         }
