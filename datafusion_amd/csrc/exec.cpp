@@ -216,6 +216,14 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         // binary-search emitter's smaller LDS footprint only pays where few
         // rows are selected)
         X.gather = 4;
+        if (!X.utf8_outs.empty() && pred) {
+            // latency-bound gather: a 2 KiB staging arena per wave and a soft
+            // 8-waves/SIMD hint (4 blocks/CU: LDS 34 KiB, 64 VGPRs) -- C3 gather
+            // 1.45 -> 1.36 ms per 1.25e8-row batch
+            X.arena = 128;
+            X.waves_per_eu = 8;
+            X.waves_soft = true;
+        }
     }
     // diagnostic knobs (tools/*): read only when DFMI_DIAG is set -- a dozen
     // getenv scans per call would cost the 1024-row batch path microseconds
@@ -238,14 +246,16 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         if (const char* e = getenv("DFMI_OUT_SLICES")) X.KO = atoi(e);
         if (const char* e = getenv("DFMI_SUBTILE_PREFETCH")) X.prefetch = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_SUBTILE_SPARSE")) X.sparse = atoi(e) & 1;
     }
-    // a numeric predicate's tiles are VGPR-limited (3 blocks/CU): LDS has room
-    // for a 4 KiB staging arena per wave, which stages ~4 slices per round trip
-    if (!X.utf8_outs.empty() && !X.pred_slots.empty()) X.arena = 256;
+
     if (diag)
         if (const char* e = getenv("DFMI_UTF8_ARENA")) X.arena = std::max(128, std::min(1024, atoi(e)));
     if (diag)
         if (const char* e = getenv("DFMI_UTF8_IMAGE")) X.image = std::max(32, std::min(129, atoi(e)));
+    if (diag)
+        if (const char* e = getenv("DFMI_UTF8_DBUF")) X.dbuf = atoi(e) & 1;
+    if (X.dbuf && X.arena < 2 * 128) X.dbuf = 0;  // each half holds one slice's span
     if (X.M == 1 || X.KO == 0) X.KO = X.K;
     if (X.KO < 1 || X.KO > X.K || X.K % X.KO) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.M * X.BLOCK / 64 > 256)

@@ -713,19 +713,9 @@ std::string generate(const Plan& P, Launch& X) {
         // Compacted stores of the selected rows at `base` (selm, wm, the
         // Utf8 offsets and the column registers in scope; the tile's offsets
         // resolved in T); `kb`: the rows' first word of the tile.
-        auto emit_outputs = [&](const std::string& kb, bool prestaged) {
-            // byte-light predicates: projection-only columns after the look-back
-            // (fewer registers held across it; few rows are selected)
-            if (X.late_proj || X.M > 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
-            o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
-              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][(" << kb
-              << " + k) * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
-            // projections over the selected rows (filtered batch: no validity)
-            g.filtered_cols = true;
-            for (size_t oi = 0; oi < P.outs.size(); ++oi)
-                if (P.outs[oi].nullable) o << "  unsigned nn" << oi << " = 0;\n";
-            o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
-              << "    const i64 row = base + k * BLOCK + tid;\n    const unsigned d = dst[k];\n";
+        // The numeric / Boolean outputs of one selected row (`k`, `row` and its
+        // output index `d` in scope; the column registers c<slot>[k]).
+        auto emit_out_values = [&]() {
             for (size_t oi = 0; oi < P.outs.size(); ++oi) {
                 const OutSpec& os = P.outs[oi];
                 if (os.kind == OutSpec::SKIP || os.kind == OutSpec::UTF8) continue;
@@ -751,6 +741,21 @@ std::string generate(const Plan& P, Launch& X) {
                 else
                     o << "    ((" << ct << "*)A.out[" << oi << "] + obase)[d] = " << v.v << ";\n";
             }
+        };
+        auto emit_outputs = [&](const std::string& kb, bool prestaged) {
+            // byte-light predicates: projection-only columns after the look-back
+            // (fewer registers held across it; few rows are selected)
+            if (X.late_proj || X.M > 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
+              << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][(" << kb
+              << " + k) * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
+            // projections over the selected rows (filtered batch: no validity)
+            g.filtered_cols = true;
+            for (size_t oi = 0; oi < P.outs.size(); ++oi)
+                if (P.outs[oi].nullable) o << "  unsigned nn" << oi << " = 0;\n";
+            o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n    if (!((selm >> k) & 1)) continue;\n"
+              << "    const i64 row = base + k * BLOCK + tid;\n    const unsigned d = dst[k];\n";
+            emit_out_values();
             o << "  }\n";
             for (size_t oi = 0; oi < P.outs.size(); ++oi)
                 if (P.outs[oi].nullable)
@@ -772,7 +777,8 @@ std::string generate(const Plan& P, Launch& X) {
                       << "G[wave], lane, wave, " << kb
                       << (X.gather == 2 ? "" : X.gather == 4 ? ", 1" : X.gather == 5 ? ", 2" : ", 0")
                       << (X.gather == 2 ? "" : (prestaged && j == 0 ? ", pre_" : ", -1"))
-                      << (X.gather == 2 ? "" : X.gather_phases ? ", true" : ", false") << ");\n";
+                      << (X.gather == 2 ? "" : X.gather_phases ? ", true" : ", false")
+                      << (X.gather == 2 ? "" : X.dbuf ? ", true" : ", false") << ");\n";
             }
             if (!X.utf8_outs.empty()) o << "  }\n";
         };
@@ -804,7 +810,8 @@ std::string generate(const Plan& P, Launch& X) {
             // look-back, whose wait then hides it
             const bool pre = !X.utf8_outs.empty() && (X.gather == 1 || X.gather >= 4) && X.prestage;
             if (pre)
-                o << "  const int pre_ = dfmi::utf8_gather_prestage<K, ARENA>(A, " << X.utf8_outs[0].second
+                o << "  const int pre_ = dfmi::utf8_gather_prestage<K, " << (X.dbuf ? "ARENA / 2" : "ARENA") << ">(A, "
+                  << X.utf8_outs[0].second
                   << ", wm, us" << offs_name(X.utf8_outs[0].second) << ", ux" << offs_name(X.utf8_outs[0].second)
                   << ", G[wave], lane);\n";
             o << "  dfmi::tile_offsets<BLOCK, K, NCH, " << tparams << ">(A, T, t, cnt, lane, wave);\n";
@@ -854,6 +861,70 @@ std::string generate(const Plan& P, Launch& X) {
             o << "  dfmi::tile_scan_lds<BLOCK, K * M, NCH, " << sp << ">(A, T, t, lane, wave);\n"
               << "  dfmi::tile_resolve<BLOCK, K * M, NCH, " << tparams << ">(A, T, t, lane, wave);\n"
               << "  dfmi::lds_sync();\n";
+            // sparse output pass: when the wave's sub-tiles hold at most 64
+            // selected rows (an equality on a Utf8 column), one lane per
+            // selected row loads what it needs and stores its outputs -- one
+            // round of loads for the whole wave instead of one per slice
+            // (not with the two-pass gather: its second kernel reads the source
+            // starts only the dense pass's utf8_offsets_src writes)
+            bool sparse = X.sparse && X.gather != 3;
+            for (int sl : X.proj_slots) sparse = sparse && X.col_type(X.num_cols[sl]) != DFMI_TYPE_BOOLEAN;
+            if (sparse) {
+                o << "  __shared__ unsigned short SLR[WAVES][64];\n  unsigned tot_ = 0;\n"
+                  << "  for (int q_ = 0; q_ < M * K; ++q_) {\n"
+                  << "    const u64 w_ = dfmi::lds_uniform_u64(&WS[q_ * WAVES + wave]);\n    if (!w_) continue;\n"
+                  << "    if (tot_ + (unsigned)__builtin_popcountll(w_) <= 64u && ((w_ >> lane) & 1))\n"
+                  << "      SLR[wave][tot_ + dfmi::lane_rank(w_)] = (unsigned short)(q_ * 64 + lane);\n"
+                  << "    tot_ += (unsigned)__builtin_popcountll(w_);\n  }\n"
+                  << "  if (tot_ <= 64u) {\n  dfmi::wave_lds_fence();\n"
+                  << "  const bool have_ = (unsigned)lane < tot_;\n"
+                  << "  const unsigned e_ = have_ ? (unsigned)SLR[wave][lane] : 0u;\n"
+                  << "  const int qs_ = (int)(e_ >> 6), ls_ = (int)(e_ & 63u);\n"
+                  << "  const i64 row = ((i64)t * M + qs_ / K) * (BLOCK * K) + (i64)(qs_ % K) * BLOCK + 64 * wave + ls_;\n"
+                  << "  const u64 wq_ = have_ ? WS[qs_ * WAVES + wave] : 0ull;\n"
+                  << "  const unsigned d = have_ ? (unsigned)T.excl[0][qs_ * WAVES + wave] + "
+                     "(unsigned)__builtin_popcountll(wq_ & ((1ull << ls_) - 1ull)) : 0u;\n"
+                  << "  const i64 obase = (i64)T.prefix[0];\n  const int k = 0;\n";
+                for (int sl : X.proj_slots) {
+                    const std::string ct = ctype(X.col_type(X.num_cols[sl]));
+                    o << "  " << ct << " c" << sl << "[1];\n  c" << sl << "[0] = have_ ? ((const " << ct << "*)A.col[" << sl
+                      << "])[row] : (" << ct << ")0;\n";
+                }
+                for (size_t j = 0; j < X.utf8_outs.size(); ++j)
+                    o << "  const int su" << j << "_ = have_ ? A.offs[" << X.utf8_outs[j].second << "][row] : 0, eu" << j
+                      << "_ = have_ ? A.offs[" << X.utf8_outs[j].second << "][row + 1] : 0;\n";
+                g.filtered_cols = true;
+                for (size_t oi = 0; oi < P.outs.size(); ++oi)
+                    if (P.outs[oi].nullable) o << "  unsigned nn" << oi << " = 0;\n";
+                o << "  if (have_) {\n";
+                emit_out_values();
+                o << "  }\n";
+                for (size_t oi = 0; oi < P.outs.size(); ++oi)
+                    if (P.outs[oi].nullable)
+                        o << "  { const u64 s_ = dfmi::wave_sum((u64)nn" << oi
+                          << "); if (lane == 0 && s_) atomicAdd(&A.totals[8 + " << oi << "], s_); }\n";
+                if (!X.utf8_outs.empty()) {
+                    // each selected row's bytes: its slice's byte offset plus the
+                    // lengths of the selected rows before it in the slice
+                    o << "  const int qp_ = __builtin_amdgcn_ds_bpermute(((lane + 63) & 63) << 2, qs_);\n"
+                      << "  const u64 first_ = __ballot(have_ && (lane == 0 || qp_ != qs_));\n"
+                      << "  const int fl_ = 63 - __builtin_clzll(first_ & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));\n";
+                    for (size_t j = 0; j < X.utf8_outs.size(); ++j) {
+                        const int oo = X.utf8_outs[j].first, u = X.utf8_outs[j].second;
+                        o << "  { const unsigned L_ = have_ ? (unsigned)(eu" << j << "_ - su" << j << "_) : 0u;\n"
+                          << "    const unsigned x_ = dfmi::wave_incl_scan32(L_, lane) - L_;\n"
+                          << "    const unsigned xf_ = (unsigned)__builtin_amdgcn_ds_bpermute(fl_ << 2, (int)x_);\n"
+                          << "    const u64 ob_ = T.prefix[" << (j + 1) << "] + (have_ ? T.excl[" << (j + 1)
+                          << "][qs_ * WAVES + wave] : 0ull) + (x_ - xf_);\n"
+                          << "    if (have_) {\n      A.out_offs[" << oo << "][obase + d] = (int)ob_;\n"
+                          << "      if ((i64)(ob_ + L_) > A.out_cap[" << oo
+                          << "]) dfmi::report_err(A.err, 0, 0, dfmi::ERRK_CAPACITY);\n"
+                          << "      else if (L_ && !(A.mode & 8)) dfmi::utf8_copy(A.bytes[" << u << "] + su" << j << "_, A.out_data["
+                          << oo << "] + ob_, L_);\n    }\n  }\n";
+                    }
+                }
+                o << "  } else {\n";
+            }
             // output pass in steps of KO slices (fewer registers than K)
             o << "  {\n  constexpr int KS = K, K = " << X.KO << ";  // slices per sub-tile / per output step\n"
               << "  for (int q_ = 0; q_ < M * KS; q_ += K) {\n"
@@ -868,6 +939,7 @@ std::string generate(const Plan& P, Launch& X) {
             emit_decls(o, X.proj_slots, X, "", false);
             emit_outputs("q_", false);
             o << "  }\n  }\n";
+            if (sparse) o << "  }\n";
             emit_last_offsets();
         }
     } else {
@@ -965,7 +1037,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);
@@ -1004,10 +1076,22 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
             return h.fn;
         }
     }
-    const std::string src = generate(P, X);
+    std::string src = generate(P, X);
     if (getenv("DFMI_JIT_PRINT")) fprintf(stderr, "%s\n", src.c_str() + strlen(dfmi_skeleton_src));
     ShapeHit h;
     h.fn = compile(device, src, X.kname, compile_ms);
+    if (X.waves_soft && X.waves_per_eu > 0) {
+        // a soft occupancy hint: if the register allocator had to spill to
+        // meet it, the query shape is compiled again without it
+        int scratch = 0;
+        if (hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, h.fn) == hipSuccess && scratch > 0) {
+            double ms2 = 0;
+            X.waves_per_eu = 0;
+            src = generate(P, X);
+            h.fn = compile(device, src, X.kname, &ms2);
+            if (compile_ms) *compile_ms += ms2;
+        }
+    }
     h.kname = X.kname;
     memcpy(h.lits, X.args_lits, sizeof h.lits);
     h.n_lits = X.n_lits;

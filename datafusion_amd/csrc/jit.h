@@ -53,7 +53,8 @@ struct Plan {
 // Slot tables + literal pools of one launch.
 struct Launch {
     int K = 8, BLOCK = 512;
-    int waves_per_eu = 0;  // >0: occupancy hint to the register allocator (diagnostics)
+    int waves_per_eu = 0;  // >0: occupancy hint to the register allocator
+    bool waves_soft = false;  // ... dropped (recompiled without) when meeting it spills
     // look-back: R windows of 64 status words per round trip, s_sleep(sleep)
     // between polls, one status word per `spread` words (16 = one per 128-byte
     // line: polling blocks then do not contend on shared lines)
@@ -67,7 +68,8 @@ struct Launch {
     // selection ballots (LDS), then one scan + look-back for all of them and
     // an output pass that reloads what the selected rows need
     int M = 1;
-    int prefetch = 1;  // ... and load sub-tile m+1's Utf8 offsets while sub-tile m's heads are in flight
+    int prefetch = 0;  // ... and load sub-tile m+1's Utf8 offsets while sub-tile m's heads are in flight
+    int sparse = 1;    // ... with a one-lane-per-row output pass when a wave holds <= 64 selected rows
     int KO = 0;  // ... whose output pass handles KO slices per wave at a time (divides K; 0 = K)
     int gather = 1;  // Utf8 gather: 1 = wave-cooperative, consecutive slices staged together,
                      //     lanes on output words found by binary search (utf8_emit_slice);
@@ -76,6 +78,7 @@ struct Launch {
                      // 4 = as 1, but each slice assembled in an LDS image (round 2's form);
                      // 5 = as 1, output words' strings found by a marker max-scan
     int arena = 128; // Utf8 gather staging arena per wave, 16-byte chunks
+    int dbuf = 0;      // gather 1 / 4 / 5: the arena's halves double-buffer the staging (ARENA >= 256)
     int image = 129;   // gather 4: LDS image per wave, 16-byte chunks (a longer slice output copies per lane)
     int prestage = 0;
     int gather_phases = 0;  // diagnostics: per-phase cycle counters in utf8_gather (DFMI_DEBUG_MODE bit 5)  // gather 1 / 4: the first staging round is issued before the look-back

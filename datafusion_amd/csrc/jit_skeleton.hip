@@ -869,30 +869,6 @@ __device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLO
 __device__ __forceinline__ void utf8_place(const unsigned* sg, unsigned* gd, int a, int d, int L) {
     const int delta = a - d;  // source byte = output byte + delta
     const int wf = d >> 2, wl = (d + L - 1) >> 2;
-    if (wl - wf < 8) {
-        // up to 8 output words (strings up to 25..32 bytes): every source
-        // word read at once (one LDS round trip), output word i of the string
-        // is v_alignbyte(x[i + 1], x[i]) with one shift for the whole string
-        const int nwo = wl - wf + 1;
-        const int sw0 = (4 * wf + delta) >> 2;  // arithmetic shift: -1 at most
-        const unsigned sh = (unsigned)delta & 3u;
-        unsigned x[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) x[i] = i <= nwo ? sg[sw0 + i < 0 ? 0 : sw0 + i] : 0u;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i >= nwo) break;
-            const unsigned val = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
-            if (i == 0 || i == nwo - 1) {  // edge words: shared with the neighbouring strings
-                const int p = 4 * (wf + i) - d;
-                const unsigned msk = byte_mask(p < 0 ? -p : 0, p + 4 > L ? L - p : 4);
-                __hip_atomic_fetch_or(gd + wf + i, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            } else {
-                gd[wf + i] = val;
-            }
-        }
-        return;
-    }
     auto edge = [&](int w) {
         const int p = 4 * w - d;  // position of the word's first byte in the string (>= -3)
         const int sb = a + p;     // ... in the span (>= -3)
@@ -1097,9 +1073,10 @@ __device__ __forceinline__ int utf8_stage_group(const u8* src, const u64 (&wm)[K
 // The first staging round of utf8_gather, issued before the tile's look-back
 // so that the look-back's wait hides the staging loads; returns the `pre`
 // argument of utf8_gather (-1: nothing staged).
-template <int K, int ARENA, int DST>
+template <int K, int CAP, int ARENA, int DST>
 __device__ __forceinline__ int utf8_gather_prestage(const Args& A, int u, const u64 (&wm)[K], const int (&s)[K],
                                                     const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane) {
+    static_assert(CAP <= ARENA, "staging capacity within the arena");
     const u8* src = A.bytes[u];
     i64 cs[K];
     int cn[K];
@@ -1108,7 +1085,7 @@ __device__ __forceinline__ int utf8_gather_prestage(const Args& A, int u, const 
 #pragma unroll
     for (int k = K - 1; k >= 0; --k)
         if (wm[k]) k0 = k;
-    return k0 < 0 ? -1 : utf8_stage_group<K, ARENA>(src, wm, cs, cn, k0, G.src, lane);
+    return k0 < 0 ? -1 : utf8_stage_group<K, CAP>(src, wm, cs, cn, k0, G.src, lane);
 }
 
 // Copy the selected rows of Utf8 input u into output o (rebased i32
@@ -1125,7 +1102,8 @@ template <int BLOCK, int K, int NCH, int ARENA, int KT = K, int DST = kStageChun
 __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
                                             unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
                                             const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane,
-                                            int wave, int kb = 0, int emit = 0, int pre = -1, bool prof = false) {
+                                            int wave, int kb = 0, int emit = 0, int pre = -1, bool prof = false,
+                                            bool dbuf = false) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -1143,7 +1121,6 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     // slice setup, image zeroing, placing, stores. Reading the counter
     // serialises the wave (~10x slower kernel): relative figures only.
     const bool tp_on = prof && (A.mode & 32) != 0;
-    bool zeroed = false;  // LDS image (emit == 1) zeroed for this tile
     u64 tacc[5] = {0, 0, 0, 0, 0};
     u64 tcur = tp_on ? __builtin_readcyclecounter() : 0;
     auto tick = [&](int ph) {
@@ -1153,9 +1130,23 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             tcur = n;
         }
     };
+    // dbuf: the arena's two halves alternate -- while one group of slices is
+    // placed and stored, the next group's spans are already being staged
+    // into the other half; its wait counts only the loads, not the stores
+    // issued after them (vmcnt counts both, in issue order: at least 2
+    // store instructions per slice placed through the image follow them)
+    constexpr int HALF = ARENA / 2;
+    int cur = 1;          // dbuf: the half holding slices (.., staged_to]
+    int next_to = -1;     // dbuf: slices (staged_to, next_to] are being staged into the other half
+    unsigned since = 0;   // dbuf: store instructions issued after those loads (a lower bound)
     if (pre >= 0) {
-        wait_vm_loads();
-        wave_lds_fence();
+        if (dbuf) {
+            next_to = pre;  // prestaged into half 0 (cur ^ 1)
+            staged_to = -1;
+        } else {
+            wait_vm_loads();
+            wave_lds_fence();
+        }
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1163,10 +1154,32 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         if (!m) continue;
         tick(1);
         if (k > staged_to) {
-            staged_to = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k, G.src, lane);
-            wait_vm_loads();
+            if (!dbuf) {
+                staged_to = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k, G.src, lane);
+                wait_vm_loads();
+                aoff = 0;
+            } else {
+                cur ^= 1;
+                if (next_to >= k) {
+                    staged_to = next_to;
+                    if (since >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    else if (since >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else if (since >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    else if (since >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                    else wait_vm_loads();
+                } else {
+                    staged_to = utf8_stage_group<K, HALF>(src, wm, cs, cn, k, G.src + cur * HALF, lane);
+                    wait_vm_loads();
+                }
+                aoff = cur * HALF;
+                next_to = -1;
+                since = 0;
+                if (staged_to + 1 < K) {
+                    const int nt = utf8_stage_group<K, HALF>(src, wm, cs, cn, staged_to + 1, G.src + (cur ^ 1) * HALF, lane);
+                    if (nt > staged_to) next_to = nt;
+                }
+            }
             wave_lds_fence();
-            aoff = 0;
         }
         tick(0);
         const bool sel = (selm >> k) & 1;
@@ -1204,37 +1217,26 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         }
         const int nw = (sh + (int)Ls + 3) >> 2;
         tick(1);
-        if (!zeroed) {  // the image is zero from here on: the store pass clears what it reads
-            for (int c = lane; c < DST; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
-            wave_lds_fence();
-            zeroed = true;
-        }
+        for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_fence();
         tick(2);
         if (L) utf8_place(gs + 4 * my_off, gd, (int)(s[k] - c0), sh + (int)rel, (int)L);
         wave_lds_fence();
         tick(3);
-        for (int j0 = 0; j0 < nw; j0 += 128) {
-            const int ja = j0 + lane, jb = ja + 64;
-            const unsigned va = ja < nw ? gd[ja] : 0u, vb = jb < nw ? gd[jb] : 0u;
-            if (ja < nw) gd[ja] = 0u;
-            if (jb < nw) gd[jb] = 0u;
+        for (int j = lane; j < nw; j += 64) {
+            const unsigned val = gd[j];
+            const int p = 4 * j - sh;  // output position of the word's first byte
+            if (p >= 0 && p + 4 <= (int)Ls) {
+                *at<unsigned>(w0, 4 * j) = val;
+            } else {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int j = h ? jb : ja;
-                const unsigned val = h ? vb : va;
-                if (j >= nw) continue;
-                const int p = 4 * j - sh;  // output position of the word's first byte
-                if (p >= 0 && p + 4 <= (int)Ls) {
-                    *at<unsigned>(w0, 4 * j) = val;
-                } else {
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        if (p + b >= 0 && p + b < (int)Ls) w0[4 * j + b] = (u8)(val >> (8 * b));
-                }
+                for (int b = 0; b < 4; ++b)
+                    if (p + b >= 0 && p + b < (int)Ls) w0[4 * j + b] = (u8)(val >> (8 * b));
             }
         }
         wave_lds_fence();
         tick(4);
+        since += 2;  // this slice's out_offs store and at least one image store
     }
     if (tp_on && lane == 0)
 #pragma unroll

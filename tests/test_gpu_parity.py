@@ -375,16 +375,20 @@ def test_utf8_multi_channel_many_tiles():
         run_both(s, b, BinaryExpr(Column(c), Operator.NotEq, Literal(Utf8(w))), [Column(c)], DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
-@pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p"])
+@pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp"])
 def test_utf8_gather_variants(monkeypatch, variant):
     """The Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG: 3 = two
     passes -- offsets + source starts in the query kernel, bytes by
     k_utf8_copy_rows --, 2 = one staged slice per round trip, 0 = per-lane
     copy, 4 = slices assembled in an LDS image, 1 = output words' strings by
     binary search, 5 = by marker scan; p: first staging round before the
-    look-back) against the oracle on the Utf8 parity cases above."""
+    look-back; d: double-buffered staging) against the oracle on the Utf8
+    parity cases above."""
     if variant.endswith("p"):
         monkeypatch.setenv("DFMI_UTF8_PRESTAGE", "1")
+        variant = variant[:-1]
+    if variant.endswith("d"):  # the arena's halves double-buffer the staging
+        monkeypatch.setenv("DFMI_UTF8_DBUF", "1")
         variant = variant[:-1]
     monkeypatch.setenv("DFMI_DIAG", "1")
     monkeypatch.setenv("DFMI_UTF8_GATHER", variant)
@@ -394,13 +398,17 @@ def test_utf8_gather_variants(monkeypatch, variant):
         test_utf8_multi_channel_many_tiles()
 
 
-@pytest.mark.parametrize("m", ["1", "3"])
+@pytest.mark.parametrize("m", ["1", "3", "8s0", "8pf"])
 def test_utf8_subtile_counts(monkeypatch, m):
     """Utf8-only predicates run M sub-tiles per look-back (8 by default);
     M = 1 (one look-back per 2048-row tile, round 2's form) and an odd M
     (a last tile whose trailing sub-tiles hold no rows) against the oracle."""
     monkeypatch.setenv("DFMI_DIAG", "1")
-    monkeypatch.setenv("DFMI_SUBTILES", m)
+    if m.endswith("s0"):  # without the sparse (one lane per selected row) output pass
+        monkeypatch.setenv("DFMI_SUBTILE_SPARSE", "0")
+    if m.endswith("pf"):  # with the sub-tile offsets prefetch
+        monkeypatch.setenv("DFMI_SUBTILE_PREFETCH", "1")
+    monkeypatch.setenv("DFMI_SUBTILES", m.rstrip("s0pf") or "8")
     test_utf8_gather_and_equality()
     test_utf8_many_tiles()
     test_utf8_multi_channel_many_tiles()
