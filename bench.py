@@ -207,12 +207,22 @@ def abi_comm(eng, dist, rank, world, dev):
     every rank out of band -- here a torch.distributed broadcast -- then
     dfmi_shard_comm_init), as a Rust caller with one thread per GPU sets it up."""
     from datafusion_amd.execution.engine import ShardComm
-    uid = ShardComm.unique_id() if rank == 0 else bytes(_abi.DFMI_SHARD_ID_BYTES)
-    if dist:
-        t = torch.tensor(list(uid), dtype=torch.uint8, device=coll_device(dev))
-        dist.broadcast(t, 0)
-        uid = bytes(t.cpu().tolist())
-    return ShardComm(eng, world, rank, uid)
+    # RCCL prints its version banner on stdout at init: keep stdout for the
+    # one JSON line (fd-level, the banner comes from C)
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        uid = ShardComm.unique_id() if rank == 0 else bytes(_abi.DFMI_SHARD_ID_BYTES)
+        if dist:
+            t = torch.tensor(list(uid), dtype=torch.uint8, device=coll_device(dev))
+            dist.broadcast(t, 0)
+            uid = bytes(t.cpu().tolist())
+        return ShardComm(eng, world, rank, uid)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def _checksum(t):
