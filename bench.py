@@ -352,6 +352,7 @@ def batches_line(eng, schema, cols, sel, dev):
             torch.cuda.empty_cache()
     out["1024_rows_x256_coalesced"] = coalesced_batches(eng, schema, cols, sel, dev, 1024, 256)
     out["1024_rows_host"] = host_small_batches(eng, schema, sel, 1024)
+    out["1024_rows_host_x256_coalesced"] = host_coalesced_batches(eng, schema, sel, 1024, 256)
     # a new query shape: generate + hipRTC compile on the first call, cached after
     pred, projs = query(sel)
     pred = BinaryExpr(pred, Operator.And, BinaryExpr(Column(2), Operator.GtEq, Literal(Float64(0.0))))
@@ -464,6 +465,69 @@ def host_small_batches(eng, schema, sel, m, calls=2000):
     L.dfmi_context_set_timing(eng.ctx, 1)
     return {"us_per_batch": round(el * 1e6, 2), "rows_per_s": m / el, "calls": calls,
             "note": "host buffers in, host results out (PCIe both ways), one synchronous call per batch"}
+
+
+def host_coalesced_batches(eng, schema, sel, m, nb, calls=200):
+    """dfmi_filter_project_host_batches: nb consecutive m-row HOST batches
+    (pageable numpy buffers, as csv::Reader hands them out) per call -- packed
+    into pinned memory, one H2D, one launch, one D2H; one output batch per
+    input batch. Checked against one dfmi_filter_project_host call per batch."""
+    from oracle_ffi import gen_unit_f64
+    host = [gen_unit_f64(SEED, j, 0, m * nb) for j in range(3)]
+    pred_e, proj_e = query(sel)
+    pred = compile_scalar_expr(None, pred_e, schema)
+    projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+    progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
+    keep = []
+    barr = (_abi.dfmi_batch * nb)()
+    for b in range(nb):
+        carr = (_abi.dfmi_column * 3)()
+        for j, h in enumerate(host):
+            carr[j].type = int(DataType.Float64)
+            carr[j].length = m
+            carr[j].values = h.ctypes.data + b * m * 8
+        keep.append(carr)
+        barr[b] = _abi.dfmi_batch(3, 0, m, carr)
+    L = _abi.lib()
+    err = _abi.dfmi_error()
+    failed = C.c_int32()
+
+    def call(check=False):
+        res = C.c_void_p()
+        rc = L.dfmi_filter_project_host_batches(eng.ctx, pred.handle, progs, 3, barr, nb, 0, C.byref(res),
+                                                C.byref(failed), C.byref(err))
+        if rc != 0:
+            raise RuntimeError(err.message.decode())
+        ok = True
+        if check:  # batch by batch against the single-batch host entry point
+            for b in (0, nb // 2, nb - 1):
+                one = C.c_void_p()
+                rc = L.dfmi_filter_project_host(eng.ctx, pred.handle, progs, 3, C.byref(barr[b]), 0, C.byref(one),
+                                                C.byref(err))
+                if rc != 0:
+                    raise RuntimeError(err.message.decode())
+                for o in range(3):
+                    va, vb = _abi.dfmi_column(), _abi.dfmi_column()
+                    L.dfmi_host_result_column(res, b * 3 + o, C.byref(va))
+                    L.dfmi_host_result_column(one, o, C.byref(vb))
+                    ok = ok and va.length == vb.length and C.string_at(va.values, va.length * 8) == \
+                        C.string_at(vb.values, vb.length * 8)
+                L.dfmi_host_result_free(one)
+        L.dfmi_host_result_free(res)
+        return ok
+    same = call(check=True)
+    for _ in range(20):
+        call()
+    L.dfmi_context_set_timing(eng.ctx, 0)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        call()
+    el = (time.perf_counter() - t0) / calls
+    L.dfmi_context_set_timing(eng.ctx, 1)
+    return {"batches_per_call": nb, "rows_per_batch": m, "us_per_call": round(el * 1e6, 2),
+            "us_per_batch": round(el * 1e6 / nb, 3), "rows_per_s": m * nb / el, "calls": calls,
+            "matches_single_batch_calls": same,
+            "note": "pageable host buffers in, pinned host results out (PCIe both ways)"}
 
 
 def prefix_gate(eng, schema, dev_cols, m, pred_e, proj_e, flags=0):

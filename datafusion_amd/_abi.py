@@ -139,6 +139,7 @@ EXPORTED = [
     "dfmi_filter_project",
     "dfmi_filter_project_batches",
     "dfmi_filter_project_host",
+    "dfmi_filter_project_host_batches",
     "dfmi_host_result_num_columns",
     "dfmi_host_result_column",
     "dfmi_host_result_free",
@@ -258,6 +259,10 @@ def lib() -> C.CDLL:
                                            C.POINTER(dfmi_batch), C.c_uint32, C.POINTER(C.c_void_p),
                                            C.POINTER(dfmi_error)]
     L.dfmi_filter_project_host.restype = C.c_int32
+    L.dfmi_filter_project_host_batches.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                                   C.POINTER(dfmi_batch), C.c_int32, C.c_uint32,
+                                                   C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.POINTER(dfmi_error)]
+    L.dfmi_filter_project_host_batches.restype = C.c_int32
     L.dfmi_host_result_num_columns.argtypes = [C.c_void_p]
     L.dfmi_host_result_num_columns.restype = C.c_int32
     L.dfmi_host_result_column.argtypes = [C.c_void_p, C.c_int32, C.POINTER(dfmi_column)]

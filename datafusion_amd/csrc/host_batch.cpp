@@ -159,15 +159,22 @@ struct dfmi_host_result {
         std::vector<uint8_t, uninit_alloc<uint8_t>> bits;        // Boolean values
         std::vector<uint8_t, uninit_alloc<uint8_t>> validity;
         bool has_validity = false;
+        // dfmi_filter_project_host_batches: views into the result's arena
+        const uint8_t* v_values = nullptr;
+        const int32_t* v_offsets = nullptr;
+        const uint8_t* v_validity = nullptr;
     };
     std::shared_ptr<dfmi_host::PinnedPool> pool;
     std::vector<Col> cols;
+    dfmi_host::PinnedPool::Blk arena;  // one block holding every column (batches form)
     ~dfmi_host_result() {
-        if (pool)
+        if (pool) {
             for (Col& c : cols) {
                 pool->put(c.values);
                 pool->put(c.offsets);
             }
+            pool->put(arena);
+        }
     }
 };
 
@@ -1097,7 +1104,226 @@ extern "C" int32_t dfmi_host_result_column(const dfmi_host_result* r, int32_t i,
     view->validity = c.has_validity ? c.validity.data() : nullptr;
     view->values = c.type == DFMI_TYPE_BOOLEAN && !c.values.p ? (const void*)c.bits.data() : (const void*)c.values.p;
     view->offsets = c.type == DFMI_TYPE_UTF8 ? (const int32_t*)c.offsets.p : nullptr;
+    if (c.v_values || c.v_offsets) {  // batches form
+        view->values = c.v_values;
+        view->offsets = c.type == DFMI_TYPE_UTF8 ? c.v_offsets : nullptr;
+        view->validity = c.null_count > 0 ? c.v_validity : nullptr;
+    }
     return DFMI_OK;
 }
 
 extern "C" void dfmi_host_result_free(dfmi_host_result* r) { delete r; }
+
+// ---------------------------------------------------------------------------
+// Many small HOST batches in one call (csv_sql.rs:49-62 pulls 1024-row
+// batches from csv::Reader, in host memory): every batch's buffers are packed
+// into one pinned staging region (host threads), moved with ONE H2D copy,
+// run as ONE coalesced launch (dfmi_filter_project_batches), and the outputs
+// come back with ONE D2H copy into one pinned block the result owns; the
+// result holds num_batches x n columns, batch-major, as views into it.
+extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfmi_program* pred,
+                                                    const dfmi_program* const* projs, int32_t np,
+                                                    const dfmi_batch* ins, int32_t nb, uint32_t flags,
+                                                    dfmi_host_result** out, int32_t* failed, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    int32_t dummy_failed;
+    if (!failed) failed = &dummy_failed;
+    *failed = -1;
+    dfmi_host_result* R = nullptr;
+    try {
+        if (!ctx || !out || nb < 0 || (nb > 0 && !ins) || (np > 0 && !projs))
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        *out = nullptr;
+        dfmi::ctx_last_err_key(ctx) = ~0ull;
+        if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        HIP_TRY(hipSetDevice(dfmi::ctx_device(ctx)));
+        hipStream_t st = dfmi::ctx_stream(ctx);
+        Arena& A = arena_of(ctx);
+        A.init(dfmi::ctx_device(ctx));
+        R = new dfmi_host_result();
+        R->pool = A.results;
+        if (nb == 0) {
+            *out = R;
+            return DFMI_OK;
+        }
+        const int ncols = ins[0].num_columns;
+        const int nout = np > 0 ? np : ncols;
+        for (int32_t b = 0; b < nb; ++b) {
+            if (ins[b].num_columns != ncols || (ncols > 0 && !ins[b].columns))
+                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
+            for (int i = 0; i < ncols; ++i) {
+                const dfmi_column& c = ins[b].columns[i];
+                if (c.type != ins[0].columns[i].type) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
+                if (c.length != ins[b].num_rows) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
+                if (c.type == DFMI_TYPE_UTF8 && !c.offsets) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 offsets are NULL"};
+                if (!c.values && values_bytes(c)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
+            }
+        }
+        // ---- input layout: per batch and column, values / offsets / validity
+        struct In {
+            size_t val = 0, off = 0, vld = 0, nval = 0, noff = 0, nvld = 0;
+        };
+        std::vector<In> lay((size_t)nb * ncols);
+        size_t in_bytes = 0;
+        for (int32_t b = 0; b < nb; ++b)
+            for (int i = 0; i < ncols; ++i) {
+                const dfmi_column& c = ins[b].columns[i];
+                In& L = lay[(size_t)b * ncols + i];
+                L.nval = values_bytes(c);
+                L.val = in_bytes;
+                in_bytes += align256(L.nval);
+                if (c.type == DFMI_TYPE_UTF8) {
+                    L.noff = (size_t)(c.length + 1) * 4;
+                    L.off = in_bytes;
+                    in_bytes += align256(L.noff);
+                }
+                if (c.validity && c.null_count > 0) {
+                    L.nvld = (size_t)((c.length + 7) / 8);
+                    L.vld = in_bytes;
+                    in_bytes += align256(L.nvld);
+                }
+            }
+        // ---- output layout (worst case per batch: every row selected)
+        std::vector<int> otype(nout);
+        for (int o = 0; o < nout; ++o) {
+            if (np > 0 && !projs[o]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL projection"};
+            otype[o] = np > 0 ? projs[o]->type : ins[0].columns[o].type;
+        }
+        auto osrc = [&](int o) -> int {  // the input column a Utf8 output gathers
+            if (np == 0) return o;
+            const dfmi::IrNode& root = projs[o]->ir[projs[o]->root];
+            return root.kind == dfmi::IR_COL ? root.col : -1;
+        };
+        struct Out {
+            size_t val = 0, vld = 0, off = 0, dat = 0, ndat = 0;
+        };
+        std::vector<Out> olay((size_t)nb * nout);
+        size_t out_bytes = 0;
+        for (int32_t b = 0; b < nb; ++b)
+            for (int o = 0; o < nout; ++o) {
+                const int64_t n = ins[b].num_rows;
+                Out& L = olay[(size_t)b * nout + o];
+                const int t = otype[o];
+                L.val = out_bytes;
+                out_bytes += align256(t == DFMI_TYPE_BOOLEAN ? (size_t)bitmap_bytes(n)
+                                                             : (t == DFMI_TYPE_UTF8 ? 0 : (size_t)n * width_of(t)));
+                L.vld = out_bytes;
+                out_bytes += align256(bitmap_bytes(n));
+                if (t == DFMI_TYPE_UTF8) {
+                    L.off = out_bytes;
+                    out_bytes += align256((size_t)(n + 1) * 4);
+                    const int c = osrc(o);
+                    L.ndat = c >= 0 ? values_bytes(ins[b].columns[c]) : 0;
+                    L.dat = out_bytes;
+                    out_bytes += align256(std::max<size_t>(L.ndat, 1));
+                }
+            }
+        // ---- pack the inputs into pinned staging (host threads), one H2D
+        A.reserve_pin(std::max<size_t>(in_bytes, 256));
+        A.reserve_dev(std::max<size_t>(in_bytes + out_bytes, 256));
+        {
+            std::vector<std::function<void()>> tasks;
+            const int ways = std::max(1, std::min(A.pool->ways(), (int)(in_bytes >> 20) + 1));
+            for (int w = 0; w < ways; ++w)
+                tasks.push_back([&, w] {
+                    for (int32_t b = w; b < nb; b += ways)
+                        for (int i = 0; i < ncols; ++i) {
+                            const dfmi_column& c = ins[b].columns[i];
+                            const In& L = lay[(size_t)b * ncols + i];
+                            if (L.nval) memcpy(A.pin + L.val, c.values, L.nval);
+                            if (L.noff) memcpy(A.pin + L.off, c.offsets, L.noff);
+                            if (L.nvld) memcpy(A.pin + L.vld, c.validity, L.nvld);
+                        }
+                });
+            A.pool->run(tasks);
+        }
+        uint8_t* dev = A.dev;
+        uint8_t* dout = A.dev + align256(in_bytes);
+        HIP_TRY(hipMemcpyAsync(dev, A.pin, in_bytes, hipMemcpyHostToDevice, st));
+        std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
+        std::vector<dfmi_batch> dins(nb);
+        for (int32_t b = 0; b < nb; ++b) {
+            for (int i = 0; i < ncols; ++i) {
+                const dfmi_column& c = ins[b].columns[i];
+                const In& L = lay[(size_t)b * ncols + i];
+                dfmi_column& d = dcols[(size_t)b * ncols + i];
+                d = c;
+                d.values = dev + L.val;
+                d.offsets = c.type == DFMI_TYPE_UTF8 ? (const int32_t*)(dev + L.off) : nullptr;
+                d.validity = L.nvld ? dev + L.vld : nullptr;
+                if (!L.nvld) d.null_count = 0;
+            }
+            dins[b] = dfmi_batch{ncols, 0, ins[b].num_rows, dcols.data() + (size_t)b * ncols};
+        }
+        std::vector<dfmi_out_column> douts((size_t)nb * nout);
+        for (size_t k = 0; k < douts.size(); ++k) {
+            const Out& L = olay[k];
+            dfmi_out_column& d = douts[k];
+            memset(&d, 0, sizeof d);
+            d.values = dout + L.val;
+            d.validity = dout + L.vld;
+            if (otype[k % nout] == DFMI_TYPE_UTF8) {
+                d.offsets = (int32_t*)(dout + L.off);
+                d.data = dout + L.dat;
+                d.data_capacity = (int64_t)L.ndat;
+            }
+        }
+        // ---- the coalesced launch (synchronous), then one D2H of the outputs
+        dfmi_error e2{};
+        const int32_t rc = dfmi_filter_project_batches(ctx, pred, projs, np, dins.data(), nb, douts.data(), flags,
+                                                       failed, &e2);
+        const int32_t nok = rc == DFMI_OK ? nb : std::max(0, *failed);
+        R->arena = R->pool->get(std::max<size_t>(out_bytes, 256));
+        if (nok > 0)
+            HIP_TRY(hipMemcpyAsync(R->arena.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        R->cols.resize((size_t)nb * nout);
+        for (int32_t b = 0; b < nb; ++b)
+            for (int o = 0; o < nout; ++o) {
+                const size_t k = (size_t)b * nout + o;
+                dfmi_host_result::Col& c = R->cols[k];
+                c.type = otype[o];
+                if (b >= nok) continue;  // a failed call: batches from the failing one are empty
+                const dfmi_out_column& d = douts[k];
+                const Out& L = olay[k];
+                if (d.passthrough_column >= 0) {  // Arc clone: the caller's own column, copied
+                    const dfmi_column& src = ins[b].columns[d.passthrough_column];
+                    const In& I = lay[(size_t)b * ncols + d.passthrough_column];
+                    c.length = src.length;
+                    c.null_count = I.nvld ? src.null_count : 0;
+                    c.values = R->pool->get(std::max<size_t>(I.nval, 1));
+                    if (I.nval) memcpy(c.values.p, src.values, I.nval);
+                    c.v_values = c.values.p;
+                    if (src.type == DFMI_TYPE_UTF8) {
+                        c.offsets = R->pool->get(I.noff);
+                        memcpy(c.offsets.p, src.offsets, I.noff);
+                        c.v_offsets = (const int32_t*)c.offsets.p;
+                        c.data_length = (int64_t)I.nval;
+                    }
+                    if (I.nvld) {
+                        c.validity.assign(src.validity, src.validity + I.nvld);
+                        c.has_validity = true;
+                        c.v_validity = c.validity.data();
+                    }
+                    continue;
+                }
+                c.length = d.length;
+                c.null_count = d.null_count;
+                c.data_length = d.data_length;
+                c.v_values = R->arena.p + (otype[o] == DFMI_TYPE_UTF8 ? L.dat : L.val);
+                c.v_offsets = otype[o] == DFMI_TYPE_UTF8 ? (const int32_t*)(R->arena.p + L.off) : nullptr;
+                c.v_validity = R->arena.p + L.vld;
+            }
+        *out = R;
+        R = nullptr;
+        if (rc != DFMI_OK) {
+            if (err) *err = e2;
+            return rc;
+        }
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        delete R;
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}

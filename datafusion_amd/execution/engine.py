@@ -232,8 +232,6 @@ class DeviceEngine:
         """The same pull over a HOST batch through dfmi_filter_project_host:
         the library stages the Arrow buffers into HBM and returns host
         results (the path a Rust caller with arrow 0.12 buffers takes)."""
-        import numpy as np
-        from ..arrow import _bytes_tensor, _offsets_tensor
         L = _abi.lib()
         cols = batch.columns
         if any(c.values.device.type != "cpu" for c in cols):
@@ -254,30 +252,55 @@ class DeviceEngine:
                                         progs, len(projections), C.byref(cb), flags, C.byref(res), C.byref(err))
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
-        out = []
         try:
-            for i in range(L.dfmi_host_result_num_columns(res)):
-                v = _abi.dfmi_column()
-                L.dfmi_host_result_column(res, i, C.byref(v))
-                t = DataType(v.type)
-                n = v.length
-                if t == DataType.Utf8:
-                    offs = np.ctypeslib.as_array(C.cast(v.offsets, C.POINTER(C.c_int32)), shape=(n + 1,)).copy()
-                    nb = int(offs[-1])
-                else:
-                    offs = None
-                    nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
-                vals = (np.ctypeslib.as_array(C.cast(v.values, C.POINTER(C.c_uint8)), shape=(nb,))
-                        if nb else np.zeros(0, np.uint8))
-                valid = None
-                if v.null_count and v.validity:
-                    valid = _bytes_tensor(np.ctypeslib.as_array(C.cast(v.validity, C.POINTER(C.c_uint8)),
-                                                            shape=((n + 7) // 8,)).copy())
-                out.append(Array(t, n, _bytes_tensor(vals.copy()), valid,
-                                 _offsets_tensor(offs, "cpu") if offs is not None else None, v.null_count))
+            return _host_result_arrays(res)
         finally:
             L.dfmi_host_result_free(res)
-        return out
+
+    def filter_project_host_batches(self, predicate, projections: Optional[Sequence], batches: Sequence[RecordBatch],
+                                    flags: int = 0):
+        """The pull over many small HOST batches in one call
+        (dfmi_filter_project_host_batches): (one output column list per batch
+        up to the failing one, the error or None) -- the pull loop's view."""
+        L = _abi.lib()
+        projections = list(projections or [])
+        nb = len(batches)
+        if nb == 0:
+            return [], None
+        ncols = len(batches[0].columns)
+        nout = len(projections) if projections else ncols
+        keep = []
+        barr = (_abi.dfmi_batch * nb)()
+        for b, batch in enumerate(batches):
+            if any(c.values.device.type != "cpu" for c in batch.columns):
+                raise ValueError("filter_project_host_batches takes host batches")
+            carr = (_abi.dfmi_column * max(1, ncols))()
+            for i, a in enumerate(batch.columns):
+                carr[i] = column_struct(a)
+            keep.append(carr)
+            barr[b].num_columns = ncols
+            barr[b].num_rows = batch.num_rows()
+            barr[b].columns = carr
+        progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
+        err = _abi.dfmi_error()
+        res = C.c_void_p()
+        failed = C.c_int32(-1)
+        L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        rc = L.dfmi_filter_project_host_batches(self.ctx, predicate.handle if predicate is not None else None, progs,
+                                                len(projections), barr, nb, flags, C.byref(res), C.byref(failed),
+                                                C.byref(err))
+        error = None
+        if rc != _abi.DFMI_OK:
+            error = ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+            error.failed_batch = failed.value
+            if not res.value:
+                raise error
+        try:
+            cols = _host_result_arrays(res)
+        finally:
+            L.dfmi_host_result_free(res)
+        done = nb if error is None else max(0, failed.value)
+        return [cols[b * nout:(b + 1) * nout] for b in range(done)], error
 
     # ---- aggregate extension (DFMI_FLAG_EXT_AGGREGATE)
     def _batch_struct(self, batch: RecordBatch):
@@ -505,3 +528,32 @@ class ShardComm:
             except Exception:
                 pass
             self.handle = C.c_void_p(0)
+
+
+def _host_result_arrays(res) -> List[Array]:
+    """Every column of a dfmi_host_result, copied into host Arrays."""
+    import numpy as np
+    from ..arrow import _bytes_tensor, _offsets_tensor
+    L = _abi.lib()
+    out = []
+    for i in range(L.dfmi_host_result_num_columns(res)):
+        v = _abi.dfmi_column()
+        L.dfmi_host_result_column(res, i, C.byref(v))
+        t = DataType(v.type)
+        n = v.length
+        if t == DataType.Utf8:
+            offs = (np.ctypeslib.as_array(C.cast(v.offsets, C.POINTER(C.c_int32)), shape=(n + 1,)).copy()
+                    if v.offsets else np.zeros(1, np.int32))
+            nb = int(offs[-1])
+        else:
+            offs = None
+            nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
+        vals = (np.ctypeslib.as_array(C.cast(v.values, C.POINTER(C.c_uint8)), shape=(nb,))
+                if nb else np.zeros(0, np.uint8))
+        valid = None
+        if v.null_count and v.validity:
+            valid = _bytes_tensor(np.ctypeslib.as_array(C.cast(v.validity, C.POINTER(C.c_uint8)),
+                                                    shape=((n + 7) // 8,)).copy())
+        out.append(Array(t, n, _bytes_tensor(vals.copy()), valid,
+                         _offsets_tensor(offs, "cpu") if offs is not None else None, v.null_count))
+    return out

@@ -289,6 +289,21 @@ int32_t dfmi_host_result_num_columns(const dfmi_host_result* result);
 int32_t dfmi_host_result_column(const dfmi_host_result* result, int32_t i, dfmi_column* view);
 void dfmi_host_result_free(dfmi_host_result* result);
 
+/* Coalesced form of dfmi_filter_project_host for many small HOST batches
+ * (csv_sql.rs:49-62: 1024-row batches read from csv::Reader, pulled one
+ * next() at a time): the batches' buffers are packed into pinned memory, moved
+ * with one H2D copy, run as one dfmi_filter_project_batches launch, and the
+ * outputs come back with one D2H copy. The result holds num_batches x n
+ * columns, batch-major (n = num_projections, or num_columns without a
+ * projection). Errors as dfmi_filter_project_batches: the call returns the
+ * error of the first batch that raises one and *failed_batch names it; the
+ * result is still returned, with the batches before it complete and the rest
+ * empty (the caller hands those out first). Free the result in every case. */
+int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfmi_program* predicate,
+                                         const dfmi_program* const* projections, int32_t num_projections,
+                                         const dfmi_batch* inputs, int32_t num_batches, uint32_t flags,
+                                         dfmi_host_result** out, int32_t* failed_batch, dfmi_error* err);
+
 /* Pinned host memory for batch buffers (e.g. a CSV reader parsing straight
  * into them; csv_sql.rs:49's DataSource side). Columns whose buffers lie in
  * such memory -- or in any hipHostMalloc'd allocation of at least 1 MiB --

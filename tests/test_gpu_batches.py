@@ -44,13 +44,17 @@ def make_batches(sizes, seed=1, nullable_every=3, utf8=True):
     return s, out
 
 
-def check(schema, batches, pred_e, proj_e, flags=0):
+def check(schema, batches, pred_e, proj_e, flags=0, host=False):
     """Device batched results == the oracle batch by batch, or the first
-    failing batch with the oracle's error (batches before it complete)."""
+    failing batch with the oracle's error (batches before it complete).
+    host: the batches stay in host memory (dfmi_filter_project_host_batches)."""
     p = compile_scalar_expr(None, pred_e, schema, flags) if pred_e is not None else None
     cp = [compile_scalar_expr(None, e, schema, flags) for e in proj_e]
-    dbs = [b.to(engine().device) for b in batches]
-    got, err = engine().filter_project_batches(p, cp, dbs, flags)
+    if host:
+        got, err = engine().filter_project_host_batches(p, cp, [b.to("cpu") for b in batches], flags)
+    else:
+        dbs = [b.to(engine().device) for b in batches]
+        got, err = engine().filter_project_batches(p, cp, dbs, flags)
     for i, b in enumerate(batches):
         try:
             ref = oracle_filter_project(schema, b, pred_e, proj_e, flags)
@@ -67,34 +71,38 @@ def check(schema, batches, pred_e, proj_e, flags=0):
     return None
 
 
-def test_c2_query_many_batches():
+@pytest.mark.parametrize("host", [False, True])
+def test_c2_query_many_batches(host):
     s, bs = make_batches(SIZES)
     pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.3))), Operator.And,
                       BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.7))))
     projs = [Column(0), Column(1), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus,
                                               Column(2))]
-    assert check(s, bs, pred, projs) is None
+    assert check(s, bs, pred, projs, host=host) is None
     # FilterRelation output (every column, Utf8 gathered)
-    assert check(s, bs, pred, []) is None
+    assert check(s, bs, pred, [], host=host) is None
 
 
-def test_utf8_equality_and_gather_many_batches():
+@pytest.mark.parametrize("host", [False, True])
+def test_utf8_equality_and_gather_many_batches(host):
     s, bs = make_batches(SIZES, seed=2)
     pred = BinaryExpr(Column(3), Operator.Eq, Literal(Utf8("w17")))
-    assert check(s, bs, pred, [Column(3), Column(0)], DFMI_FLAG_EXT_UTF8_COMPARE) is None
+    assert check(s, bs, pred, [Column(3), Column(0)], DFMI_FLAG_EXT_UTF8_COMPARE, host=host) is None
     pred = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.5)))
-    assert check(s, bs, pred, [Column(3), Column(2)]) is None
+    assert check(s, bs, pred, [Column(3), Column(2)], host=host) is None
 
 
-def test_projection_only_many_batches():
+@pytest.mark.parametrize("host", [False, True])
+def test_projection_only_many_batches(host):
     """No predicate: dense kernel per batch, null propagation, passthrough."""
     s, bs = make_batches(SIZES, seed=3)
     projs = [BinaryExpr(Column(0), Operator.Plus, Column(1)), Column(2), Column(3),
              BinaryExpr(Column(0), Operator.Lt, Column(1))]
-    assert check(s, bs, None, projs) is None
+    assert check(s, bs, None, projs, host=host) is None
 
 
-def test_error_in_a_middle_batch():
+@pytest.mark.parametrize("host", [False, True])
+def test_error_in_a_middle_batch(host):
     """DivideByZero in batch 57 only: batches 0..56 are returned, batch 57
     raises the oracle's error."""
     s, bs = make_batches([1024] * 80, seed=4, utf8=False)
@@ -104,15 +112,16 @@ def test_error_in_a_middle_batch():
     bs[57] = RecordBatch(s, [bs[57].columns[0], Array.from_numpy(DataType.Float64, v), bs[57].columns[2]])
     pred = BinaryExpr(Column(2), Operator.GtEq, Literal(Float64(0.0)))
     projs = [BinaryExpr(Column(0), Operator.Divide, Column(1))]
-    assert check(s, bs, pred, projs) == 57
+    assert check(s, bs, pred, projs, host=host) == 57
     # not selected in batch 57 -> no error at all
     v2 = np.array(bs[57].columns[2].cpu().numpy_values())
     v2[500] = -1.0
     bs[57] = RecordBatch(s, [bs[57].columns[0], bs[57].columns[1], Array.from_numpy(DataType.Float64, v2)])
-    assert check(s, bs, pred, projs) is None
+    assert check(s, bs, pred, projs, host=host) is None
 
 
-def test_static_error_fails_batch_zero():
+@pytest.mark.parametrize("host", [False, True])
+def test_static_error_fails_batch_zero(host):
     """A plan error the reference raises on every pull ("filter not supported
     for Int64", filter.rs:106-110) fails the first batch."""
     s = Schema([Field("a", DataType.Float64, False), Field("i", DataType.Int64, False)])
@@ -120,14 +129,15 @@ def test_static_error_fails_batch_zero():
     bs = [RecordBatch(s, [Array.from_numpy(DataType.Float64, rng.random(n)),
                           Array.from_numpy(DataType.Int64, rng.integers(-5, 5, n))]) for n in (0, 100, 1024)]
     pred = BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.5)))
-    assert check(s, bs, pred, []) == 0
-    assert check(s, bs, pred, [], DFMI_FLAG_EXT_GATHER_ALL) is None  # the extension gathers Int64
+    assert check(s, bs, pred, [], host=host) == 0
+    assert check(s, bs, pred, [], DFMI_FLAG_EXT_GATHER_ALL, host=host) is None  # the extension gathers Int64
 
 
-def test_boolean_outputs_fall_back_to_per_batch():
+@pytest.mark.parametrize("host", [False, True])
+def test_boolean_outputs_fall_back_to_per_batch(host):
     s, bs = make_batches([1024] * 10 + [77, 0, 3000], seed=6)
     pred = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.8)))
-    assert check(s, bs, pred, [BinaryExpr(Column(1), Operator.Gt, Column(2)), Column(1)]) is None
+    assert check(s, bs, pred, [BinaryExpr(Column(1), Operator.Gt, Column(2)), Column(1)], host=host) is None
 
 
 def test_relation_coalesces_batches():

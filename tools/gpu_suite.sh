@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=${1:-suite}
 mkdir -p gpurun_out
-timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --durations=30 --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; tail -5 gpurun_out/pytest_$TAG.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { cat gpurun_out/smoke_$TAG.log; exit 1; }
 cat gpurun_out/smoke_$TAG.log
