@@ -775,7 +775,7 @@ std::string generate(const Plan& P, Launch& X) {
                     o << "  dfmi::utf8_gather" << (X.gather == 2 ? "_serial" : "") << "<BLOCK, K, NCH, ARENA>(A, T, "
                       << (j + 1) << ", " << u << ", " << X.utf8_outs[j].first << ", selm, wm, dst" << tail
                       << "G[wave], lane, wave, " << kb
-                      << (X.gather == 2 ? "" : X.gather == 4 ? ", 1" : X.gather == 5 ? ", 2" : ", 0")
+                      << (X.gather == 2 ? "" : X.gather == 4 ? (X.pairs ? ", 3" : ", 1") : X.gather == 5 ? ", 2" : ", 0")
                       << (X.gather == 2 ? "" : (prestaged && j == 0 ? ", pre_" : ", -1"))
                       << (X.gather == 2 ? "" : X.gather_phases ? ", true" : ", false")
                       << (X.gather == 2 ? "" : X.dbuf ? ", true" : ", false") << ");\n";
@@ -1037,7 +1037,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);
@@ -1081,10 +1081,18 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
     ShapeHit h;
     h.fn = compile(device, src, X.kname, compile_ms);
     if (X.waves_soft && X.waves_per_eu > 0) {
-        // a soft occupancy hint: if the register allocator had to spill to
-        // meet it, the query shape is compiled again without it
-        int scratch = 0;
-        if (hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, h.fn) == hipSuccess && scratch > 0) {
+        // a soft occupancy hint: if the register allocator had to spill more
+        // than a little to meet it, the query shape is compiled again without
+        // it (the C3 gather kernel spills 72 B/lane under hipRTC at 8
+        // waves/SIMD and is still 6% faster than at 6 waves)
+        constexpr int kSoftSpill = 128;
+        int scratch = 0, regs = 0;
+        const bool got = hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, h.fn) == hipSuccess;
+        (void)hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, h.fn);
+        if (getenv("DFMI_JIT_VERBOSE"))
+            fprintf(stderr, "dfmi jit: %s waves_per_eu %d: scratch %d B/lane, %d VGPRs%s\n", X.kname.c_str(),
+                    X.waves_per_eu, scratch, regs, got && scratch > kSoftSpill ? " -> recompiled without the hint" : "");
+        if (got && scratch > kSoftSpill) {
             double ms2 = 0;
             X.waves_per_eu = 0;
             src = generate(P, X);

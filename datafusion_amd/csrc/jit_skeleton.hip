@@ -1139,6 +1139,39 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     int cur = 1;          // dbuf: the half holding slices (.., staged_to]
     int next_to = -1;     // dbuf: slices (staged_to, next_to] are being staged into the other half
     unsigned since = 0;   // dbuf: store instructions issued after those loads (a lower bound)
+    // emit == 3: two slices' images assembled together (two images of DST/2
+    // chunks): zeroing, placing and storing of a pair each pay one LDS round
+    // trip instead of two; a slice waits for its partner while it is pending
+    constexpr int IM = DST / 2;  // chunks per image in pairs mode
+    bool pend = false;           // a slice placed-to-be in image 0 (uniform)
+    int p_sh = 0, p_Ls = 0, p_nw = 0, p_off = 0;
+    u8* p_w0 = nullptr;
+    int p_a = 0, p_d = 0, p_L = 0;  // per lane: its string in the pending slice
+    auto img_store = [&](const unsigned* im, u8* w0x, int shx, int Lsx, int nwx) {
+        for (int j = lane; j < nwx; j += 64) {
+            const unsigned val = im[j];
+            const int p = 4 * j - shx;
+            if (p >= 0 && p + 4 <= Lsx) {
+                *at<unsigned>(w0x, 4 * j) = val;
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (p + b >= 0 && p + b < Lsx) w0x[4 * j + b] = (u8)(val >> (8 * b));
+            }
+        }
+    };
+    auto flush_single = [&]() {  // the pending slice alone
+        if (!pend) return;
+        unsigned* im = gd;
+        for (int c = lane; 4 * c < p_nw; c += 64) ((uint4*)im)[c] = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_fence();
+        if (p_L) utf8_place(gs + 4 * p_off, im, p_a, p_d, p_L);
+        wave_lds_fence();
+        img_store(im, p_w0, p_sh, p_Ls, p_nw);
+        wave_lds_fence();
+        since += 2;
+        pend = false;
+    };
     if (pre >= 0) {
         if (dbuf) {
             next_to = pre;  // prestaged into half 0 (cur ^ 1)
@@ -1154,6 +1187,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         if (!m) continue;
         tick(1);
         if (k > staged_to) {
+            if (emit == 3) flush_single();  // the arena is about to be restaged
             if (!dbuf) {
                 staged_to = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k, G.src, lane);
                 wait_vm_loads();
@@ -1201,7 +1235,8 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         if (Ls == 0) continue;
         const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
         // a span over the stage, or (LDS image) an output over the image: each lane copies its string
-        if (nch > kStageChunks || (emit == 1 && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST)) {
+        if (nch > kStageChunks || (emit == 1 && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST) ||
+            (emit == 3 && ((sh + (int)Ls + 3) >> 2) > 4 * IM)) {
             if (sel && L) utf8_copy(src + s[k], out + ob0 + rel, L);
             continue;
         }
@@ -1216,6 +1251,28 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             continue;
         }
         const int nw = (sh + (int)Ls + 3) >> 2;
+        if (emit == 3) {
+            if (!pend) {  // wait for a partner
+                pend = true;
+                p_sh = sh, p_Ls = (int)Ls, p_nw = nw, p_off = my_off, p_w0 = w0;
+                p_a = (int)(s[k] - c0), p_d = sh + (int)rel, p_L = (int)L;
+                continue;
+            }
+            unsigned* im0 = gd;
+            unsigned* im1 = gd + 4 * IM;
+            for (int c = lane; 4 * c < p_nw; c += 64) ((uint4*)im0)[c] = make_uint4(0u, 0u, 0u, 0u);
+            for (int c = lane; 4 * c < nw; c += 64) ((uint4*)im1)[c] = make_uint4(0u, 0u, 0u, 0u);
+            wave_lds_fence();
+            if (p_L) utf8_place(gs + 4 * p_off, im0, p_a, p_d, p_L);
+            if (L) utf8_place(gs + 4 * my_off, im1, (int)(s[k] - c0), sh + (int)rel, (int)L);
+            wave_lds_fence();
+            img_store(im0, p_w0, p_sh, p_Ls, p_nw);
+            img_store(im1, w0, sh, (int)Ls, nw);
+            wave_lds_fence();
+            since += 4;
+            pend = false;
+            continue;
+        }
         tick(1);
         for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_fence();
@@ -1238,6 +1295,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         tick(4);
         since += 2;  // this slice's out_offs store and at least one image store
     }
+    if (emit == 3) flush_single();
     if (tp_on && lane == 0)
 #pragma unroll
         for (int i = 0; i < 5; ++i) atomicAdd(A.stats + 8 + i, tacc[i]);
