@@ -336,7 +336,7 @@ def batches_line(eng, schema, cols, sel, dev):
             # status words (tens of MB), spread over all of its own blocks
             n = cols[0].numel()
             big_outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
-            big = FusedStep(eng, schema, cols, n, *query(0.01), big_outs)
+            big = FusedStep(eng, schema, cols, n, *query(sel), big_outs)  # the headline's own query
             big()
             _abi.lib().dfmi_context_set_timing(eng.ctx, 0)
             after = []

@@ -7,10 +7,10 @@
 # bench.py reads (roofline.rocprof / roofline.traffic of every line).
 # usage: tools/profile_r03.sh <out dir, e.g. gpurun_out/r03> [runs...]
 set -o pipefail
-OUT=${1:-gpurun_out/r03}
+R=$(pwd)
+OUT=$R/${1:-gpurun_out/r03}
 shift
 RUNS=${@:-main c2_s0.01 c2_s0.99}
-R=$(pwd)
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for run in $RUNS; do
