@@ -131,7 +131,7 @@ def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
          "traffic": None}
     p = profiled(kernel, run)
     if p:
-        per_launch_alg = alg_bytes / launches
+        per_launch_alg = alg_bytes  # alg_bytes and kms are per launch
         avg_ms = p["avg_ns"] * 1e-6
         r["rocprof"] = {"source": "%s/%s/traffic.json" % (PROFILE_TAG, run), "avg_ms": round(avg_ms, 4),
                         "launches": p["launches"], "frac": round(per_launch_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
