@@ -358,6 +358,12 @@ extern "C" int32_t dfmi_last_error_order(const dfmi_context* c, uint64_t* key) {
 
 // Internal test hook: look-back timeouts relaunched on this context.
 extern "C" long dfmi_internal_relaunches(const dfmi_context* c) { return c ? c->relaunches : -1; }
+// Internal test hook: the hipRTC module cache's size after bounding it to
+// `cap` modules (cap > 0; 0 leaves the bound unchanged).
+extern "C" int64_t dfmi_internal_jit_cache(int64_t cap) {
+    jit::cache_cap(cap > 0 ? (size_t)cap : 0);
+    return (int64_t)jit::cache_size();
+}
 
 extern "C" const char* dfmi_last_kernel_name(const dfmi_context* c) {
     return c ? c->last_kernel.c_str() : "";

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -307,13 +308,40 @@ struct Gen {
 };
 
 // ------------------------------------------------------------ compile cache
+// Loaded code objects, keyed by device + source text, bounded (least recently
+// used evicted past the cap). A module is unloaded when the last holder lets
+// go: the cache, and every Launch that got its kernel from get_kernel
+// (Launch::module) -- so a launch in flight keeps its code object loaded.
+// The map itself is never destroyed: modules still cached at process exit
+// are left to the runtime's teardown, as before the bound.
 namespace {
 struct Compiled {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    ~Compiled() {
+        if (mod) (void)hipModuleUnload(mod);
+    }
+};
+struct CacheEntry {
+    std::shared_ptr<Compiled> c;
+    uint64_t used = 0;
 };
 std::mutex g_mu;
-std::map<std::string, Compiled> g_cache;  // key: device + source text
+auto& g_cache = *new std::map<std::string, CacheEntry>();  // guarded by g_mu
+uint64_t g_tick = 0;
+size_t g_cap = [] {
+    const char* e = getenv("DFMI_JIT_CACHE_MODULES");
+    return e && atoi(e) > 0 ? (size_t)atoi(e) : (size_t)256;
+}();
+// caller holds g_mu
+void evict_to(size_t cap) {
+    while (g_cache.size() > cap) {
+        auto lru = g_cache.begin();
+        for (auto it = g_cache.begin(); it != g_cache.end(); ++it)
+            if (it->second.used < lru->second.used) lru = it;
+        g_cache.erase(lru);
+    }
+}
 }  // namespace
 
 std::vector<char> compile_code(const std::string& src, double* compile_ms) {
@@ -343,23 +371,40 @@ std::vector<char> compile_code(const std::string& src, double* compile_ms) {
     return code;
 }
 
-static hipFunction_t compile(int device, const std::string& src, const std::string& name, double* compile_ms) {
+static std::shared_ptr<Compiled> compile(int device, const std::string& src, const std::string& name,
+                                         double* compile_ms) {
     const std::string key = std::to_string(device) + "\n" + src;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
-    if (it != g_cache.end()) return it->second.fn;
+    if (it != g_cache.end()) {
+        it->second.used = ++g_tick;
+        return it->second.c;
+    }
     const std::vector<char> code = compile_code(src, compile_ms);
-    Compiled c;
-    if (hipModuleLoadData(&c.mod, code.data()) != hipSuccess) throw Fail{DFMI_ERR_DEVICE, "hipModuleLoadData failed"};
-    if (hipModuleGetFunction(&c.fn, c.mod, name.c_str()) != hipSuccess)
+    auto c = std::make_shared<Compiled>();
+    if (hipModuleLoadData(&c->mod, code.data()) != hipSuccess) {
+        c->mod = nullptr;
+        throw Fail{DFMI_ERR_DEVICE, "hipModuleLoadData failed"};
+    }
+    if (hipModuleGetFunction(&c->fn, c->mod, name.c_str()) != hipSuccess)
         throw Fail{DFMI_ERR_DEVICE, "hipModuleGetFunction failed"};
-    g_cache[key] = c;
-    return c.fn;
+    evict_to(g_cap - 1);
+    g_cache[key] = CacheEntry{c, ++g_tick};
+    return c;
 }
 
 size_t cache_size() {
     std::lock_guard<std::mutex> lk(g_mu);
     return g_cache.size();
+}
+
+size_t cache_cap(size_t cap) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (cap > 0) {
+        g_cap = cap;
+        evict_to(cap);
+    }
+    return g_cap;
 }
 
 // --------------------------------------------------------------- kernels
@@ -999,7 +1044,7 @@ std::string generate(const Plan& P, Launch& X) {
 // text per call otherwise).
 namespace {
 struct ShapeHit {
-    hipFunction_t fn;
+    std::weak_ptr<Compiled> mod;  // an evicted module makes the entry stale
     std::string kname;
     uint64_t lits[32];
     int n_lits;
@@ -1063,8 +1108,11 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_shapes.find(key);
+        std::shared_ptr<Compiled> c;
+        if (it != g_shapes.end() && !(c = it->second.mod.lock())) g_shapes.erase(it), it = g_shapes.end();
         if (it != g_shapes.end()) {
             const ShapeHit& h = it->second;
+            X.module = c;
             memcpy(X.args_lits, h.lits, sizeof h.lits);
             X.n_lits = h.n_lits;
             memcpy(X.str_off, h.str_off, sizeof h.str_off);
@@ -1073,13 +1121,13 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
             X.n_str = h.n_str;
             X.str_bytes = h.str_bytes;
             X.kname = h.kname;
-            return h.fn;
+            return c->fn;
         }
     }
     std::string src = generate(P, X);
     if (getenv("DFMI_JIT_PRINT")) fprintf(stderr, "%s\n", src.c_str() + strlen(dfmi_skeleton_src));
     ShapeHit h;
-    h.fn = compile(device, src, X.kname, compile_ms);
+    std::shared_ptr<Compiled> c = compile(device, src, X.kname, compile_ms);
     if (X.waves_soft && X.waves_per_eu > 0) {
         // a soft occupancy hint: if the register allocator had to spill more
         // than a little to meet it, the query shape is compiled again without
@@ -1087,8 +1135,8 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
         // waves/SIMD and is still 6% faster than at 6 waves)
         constexpr int kSoftSpill = 128;
         int scratch = 0, regs = 0;
-        const bool got = hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, h.fn) == hipSuccess;
-        (void)hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, h.fn);
+        const bool got = hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, c->fn) == hipSuccess;
+        (void)hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, c->fn);
         if (getenv("DFMI_JIT_VERBOSE"))
             fprintf(stderr, "dfmi jit: %s waves_per_eu %d: scratch %d B/lane, %d VGPRs%s\n", X.kname.c_str(),
                     X.waves_per_eu, scratch, regs, got && scratch > kSoftSpill ? " -> recompiled without the hint" : "");
@@ -1096,10 +1144,12 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
             double ms2 = 0;
             X.waves_per_eu = 0;
             src = generate(P, X);
-            h.fn = compile(device, src, X.kname, &ms2);
+            c = compile(device, src, X.kname, &ms2);
             if (compile_ms) *compile_ms += ms2;
         }
     }
+    h.mod = c;
+    X.module = c;
     h.kname = X.kname;
     memcpy(h.lits, X.args_lits, sizeof h.lits);
     h.n_lits = X.n_lits;
@@ -1111,7 +1161,7 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_shapes.size() >= 4096) g_shapes.clear();  // bounded: programs come and go
     g_shapes[key] = h;
-    return h.fn;
+    return c->fn;
 }
 
 }  // namespace jit

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -97,6 +98,7 @@ struct Launch {
     char str[256] = {};
     int n_str = 0, str_bytes = 0;
     std::string kname;  // generated kernel's name (dfmi_<kind>_<hash>)
+    std::shared_ptr<const void> module;  // keeps the kernel's code object loaded (get_kernel)
     // coalesced batches (dfmi_filter_project_batches): blocks map to batches
     // through Args::tile_batch, and each batch's sizes and buffers come from
     // its row of Args::batch_ptrs (layout: batch_slot_* below)
@@ -143,6 +145,8 @@ std::string generate(const Plan& P, Launch& X);
 // Compiled kernel for the plan (cached per source text and device).
 hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_ms);
 size_t cache_size();
+// Bound of the module cache (least recently used evicted); cap > 0 sets it.
+size_t cache_cap(size_t cap);
 // hipRTC compile of a generated source to a gfx950 code object (no device needed).
 std::vector<char> compile_code(const std::string& src, double* compile_ms);
 
