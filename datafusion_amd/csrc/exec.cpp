@@ -256,11 +256,13 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
     if (diag)
         if (const char* e = getenv("DFMI_UTF8_DBUF")) X.dbuf = atoi(e) & 1;
     if (diag)
+        if (const char* e = getenv("DFMI_UTF8_ST16")) X.st16 = atoi(e) & 1;
+    if (diag)
         if (const char* e = getenv("DFMI_UTF8_PAIRS")) {
             X.pairs = atoi(e) & 1;
             if (X.pairs) X.image = 130;  // two images of 65 chunks
         }
-    if (X.dbuf && X.arena < 2 * 128) X.dbuf = 0;  // each half holds one slice's span
+    if (X.dbuf && X.arena < 128) X.dbuf = 0;  // halves of >= 64 chunks (longer spans copy per lane)
     if (X.M == 1 || X.KO == 0) X.KO = X.K;
     if (X.KO < 1 || X.KO > X.K || X.K % X.KO) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.M * X.BLOCK / 64 > 256)

@@ -820,7 +820,7 @@ std::string generate(const Plan& P, Launch& X) {
                     o << "  dfmi::utf8_gather" << (X.gather == 2 ? "_serial" : "") << "<BLOCK, K, NCH, ARENA>(A, T, "
                       << (j + 1) << ", " << u << ", " << X.utf8_outs[j].first << ", selm, wm, dst" << tail
                       << "G[wave], lane, wave, " << kb
-                      << (X.gather == 2 ? "" : X.gather == 4 ? (X.pairs ? ", 3" : ", 1") : X.gather == 5 ? ", 2" : ", 0")
+                      << (X.gather == 2 ? "" : X.gather == 4 ? (X.pairs ? ", 3" : X.st16 ? ", 4" : ", 1") : X.gather == 5 ? ", 2" : ", 0")
                       << (X.gather == 2 ? "" : (prestaged && j == 0 ? ", pre_" : ", -1"))
                       << (X.gather == 2 ? "" : X.gather_phases ? ", true" : ", false")
                       << (X.gather == 2 ? "" : X.dbuf ? ", true" : ", false") << ");\n";
@@ -1082,7 +1082,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

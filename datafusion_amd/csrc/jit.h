@@ -82,6 +82,7 @@ struct Launch {
     int pairs = 0;     // gather 4: two slices' LDS images assembled together (image = 2 x 65 chunks)
     int dbuf = 0;      // gather 1 / 4 / 5: the arena's halves double-buffer the staging (ARENA >= 256)
     int image = 129;   // gather 4: LDS image per wave, 16-byte chunks (a longer slice output copies per lane)
+    int st16 = 0;      // gather 4: the image 16-byte aligned, stored with 16-byte stores (edge words apart)
     int prestage = 0;
     int gather_phases = 0;  // diagnostics: per-phase cycle counters in utf8_gather (DFMI_DEBUG_MODE bit 5)  // gather 1 / 4: the first staging round is issued before the look-back
     // cache policy of the column streams: bit0 nontemporal loads, bit1 nontemporal stores

@@ -1023,6 +1023,35 @@ __device__ __forceinline__ void utf8_emit_slice_mk(const unsigned* sg, int* tab,
 // The 16-byte-chunk source span of slice k (wave-uniform): chunks from the
 // one holding the first selected string's first byte to the one holding the
 // last one's last byte, as an offset from src and a count (0: no bytes).
+// Store a slice's LDS image (output bytes [sh, sh + Ls) of the image, image
+// byte 0 at the 16-byte aligned output address w0) with 16-byte stores:
+// lanes on the whole chunks (no branches per word), then lanes 0-7 on the
+// words of the first and last chunk when they are partial -- shared with
+// the neighbouring slices' outputs, written whole words or bytes inside
+// [sh, sh + Ls) only.
+__device__ __forceinline__ void utf8_image_store16(const uint4* im, u8* w0, int sh, int Ls, int lane) {
+    const int e = sh + Ls;
+    const int cf = (sh + 15) >> 4;  // first whole chunk
+    const int cl = e >> 4;          // one past the last whole chunk
+    for (int c = cf + lane; c < cl; c += 64) *at<uint4>(w0, 16 * c) = im[c];
+    // partial chunks: the first (sh > 0, or the slice ends inside it) and the last
+    const int pf = (sh & 15) || cl < cf ? 0 : -1;
+    const int pl = (e & 15) && (e >> 4) != pf ? (e >> 4) : -1;
+    if (lane < 8) {
+        const int c = lane < 4 ? pf : pl;
+        if (c >= 0) {
+            const int w = 4 * c + (lane & 3);  // image word
+            const int lo = max(4 * w, sh), hi = min(4 * w + 4, e);
+            if (hi - lo == 4) {
+                *at<unsigned>(w0, 4 * w) = ((const unsigned*)im)[w];
+            } else if (hi > lo) {
+                const unsigned v = ((const unsigned*)im)[w];
+                for (int b = lo; b < hi; ++b) w0[b] = (u8)(v >> (8 * (b & 3)));
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void utf8_span(u64 m, int s, int e, i64 sm, i64& c0, int& nch) {
     const int fl = __builtin_ctzll(m), ll = 63 - __builtin_clzll(m);
     const i64 s0 = __builtin_amdgcn_readlane(s, fl), s1 = __builtin_amdgcn_readlane(e, ll);
@@ -1048,13 +1077,14 @@ __device__ __forceinline__ void utf8_spans(const u8* src, const u64 (&wm)[K], co
 // (slices whose span exceeds kStageChunks are copied per lane, not staged).
 template <int K, int ARENA>
 __device__ __forceinline__ int utf8_stage_group(const u8* src, const u64 (&wm)[K], const i64 (&cs)[K],
-                                                const int (&cn)[K], int k, uint4* arena, int lane) {
+                                                const int (&cn)[K], int k, uint4* arena, int lane,
+                                                int scap = kStageChunks) {
     int staged_to = k - 1, used = 0;
     bool full = false;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         if (j < k || full || !wm[j]) continue;
-        if (cn[j] > kStageChunks) {  // copied per lane when processed
+        if (cn[j] > scap) {  // copied per lane when processed
             if (j == k) staged_to = j;
             else full = true;
             continue;
@@ -1085,7 +1115,7 @@ __device__ __forceinline__ int utf8_gather_prestage(const Args& A, int u, const 
 #pragma unroll
     for (int k = K - 1; k >= 0; --k)
         if (wm[k]) k0 = k;
-    return k0 < 0 ? -1 : utf8_stage_group<K, CAP>(src, wm, cs, cn, k0, G.src, lane);
+    return k0 < 0 ? -1 : utf8_stage_group<K, CAP>(src, wm, cs, cn, k0, G.src, lane, CAP < kStageChunks ? CAP : kStageChunks);
 }
 
 // Copy the selected rows of Utf8 input u into output o (rebased i32
@@ -1136,6 +1166,10 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     // issued after them (vmcnt counts both, in issue order: at least 2
     // store instructions per slice placed through the image follow them)
     constexpr int HALF = ARENA / 2;
+    // longest span staged: a half of the arena under dbuf (a longer slice
+    // copies per lane: at 128 chunks, halves of 1 KiB hold a 64-row slice of
+    // C3's 13.9-byte strings)
+    const int scap = dbuf ? (HALF < kStageChunks ? HALF : kStageChunks) : kStageChunks;
     int cur = 1;          // dbuf: the half holding slices (.., staged_to]
     int next_to = -1;     // dbuf: slices (staged_to, next_to] are being staged into the other half
     unsigned since = 0;   // dbuf: store instructions issued after those loads (a lower bound)
@@ -1202,14 +1236,15 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
                     else if (since >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
                     else wait_vm_loads();
                 } else {
-                    staged_to = utf8_stage_group<K, HALF>(src, wm, cs, cn, k, G.src + cur * HALF, lane);
+                    staged_to = utf8_stage_group<K, HALF>(src, wm, cs, cn, k, G.src + cur * HALF, lane, scap);
                     wait_vm_loads();
                 }
                 aoff = cur * HALF;
                 next_to = -1;
                 since = 0;
                 if (staged_to + 1 < K) {
-                    const int nt = utf8_stage_group<K, HALF>(src, wm, cs, cn, staged_to + 1, G.src + (cur ^ 1) * HALF, lane);
+                    const int nt = utf8_stage_group<K, HALF>(src, wm, cs, cn, staged_to + 1, G.src + (cur ^ 1) * HALF, lane,
+                                                             scap);
                     if (nt > staged_to) next_to = nt;
                 }
             }
@@ -1227,20 +1262,22 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         const i64 c0 = cs[k];
         const int nch = cn[k];
         const int my_off = aoff;
-        if (nch <= kStageChunks) aoff += nch;
+        if (nch <= scap) aoff += nch;
         if ((i64)(ob0 + Ls) > A.out_cap[o]) {
             if (lane == 0) report_err(A.err, 0, 0, ERRK_CAPACITY);
             continue;
         }
         if (Ls == 0) continue;
-        const int sh = (int)(((u64)out + ob0) & 3u);  // output address mod 4 = the slice's offset in G.dst
+        // the slice's offset in G.dst: output address mod 4 (mod 16 for the
+        // 16-byte image stores of emit 4)
+        const int sh = (int)(((u64)out + ob0) & (emit == 4 ? 15u : 3u));
         // a span over the stage, or (LDS image) an output over the image: each lane copies its string
-        if (nch > kStageChunks || (emit == 1 && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST) ||
+        if (nch > scap || ((emit == 1 || emit == 4) && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST) ||
             (emit == 3 && ((sh + (int)Ls + 3) >> 2) > 4 * IM)) {
             if (sel && L) utf8_copy(src + s[k], out + ob0 + rel, L);
             continue;
         }
-        u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word holding the slice's first byte
+        u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word (chunk) holding the slice's first byte
         if (emit == 2) {
             utf8_emit_slice_mk(gs + 4 * my_off, (int*)gd, (u8*)(gd + 128), w0, sh, sh + (int)Ls, incl, rel, L,
                                (int)(s[k] - c0), lane);
@@ -1280,6 +1317,13 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         if (L) utf8_place(gs + 4 * my_off, gd, (int)(s[k] - c0), sh + (int)rel, (int)L);
         wave_lds_fence();
         tick(3);
+        if (emit == 4) {
+            utf8_image_store16(G.dst, w0, sh, (int)Ls, lane);
+            wave_lds_fence();
+            tick(4);
+            since += 2;
+            continue;
+        }
         for (int j = lane; j < nw; j += 64) {
             const unsigned val = gd[j];
             const int p = 4 * j - sh;  // output position of the word's first byte

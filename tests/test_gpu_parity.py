@@ -375,20 +375,24 @@ def test_utf8_multi_channel_many_tiles():
         run_both(s, b, BinaryExpr(Column(c), Operator.NotEq, Literal(Utf8(w))), [Column(c)], DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
-@pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q"])
+@pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q", "4w", "4wd"])
 def test_utf8_gather_variants(monkeypatch, variant):
     """The Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG: 3 = two
     passes -- offsets + source starts in the query kernel, bytes by
     k_utf8_copy_rows --, 2 = one staged slice per round trip, 0 = per-lane
     copy, 4 = slices assembled in an LDS image, 1 = output words' strings by
     binary search, 5 = by marker scan; p: first staging round before the
-    look-back; d: double-buffered staging; q: slices' images in pairs) against
+    look-back; d: double-buffered staging; q: slices' images in pairs; w: the
+    image stored in 16-byte chunks) against
     the oracle on the Utf8 parity cases above."""
     if variant.endswith("p"):
         monkeypatch.setenv("DFMI_UTF8_PRESTAGE", "1")
         variant = variant[:-1]
     if variant.endswith("d"):  # the arena's halves double-buffer the staging
         monkeypatch.setenv("DFMI_UTF8_DBUF", "1")
+        variant = variant[:-1]
+    if variant.endswith("w"):  # 16-byte aligned image, 16-byte stores
+        monkeypatch.setenv("DFMI_UTF8_ST16", "1")
         variant = variant[:-1]
     if variant.endswith("q"):  # two slices' images assembled together
         monkeypatch.setenv("DFMI_UTF8_PAIRS", "1")
