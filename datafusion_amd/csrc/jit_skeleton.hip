@@ -765,6 +765,17 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
+// OR v into the LDS word p (no return value). Through inline asm: the
+// compiler's wait-count pass, which does not see the explicit vmcnt wait
+// after each staging round, otherwise puts an s_waitcnt vmcnt(0) before
+// every LDS atomic after direct global->LDS loads -- which also waits for
+// the global stores issued since (the previous slice's image and offsets).
+// A wave's LDS operations execute in order: later reads of p see the result.
+__device__ __forceinline__ void lds_or(unsigned* p, unsigned v) {
+    const unsigned la = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned*)p;
+    asm volatile("ds_or_b32 %0, %1" ::"v"(la), "v"(v) : "memory");
+}
+
 // Bytes [lo, hi) of a word as a mask (0 <= lo < hi <= 4).
 __device__ __forceinline__ unsigned byte_mask(int lo, int hi) {
     return (0xffffffffu >> (8 * (4 - hi))) & (0xffffffffu << (8 * lo));
@@ -839,7 +850,7 @@ __device__ __forceinline__ void utf8_gather_serial(const Args& A, const Tile<BLO
                 const unsigned lo = gs[sw < 0 ? 0 : sw], hi = gs[sw + 1];
                 const unsigned val = __builtin_amdgcn_alignbyte(hi, lo, (unsigned)sb & 3u);
                 const unsigned msk = byte_mask(p < 0 ? -p : 0, p + 4 > (int)L ? (int)L - p : 4);
-                __hip_atomic_fetch_or(gd + w, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                lds_or(gd + w, val & msk);
             }
         }
         wave_lds_fence();
@@ -876,7 +887,7 @@ __device__ __forceinline__ void utf8_place(const unsigned* sg, unsigned* gd, int
         const unsigned lo = sg[sw < 0 ? 0 : sw], hi = sg[sw + 1];
         const unsigned val = __builtin_amdgcn_alignbyte(hi, lo, (unsigned)sb & 3u);
         const unsigned msk = byte_mask(p < 0 ? -p : 0, p + 4 > L ? L - p : 4);
-        __hip_atomic_fetch_or(gd + w, val & msk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        lds_or(gd + w, val & msk);
     };
     edge(wf);
     if (wl != wf) edge(wl);
@@ -1052,18 +1063,20 @@ __device__ __forceinline__ void utf8_image_store16(const uint4* im, u8* w0, int 
     }
 }
 
-__device__ __forceinline__ void utf8_span(u64 m, int s, int e, i64 sm, i64& c0, int& nch) {
+// (i32 offsets: the chunk offset, >= -15, fits an int -- 8 SGPRs fewer
+// for a tile's spans than i64)
+__device__ __forceinline__ void utf8_span(u64 m, int s, int e, int sm, int& c0, int& nch) {
     const int fl = __builtin_ctzll(m), ll = 63 - __builtin_clzll(m);
-    const i64 s0 = __builtin_amdgcn_readlane(s, fl), s1 = __builtin_amdgcn_readlane(e, ll);
-    c0 = ((s0 + sm) & ~15ll) - sm;  // offset of the 16-byte chunk holding byte s0, from src
-    nch = s1 > s0 ? (int)(((s1 - 1 - c0) >> 4)) + 1 : 0;
+    const int s0 = __builtin_amdgcn_readlane(s, fl), s1 = __builtin_amdgcn_readlane(e, ll);
+    c0 = (int)((((i64)s0 + sm) & ~15ll) - sm);  // offset of the 16-byte chunk holding byte s0, from src
+    nch = s1 > s0 ? (int)((((i64)s1 - 1 - c0) >> 4)) + 1 : 0;
 }
 
 // Every slice's source span (scalars): chunk offset from src and count.
 template <int K>
 __device__ __forceinline__ void utf8_spans(const u8* src, const u64 (&wm)[K], const int (&s)[K], const int (&nx)[K],
-                                           int lane, i64 (&cs)[K], int (&cn)[K]) {
-    const i64 sm = (i64)((u64)src & 15u);
+                                           int lane, int (&cs)[K], int (&cn)[K]) {
+    const int sm = (int)((u64)src & 15u);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         cs[k] = 0;
@@ -1076,7 +1089,7 @@ __device__ __forceinline__ void utf8_spans(const u8* src, const u64 (&wm)[K], co
 // arena (direct global->LDS loads, no wait); returns the last slice covered
 // (slices whose span exceeds kStageChunks are copied per lane, not staged).
 template <int K, int ARENA>
-__device__ __forceinline__ int utf8_stage_group(const u8* src, const u64 (&wm)[K], const i64 (&cs)[K],
+__device__ __forceinline__ int utf8_stage_group(const u8* src, const u64 (&wm)[K], const int (&cs)[K],
                                                 const int (&cn)[K], int k, uint4* arena, int lane,
                                                 int scap = kStageChunks) {
     int staged_to = k - 1, used = 0;
@@ -1108,7 +1121,7 @@ __device__ __forceinline__ int utf8_gather_prestage(const Args& A, int u, const 
                                                     const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane) {
     static_assert(CAP <= ARENA, "staging capacity within the arena");
     const u8* src = A.bytes[u];
-    i64 cs[K];
+    int cs[K];
     int cn[K];
     utf8_spans<K>(src, wm, s, nx, lane, cs, cn);
     int k0 = -1;
@@ -1143,7 +1156,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     unsigned* gd = (unsigned*)G.dst;
     int staged_to = pre;  // slices <= staged_to are in the arena (or need no staging)
     int aoff = 0;         // arena chunk of the next staged slice to process
-    i64 cs[K];
+    int cs[K];
     int cn[K];
     utf8_spans<K>(src, wm, s, nx, lane, cs, cn);
     // diagnostics (`prof`, compiled in by DFMI_GATHER_PHASES, and mode bit 5):
