@@ -771,9 +771,24 @@ __device__ __forceinline__ void wave_lds_fence() {
 // every LDS atomic after direct global->LDS loads -- which also waits for
 // the global stores issued since (the previous slice's image and offsets).
 // A wave's LDS operations execute in order: later reads of p see the result.
+// The same holds for plain LDS stores issued after global stores (each
+// would wait for them): the LDS image's writes all go through these.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(__attribute__((address_space(3))) const void*)p;
+}
 __device__ __forceinline__ void lds_or(unsigned* p, unsigned v) {
-    const unsigned la = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned*)p;
-    asm volatile("ds_or_b32 %0, %1" ::"v"(la), "v"(v) : "memory");
+    asm volatile("ds_or_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st32(unsigned* p, unsigned v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st32x2(unsigned* p, unsigned v0, unsigned v1) {  // p[0], p[1]
+    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(lds_addr(p)), "v"(v0), "v"(v1) : "memory");
+}
+__device__ __forceinline__ void lds_zero128(uint4* p) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(z) : "memory");
 }
 
 // Bytes [lo, hi) of a word as a mask (0 <= lo < hi <= 4).
@@ -897,13 +912,12 @@ __device__ __forceinline__ void utf8_place(const unsigned* sg, unsigned* gd, int
         const int sw = sb >> 2;
         const unsigned sh = (unsigned)sb & 3u;
         const unsigned x0 = sg[sw], x1 = sg[sw + 1], x2 = sg[sw + 2];
-        gd[w] = __builtin_amdgcn_alignbyte(x1, x0, sh);
-        gd[w + 1] = __builtin_amdgcn_alignbyte(x2, x1, sh);
+        lds_st32x2(gd + w, __builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
     }
     if (w < wl) {
         const int sb = 4 * w + delta;
         const int sw = sb >> 2;
-        gd[w] = __builtin_amdgcn_alignbyte(sg[sw + 1], sg[sw], (unsigned)sb & 3u);
+        lds_st32(gd + w, __builtin_amdgcn_alignbyte(sg[sw + 1], sg[sw], (unsigned)sb & 3u));
     }
 }
 
@@ -1040,11 +1054,17 @@ __device__ __forceinline__ void utf8_emit_slice_mk(const unsigned* sg, int* tab,
 // words of the first and last chunk when they are partial -- shared with
 // the neighbouring slices' outputs, written whole words or bytes inside
 // [sh, sh + Ls) only.
-__device__ __forceinline__ void utf8_image_store16(const uint4* im, u8* w0, int sh, int Ls, int lane) {
+// The image is zero again afterwards (every word the slice placed is read
+// here and zeroed behind the read), so the next slice places without a
+// zeroing pass.
+__device__ __forceinline__ void utf8_image_store16(uint4* im, u8* w0, int sh, int Ls, int lane) {
     const int e = sh + Ls;
     const int cf = (sh + 15) >> 4;  // first whole chunk
     const int cl = e >> 4;          // one past the last whole chunk
-    for (int c = cf + lane; c < cl; c += 64) *at<uint4>(w0, 16 * c) = im[c];
+    for (int c = cf + lane; c < cl; c += 64) {
+        *at<uint4>(w0, 16 * c) = im[c];
+        lds_zero128(im + c);
+    }
     // partial chunks: the first (sh > 0, or the slice ends inside it) and the last
     const int pf = (sh & 15) || cl < cf ? 0 : -1;
     const int pl = (e & 15) && (e >> 4) != pf ? (e >> 4) : -1;
@@ -1053,11 +1073,14 @@ __device__ __forceinline__ void utf8_image_store16(const uint4* im, u8* w0, int 
         if (c >= 0) {
             const int w = 4 * c + (lane & 3);  // image word
             const int lo = max(4 * w, sh), hi = min(4 * w + 4, e);
+            const unsigned v = ((const unsigned*)im)[w];
+            lds_st32((unsigned*)im + w, 0u);
             if (hi - lo == 4) {
-                *at<unsigned>(w0, 4 * w) = ((const unsigned*)im)[w];
+                *at<unsigned>(w0, 4 * w) = v;
             } else if (hi > lo) {
-                const unsigned v = ((const unsigned*)im)[w];
-                for (int b = lo; b < hi; ++b) w0[b] = (u8)(v >> (8 * (b & 3)));
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (4 * w + b >= lo && 4 * w + b < hi) w0[4 * w + b] = (u8)(v >> (8 * b));
             }
         }
     }
@@ -1219,6 +1242,8 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         since += 2;
         pend = false;
     };
+    if (emit == 4)
+        for (int c = lane; c < DST; c += 64) lds_zero128(G.dst + c);
     if (pre >= 0) {
         if (dbuf) {
             next_to = pre;  // prestaged into half 0 (cur ^ 1)
@@ -1324,8 +1349,10 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             continue;
         }
         tick(1);
-        for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
-        wave_lds_fence();
+        if (emit != 4) {  // emit 4: the image is zero (zeroed at the start, and behind each slice's stores)
+            for (int c = lane; 4 * c < nw; c += 64) G.dst[c] = make_uint4(0u, 0u, 0u, 0u);
+            wave_lds_fence();
+        }
         tick(2);
         if (L) utf8_place(gs + 4 * my_off, gd, (int)(s[k] - c0), sh + (int)rel, (int)L);
         wave_lds_fence();
