@@ -320,8 +320,10 @@ void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const df
     const size_t nload = X.num_cols.size();
     X.BLOCK = 512;
     X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
-    if (getenv("DFMI_DIAG"))
-        if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);  // diagnostics only
+    if (getenv("DFMI_DIAG")) {  // diagnostics only
+        if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);
+        if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
+    }
     if (X.K < 1 || X.K > 32) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
     B.n_tiles = (n + tile_rows - 1) / tile_rows;

@@ -242,6 +242,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_GATHER_PHASES")) X.gather_phases = atoi(e) & 1;
         if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 6;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         if (const char* e = getenv("DFMI_OUT_SLICES")) X.KO = atoi(e);

@@ -529,9 +529,12 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
     if (P.pred) {
         g.filtered_cols = false;
+        // proj_dense: argument-only columns loaded for every row, in the
+        // predicate's memory round trip
+        if (X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", nullptr, false);
         emit_predicate(g, o, P, X, "", {});
         // argument-only columns, loaded only where selected
-        emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+        if (!X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
     } else {
         o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) selm |= (unsigned)(base + k * BLOCK "
              "+ tid < A.n_rows) << k;\n";
@@ -610,8 +613,9 @@ static void generate_agg_grouped(Gen& g, std::ostringstream& o, const Plan& P, L
     o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
     if (P.pred) {
         g.filtered_cols = false;
+        if (X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", nullptr, false);
         emit_predicate(g, o, P, X, "", {});
-        emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+        if (!X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
     } else {
         o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) selm |= (unsigned)(base + k * BLOCK "
              "+ tid < A.n_rows) << k;\n";
@@ -742,9 +746,11 @@ std::string generate(const Plan& P, Launch& X) {
         // loads (unless late), the selection ballots wm and counts cnt.
         auto emit_select = [&]() {
             g.filtered_cols = false;
+            const bool dense = X.proj_dense && !X.late_proj && X.M == 1;
+            if (dense) emit_loads(o, X.proj_slots, X, "", "base", nullptr, false);
             emit_predicate(g, o, P, X, "", utf8_out_cols);
             // projection-only columns, loaded only where selected
-            if (!X.late_proj && X.M == 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            if (!dense && !X.late_proj && X.M == 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
             // compaction offsets (rows + Utf8 bytes)
             o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
               << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
@@ -1082,7 +1088,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -64,6 +64,7 @@ struct Launch {
     // (64 cost ~9% of the C2 kernel in polling traffic)
     int window = 8;
     int late_proj = 0;  // projection-only columns loaded after the look-back (byte-light predicates)
+    int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their
     // selection ballots (LDS), then one scan + look-back for all of them and

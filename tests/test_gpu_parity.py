@@ -385,6 +385,7 @@ def test_utf8_gather_variants(monkeypatch, variant):
     look-back; d: double-buffered staging; q: slices' images in pairs; w: the
     image stored in 16-byte chunks) against
     the oracle on the Utf8 parity cases above."""
+    plain = variant in ("3", "4")  # the defaults' multi-channel case runs for these (suffixed: diagnostics)
     if variant.endswith("p"):
         monkeypatch.setenv("DFMI_UTF8_PRESTAGE", "1")
         variant = variant[:-1]
@@ -401,8 +402,8 @@ def test_utf8_gather_variants(monkeypatch, variant):
     monkeypatch.setenv("DFMI_UTF8_GATHER", variant)
     test_utf8_gather_and_equality()
     test_utf8_many_tiles()
-    if variant in ("3", "4") or os.environ.get("DFMI_UTF8_PAIRS"):  # 0 is the per-lane fallback; the others
-        test_utf8_multi_channel_many_tiles()                              # differ only in staging / emitting
+    if plain or os.environ.get("DFMI_UTF8_PAIRS"):  # 0 is the per-lane fallback; the others
+        test_utf8_multi_channel_many_tiles()           # differ only in staging / emitting
 
 
 @pytest.mark.parametrize("m", ["1", "3", "8s0", "8pf"])
