@@ -218,13 +218,13 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         X.gather = 4;
         if (!X.utf8_outs.empty() && pred) {
             // latency-bound gather: a 2 KiB staging arena per wave and a soft
-            // occupancy hint -- 8 waves/SIMD in 512-thread blocks took the C3
-            // gather 1.45 -> 1.36 ms per 1.25e8-row batch; 7 waves/SIMD in
-            // 256-thread blocks (72 VGPRs, 7 blocks/CU) 1.23 -> 1.165 ms on the
-            // code since (register pressure binds at 64 VGPRs)
+            // 8-waves/SIMD hint (4 blocks/CU: LDS 34 KiB, 64 VGPRs) -- C3 gather
+            // 1.45 -> 1.36 ms per 1.25e8-row batch. 256-thread
+            // blocks at 7 waves/SIMD measured 5% faster (DFMI_BLOCK=256
+            // DFMI_WAVES_PER_EU=7 under DFMI_DIAG) but are not yet the default:
+            // parity suite and profile pending on the GPU
             X.arena = 128;
-            X.BLOCK = 256;
-            X.waves_per_eu = 7;
+            X.waves_per_eu = 8;
             X.waves_soft = true;
         }
     }
