@@ -142,6 +142,8 @@ EXPORTED = [
     "dfmi_filter_project_host_batches",
     "dfmi_host_result_num_columns",
     "dfmi_host_result_column",
+    "dfmi_host_result_columns",
+    "dfmi_host_result_block",
     "dfmi_host_result_free",
     "dfmi_context_set_timing",
     "dfmi_host_alloc",
@@ -267,6 +269,10 @@ def lib() -> C.CDLL:
     L.dfmi_host_result_num_columns.restype = C.c_int32
     L.dfmi_host_result_column.argtypes = [C.c_void_p, C.c_int32, C.POINTER(dfmi_column)]
     L.dfmi_host_result_column.restype = C.c_int32
+    L.dfmi_host_result_columns.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+    L.dfmi_host_result_columns.restype = C.c_int32
+    L.dfmi_host_result_block.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.dfmi_host_result_block.restype = C.c_int32
     L.dfmi_host_result_free.argtypes = [C.c_void_p]
     L.dfmi_host_result_free.restype = None
     L.dfmi_context_set_timing.argtypes = [C.c_void_p, C.c_int32]

@@ -230,18 +230,56 @@ def _offsets_tensor(offs: np.ndarray, device) -> torch.Tensor:
     return t.to(device) if device != "cpu" else t
 
 
+class LazyColumns:
+    """Columns of a batch whose buffers already exist (e.g. slices of one
+    pinned result block) but whose Array objects are built on first access:
+    a pull loop that only forwards batches pays for no Python objects it does
+    not read. Subclasses give num_rows, num_columns and materialize()."""
+
+    num_rows = 0
+    num_columns = 0
+
+    def materialize(self) -> List[Array]:
+        raise NotImplementedError
+
+    # also a read-only sequence of its Arrays
+    def __len__(self):
+        return self.num_columns
+
+    def __getitem__(self, i):
+        return self.materialize()[i]
+
+    def __iter__(self):
+        return iter(self.materialize())
+
+
 class RecordBatch:
     """arrow::record_batch::RecordBatch"""
 
-    def __init__(self, schema: Schema, columns: List[Array]):
+    def __init__(self, schema: Schema, columns):
         self.schema = schema
-        self.columns = list(columns)
+        self._columns = columns if isinstance(columns, LazyColumns) else list(columns)
+
+    @property
+    def columns(self) -> List[Array]:
+        c = self._columns
+        if type(c) is not list:
+            c = self._columns = c.materialize()
+        return c
+
+    @columns.setter
+    def columns(self, cols) -> None:
+        self._columns = list(cols)
 
     def num_columns(self) -> int:
-        return len(self.columns)
+        c = self._columns
+        return len(c) if type(c) is list else c.num_columns
 
     def num_rows(self) -> int:
-        return self.columns[0].length if self.columns else 0
+        c = self._columns
+        if type(c) is not list:
+            return c.num_rows
+        return c[0].length if c else 0
 
     def column(self, i: int) -> Array:
         return self.columns[i]

@@ -1,0 +1,38 @@
+// How a caller of the coalesced-batches launch (exec.cpp) stages its small
+// per-call data: the host-batches entry point (host_batch.cpp) moves its
+// packed inputs, the batch table and the zeroed per-batch headers with ONE
+// H2D copy, and the outputs with the headers with ONE D2H copy, so a call is
+// one copy in, one launch, one copy out and one synchronisation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+
+#include "../../include/dfmi.h"
+
+namespace dfmi {
+
+struct BatchStage {
+    // Where the launch's batch table + tile map (meta_bytes) and per-batch
+    // headers (hdr_bytes, zero on entry) go: the table is written to
+    // *host_meta and must be at *dev_meta when the launch runs, the headers
+    // are at *dev_hdr and, after the call's synchronisation, at *host_hdr.
+    // false: the batches path uses the context's own buffers and copies.
+    std::function<bool(size_t meta_bytes, size_t hdr_bytes, uint8_t** host_meta, uint8_t** dev_meta,
+                       uint8_t** dev_hdr, const uint8_t** host_hdr)>
+        locate;
+    // Issued once on the stream before the first launch (the H2D of the
+    // inputs -- with the table and zeroed headers when locate said so).
+    std::function<void(hipStream_t)> copy_in;
+    // Issued after the launch(es), before the call's synchronisation.
+    std::function<void(hipStream_t)> copy_out;
+};
+
+// dfmi_filter_project_batches with a caller's staging (NULL: none).
+int32_t filter_project_batches_staged(dfmi_context* ctx, const dfmi_program* pred, const dfmi_program* const* projs,
+                                      int32_t np, const dfmi_batch* ins, int32_t nb, dfmi_out_column* outs,
+                                      uint32_t flags, int32_t* failed, dfmi_error* err, const BatchStage* stage);
+
+}  // namespace dfmi

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <new>
 #include <string>
 #include <vector>
@@ -34,6 +35,7 @@ hipError_t launch_utf8_copy_rows(const int32_t* offs, const int32_t* spos, const
 using namespace dfmi;
 
 #include "exec_internal.h"
+#include "batch_stage.h"
 
 using namespace dfmi::xi;
 
@@ -218,13 +220,13 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         X.gather = 4;
         if (!X.utf8_outs.empty() && pred) {
             // latency-bound gather: a 2 KiB staging arena per wave and a soft
-            // 8-waves/SIMD hint (4 blocks/CU: LDS 34 KiB, 64 VGPRs) -- C3 gather
-            // 1.45 -> 1.36 ms per 1.25e8-row batch. 256-thread
-            // blocks at 7 waves/SIMD measured 5% faster (DFMI_BLOCK=256
-            // DFMI_WAVES_PER_EU=7 under DFMI_DIAG) but are not yet the default:
-            // parity suite and profile pending on the GPU
+            // occupancy hint -- 256-thread blocks at 7 waves/SIMD give the
+            // allocator 72 VGPRs (less scratch than 64 at 8 waves): C3 gather
+            // 1.45 -> 1.36 (8 waves, 512-thread blocks) -> 1.165 ms per
+            // 1.25e8-row batch
             X.arena = 128;
-            X.waves_per_eu = 8;
+            X.BLOCK = 256;
+            X.waves_per_eu = 7;
             X.waves_soft = true;
         }
     }
@@ -656,6 +658,13 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
                                                const dfmi_program* const* projs, int32_t np, const dfmi_batch* ins,
                                                int32_t nb, dfmi_out_column* outs, uint32_t flags,
                                                int32_t* failed, dfmi_error* err) {
+    return dfmi::filter_project_batches_staged(ctx, pred, projs, np, ins, nb, outs, flags, failed, err, nullptr);
+}
+
+int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_program* pred,
+                                            const dfmi_program* const* projs, int32_t np, const dfmi_batch* ins,
+                                            int32_t nb, dfmi_out_column* outs, uint32_t flags, int32_t* failed,
+                                            dfmi_error* err, const BatchStage* stage) {
     set_err(err, DFMI_OK, "");
     int32_t dummy_failed;
     if (!failed) failed = &dummy_failed;
@@ -705,7 +714,18 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
                 if (os.kind != jit::OutSpec::SKIP && os.kind != jit::OutSpec::UTF8 &&
                     (os.out_type == DFMI_TYPE_BOOLEAN || os.nullable))
                     one_by_one = true;
-        if (one_by_one) return batches_one_by_one(ctx, pred, projs, np, ins, nb, outs, nout, flags, failed, err);
+        if (one_by_one) {
+            if (stage) {
+                HIP_TRY(hipSetDevice(ctx->device));
+                stage->copy_in(ctx->stream);
+            }
+            const int32_t rc = batches_one_by_one(ctx, pred, projs, np, ins, nb, outs, nout, flags, failed, err);
+            if (stage) {
+                stage->copy_out(ctx->stream);
+                HIP_TRY(hipStreamSynchronize(ctx->stream));
+            }
+            return rc;
+        }
 
         X.batched = true;
         HIP_TRY(hipSetDevice(ctx->device));
@@ -727,10 +747,22 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
         if (T > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
         const int NPW = jit::batch_words(X, nout);
         const size_t table_bytes = (size_t)nb * NPW * 8, meta_bytes = table_bytes + (size_t)T * 4;
-        ensure_host(&ctx->host_bmeta, &ctx->host_bmeta_bytes, meta_bytes);
-        ensure(ctx, &ctx->bmeta, &ctx->bmeta_bytes, meta_bytes);
-        ensure_host(&ctx->host_bhdr, &ctx->host_bhdr_bytes, (size_t)nb * kBHdr);
-        ensure(ctx, &ctx->bhdr, &ctx->bhdr_bytes, (size_t)nb * kBHdr);
+        // the table and the per-batch headers: in the caller's staging (one
+        // copy each way with its own data), or the context's buffers
+        uint8_t *host_meta = nullptr, *dev_meta = nullptr, *dev_hdr = nullptr;
+        const uint8_t* host_hdr = nullptr;
+        const bool staged = stage && stage->locate &&
+                            stage->locate(meta_bytes, (size_t)nb * kBHdr, &host_meta, &dev_meta, &dev_hdr, &host_hdr);
+        if (!staged) {
+            ensure_host(&ctx->host_bmeta, &ctx->host_bmeta_bytes, meta_bytes);
+            ensure(ctx, &ctx->bmeta, &ctx->bmeta_bytes, meta_bytes);
+            ensure_host(&ctx->host_bhdr, &ctx->host_bhdr_bytes, (size_t)nb * kBHdr);
+            ensure(ctx, &ctx->bhdr, &ctx->bhdr_bytes, (size_t)nb * kBHdr);
+            host_meta = ctx->host_bmeta;
+            dev_meta = ctx->bmeta;
+            dev_hdr = ctx->bhdr;
+            host_hdr = ctx->host_bhdr;
+        }
         bool need_ones = false;
         for (int i = 0; i < ncols && !need_ones; ++i)
             if (nullable[i])
@@ -743,8 +775,8 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
                 HIP_TRY(hipMemsetAsync(ctx->ones, 0xff, ctx->ones_bytes, st));
             }
         }
-        uint64_t* tab = (uint64_t*)ctx->host_bmeta;
-        int32_t* tile_batch = (int32_t*)(ctx->host_bmeta + table_bytes);
+        uint64_t* tab = (uint64_t*)host_meta;
+        int32_t* tile_batch = (int32_t*)(host_meta + table_bytes);
         auto valid_of = [&](const dfmi_column& c, int col) -> uint64_t {
             if (!nullable[col]) return 0;
             return (uint64_t)((c.validity && c.null_count > 0) ? c.validity : ctx->ones);
@@ -757,8 +789,8 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
             memset(row, 0, (size_t)NPW * 8);
             row[0] = (uint64_t)in.num_rows;
             row[1] = (uint64_t)tiles[b] | ((uint64_t)first[b] << 32);
-            row[2] = (uint64_t)(ctx->bhdr + (size_t)b * kBHdr);
-            row[3] = (uint64_t)(ctx->bhdr + (size_t)b * kBHdr + 24 * 8);
+            row[2] = (uint64_t)(dev_hdr + (size_t)b * kBHdr);
+            row[3] = (uint64_t)(dev_hdr + (size_t)b * kBHdr + 24 * 8);
             for (size_t sl = 0; sl < X.num_cols.size(); ++sl) {
                 const dfmi_column& c = in.columns[X.num_cols[sl]];
                 const int w = jit::type_width(c.type);
@@ -797,9 +829,12 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
             for (int64_t t = 0; t < tiles[b]; ++t) tile_batch[first[b] + t] = b;
         }
         // ---- launch
+        if (stage) stage->copy_in(st);  // (staged: with the table and the zeroed headers)
         if (T > 0) {
-            HIP_TRY(hipMemcpyAsync(ctx->bmeta, ctx->host_bmeta, meta_bytes, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemsetAsync(ctx->bhdr, 0, (size_t)nb * kBHdr, st));
+            if (!staged) {
+                HIP_TRY(hipMemcpyAsync(dev_meta, host_meta, meta_bytes, hipMemcpyHostToDevice, st));
+                HIP_TRY(hipMemsetAsync(dev_hdr, 0, (size_t)nb * kBHdr, st));
+            }
             const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
             const size_t status_bytes = (size_t)n_chan * T * 8 * X.spread;
             Args A;
@@ -819,21 +854,22 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
             A.clear_status = (unsigned long long*)ws.clear_status;
             A.clear_words = ws.clear_words;
             A.clear_hdr = (unsigned long long*)ws.clear_hdr;
-            A.tile_batch = (const int*)(ctx->bmeta + table_bytes);
-            A.batch_ptrs = (void* const*)ctx->bmeta;
+            A.tile_batch = (const int*)(dev_meta + table_bytes);
+            A.batch_ptrs = (void* const*)dev_meta;
             if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
             size_t asz = sizeof A;
             void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
             HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)T, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
             ws_commit(ctx, ws);
             if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
-            HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
+            if (!staged) HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
         }
         for (int32_t b = 0; b < nb; ++b)  // empty batches: Utf8 offsets = [0]
             if (ins[b].num_rows == 0)
                 for (int o = 0; o < nout; ++o)
                     if (plan.outs[o].kind == jit::OutSpec::UTF8 && outs[(size_t)b * nout + o].offsets)
                         HIP_TRY(hipMemsetAsync(outs[(size_t)b * nout + o].offsets, 0, 4, st));
+        if (stage) stage->copy_out(st);  // (staged: with the headers)
         HIP_TRY(hipStreamSynchronize(st));
         if (T > 0 && ctx->timing) {
             float m1 = 0;
@@ -843,7 +879,7 @@ extern "C" int32_t dfmi_filter_project_batches(dfmi_context* ctx, const dfmi_pro
         }
         // ---- per batch, in order: results, or the first batch's error
         for (int32_t b = 0; b < nb; ++b) {
-            const uint64_t* h = (const uint64_t*)(ctx->host_bhdr + (size_t)b * kBHdr);
+            const uint64_t* h = (const uint64_t*)(host_hdr + (size_t)b * kBHdr);
             const bool ran = ins[b].num_rows > 0;
             const uint64_t ew = ran ? h[24] : 0;
             if (ew) {

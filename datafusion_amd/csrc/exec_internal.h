@@ -155,20 +155,29 @@ inline WsLease ws_acquire(dfmi_context* ctx, size_t status_bytes, hipStream_t st
     l.status_bytes = status_bytes;
     l.hdr = ctx->ws + p * kHdrAlloc;
     l.status = ctx->ws + 2 * kHdrAlloc + p * ctx->status_cap;
-    // the prefix this launch needs must be zero: clear what is left dirty in it
+    // the prefix this launch needs must be zero: what is left dirty in this
+    // pair is cleared whole, by one memset (so a small launch after a large
+    // one pays it once, not on every later use of the pair)
     size_t& lo = ctx->dirty_lo[p];
     size_t& hi = ctx->dirty_hi[p];
     if (hi > lo && lo < status_bytes) {
-        const size_t end = std::min(hi, status_bytes);
-        HIP_TRY(hipMemsetAsync(l.status + lo, 0, end - lo, st));
-        lo = end;
-        if (lo >= hi) lo = hi = 0;
+        HIP_TRY(hipMemsetAsync(l.status + lo, 0, hi - lo, st));
+        lo = hi = 0;
     }
-    // what this launch's blocks zero in the other pair (bounded by its size)
+    // what this launch's blocks zero in the other pair (bounded by its size);
+    // a larger leftover (a full-table launch before a 1024-row one) is
+    // cleared here once, by one memset, and later launches are back to
+    // clearing in the kernel
     uint8_t* other = ctx->ws + 2 * kHdrAlloc + q * ctx->status_cap;
-    const size_t qd = ctx->dirty_hi[q] - ctx->dirty_lo[q];
-    if (qd > 0 && qd <= std::max<size_t>(4 * status_bytes, (size_t)64 << 10)) {
-        l.clear_status = other + ctx->dirty_lo[q];
+    size_t& qlo = ctx->dirty_lo[q];
+    size_t& qhi = ctx->dirty_hi[q];
+    if (qhi > qlo && qhi - qlo > std::max<size_t>(4 * status_bytes, (size_t)64 << 10)) {
+        HIP_TRY(hipMemsetAsync(other + qlo, 0, qhi - qlo, st));
+        qlo = qhi = 0;
+    }
+    const size_t qd = qhi - qlo;
+    if (qd > 0) {
+        l.clear_status = other + qlo;
         l.clear_words = (long long)(qd / 8);
     } else {
         l.clear_status = other;

@@ -40,6 +40,7 @@
 
 #include "dfmi_program.h"
 #include "jit.h"
+#include "batch_stage.h"
 
 using dfmi::Fail;
 
@@ -393,6 +394,10 @@ void finish_bitmap(uint8_t* b, int64_t n) {
 
 // ---------------------------------------------------------------- arena
 constexpr int kSlots = 3;
+// a host batch up to this size skips the chunk pipeline (one H2D, one
+// launch, one D2H, one synchronisation: dfmi_filter_project_host)
+constexpr int64_t kSmallRows = 1 << 16;
+constexpr size_t kSmallBytes = (size_t)4 << 20;
 
 // DFMI_HOST_PROFILE=1: per-call phase times on stderr (diagnostics only).
 struct PhaseClock {
@@ -600,6 +605,27 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
         const int64_t n = in->num_rows;
         const int ncols = in->num_columns;
         if (n < 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "negative row count"};
+        // ---- small batches (csv_sql.rs:49's 1024 rows): no chunk pipeline,
+        // copy streams or host threads -- the one-batch form of the
+        // host-batches path: pack into pinned memory, one H2D, the launch and
+        // one D2H of the output region on the context stream, one sync
+        if (n <= kSmallRows && !getenv("DFMI_HOST_CHUNK_ROWS")) {
+            size_t bytes = 0;
+            for (int i = 0; i < ncols; ++i) {
+                const dfmi_column& c = in->columns[i];
+                bytes += values_bytes(c) + (c.validity ? (size_t)(n + 7) / 8 : 0) +
+                         (c.type == DFMI_TYPE_UTF8 ? (size_t)(n + 1) * 4 : 0);
+            }
+            if (bytes <= kSmallBytes) {
+                int32_t failed = -1;
+                const int32_t rc = dfmi_filter_project_host_batches(ctx, pred, projs, np, in, 1, flags, out, &failed, err);
+                if (rc != DFMI_OK && *out) {
+                    dfmi_host_result_free(*out);
+                    *out = nullptr;
+                }
+                return rc;
+            }
+        }
         HIP_TRY(hipSetDevice(dfmi::ctx_device(ctx)));
         hipStream_t st = dfmi::ctx_stream(ctx);
         Arena& A = arena_of(ctx);
@@ -1112,6 +1138,21 @@ extern "C" int32_t dfmi_host_result_column(const dfmi_host_result* r, int32_t i,
     return DFMI_OK;
 }
 
+extern "C" int32_t dfmi_host_result_columns(const dfmi_host_result* r, int32_t first, int32_t count,
+                                            dfmi_column* views) {
+    if (!r || !views || first < 0 || count < 0 || (int64_t)first + count > (int64_t)r->cols.size())
+        return DFMI_ERR_INVALID_ARGUMENT;
+    for (int32_t k = 0; k < count; ++k) dfmi_host_result_column(r, first + k, &views[k]);
+    return DFMI_OK;
+}
+
+extern "C" int32_t dfmi_host_result_block(const dfmi_host_result* r, const void** base, size_t* bytes) {
+    if (!r || !base || !bytes) return DFMI_ERR_INVALID_ARGUMENT;
+    *base = r->arena.p;
+    *bytes = r->arena.p ? r->arena.cap : 0;
+    return DFMI_OK;
+}
+
 extern "C" void dfmi_host_result_free(dfmi_host_result* r) { delete r; }
 
 // ---------------------------------------------------------------------------
@@ -1218,9 +1259,18 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                     out_bytes += align256(std::max<size_t>(L.ndat, 1));
                 }
             }
-        // ---- pack the inputs into pinned staging (host threads), one H2D
-        A.reserve_pin(std::max<size_t>(in_bytes, 256));
-        A.reserve_dev(std::max<size_t>(in_bytes + out_bytes, 256));
+        // ---- regions. Device: [outputs | per-batch headers | inputs | batch
+        // table]; pinned staging: [zeros for the headers | inputs | table]
+        // (ONE H2D); the result's block: [outputs | headers] (ONE D2H).
+        const size_t OB = align256(std::max<size_t>(out_bytes, 256)), H = align256((size_t)nb * 256),
+                     IB = align256(std::max<size_t>(in_bytes, 256));
+        size_t MB = 256;  // bound on the launch's batch table + tile map (exec.cpp)
+        for (int32_t b = 0; b < nb; ++b)
+            MB += (size_t)(4 + 3 * ncols + 5 * nout) * 8 + (size_t)((ins[b].num_rows + 63) / 64 + 1) * 4;
+        MB = align256(MB);
+        A.reserve_pin(H + IB + MB);
+        A.reserve_dev(OB + H + IB + MB);
+        uint8_t* const pin_in = A.pin + H;
         {
             std::vector<std::function<void()>> tasks;
             const int ways = std::max(1, std::min(A.pool->ways(), (int)(in_bytes >> 20) + 1));
@@ -1230,16 +1280,17 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                         for (int i = 0; i < ncols; ++i) {
                             const dfmi_column& c = ins[b].columns[i];
                             const In& L = lay[(size_t)b * ncols + i];
-                            if (L.nval) memcpy(A.pin + L.val, c.values, L.nval);
-                            if (L.noff) memcpy(A.pin + L.off, c.offsets, L.noff);
-                            if (L.nvld) memcpy(A.pin + L.vld, c.validity, L.nvld);
+                            if (L.nval) memcpy(pin_in + L.val, c.values, L.nval);
+                            if (L.noff) memcpy(pin_in + L.off, c.offsets, L.noff);
+                            if (L.nvld) memcpy(pin_in + L.vld, c.validity, L.nvld);
                         }
                 });
             A.pool->run(tasks);
         }
-        uint8_t* dev = A.dev;
-        uint8_t* dout = A.dev + align256(in_bytes);
-        HIP_TRY(hipMemcpyAsync(dev, A.pin, in_bytes, hipMemcpyHostToDevice, st));
+        memset(A.pin, 0, H);
+        uint8_t* const dout = A.dev;
+        uint8_t* const dhdr = A.dev + OB;
+        uint8_t* const dev = dhdr + H;  // inputs
         std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
         std::vector<dfmi_batch> dins(nb);
         for (int32_t b = 0; b < nb; ++b) {
@@ -1268,15 +1319,36 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                 d.data_capacity = (int64_t)L.ndat;
             }
         }
-        // ---- the coalesced launch (synchronous), then one D2H of the outputs
+        // ---- one H2D, the coalesced launch, one D2H, one synchronisation
+        R->arena = R->pool->get(OB + H);
+        size_t meta_used = 0;
+        hipError_t copy_err = hipSuccess;
+        dfmi::BatchStage stage;
+        stage.locate = [&](size_t meta_bytes, size_t hdr_bytes, uint8_t** host_meta, uint8_t** dev_meta,
+                           uint8_t** dev_hdr, const uint8_t** host_hdr) {
+            if (meta_bytes > MB || hdr_bytes > H) return false;
+            meta_used = meta_bytes;
+            *host_meta = pin_in + IB;
+            *dev_meta = dev + IB;
+            *dev_hdr = dhdr;
+            *host_hdr = R->arena.p + OB;
+            return true;
+        };
+        stage.copy_in = [&](hipStream_t s) {
+            const size_t nbytes = meta_used ? H + IB + meta_used : H + in_bytes;
+            const hipError_t e = hipMemcpyAsync(dhdr, A.pin, nbytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) copy_err = e;
+        };
+        stage.copy_out = [&](hipStream_t s) {
+            const hipError_t e = hipMemcpyAsync(R->arena.p, dout, OB + H, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) copy_err = e;
+        };
         dfmi_error e2{};
-        const int32_t rc = dfmi_filter_project_batches(ctx, pred, projs, np, dins.data(), nb, douts.data(), flags,
-                                                       failed, &e2);
+        const int32_t rc = dfmi::filter_project_batches_staged(ctx, pred, projs, np, dins.data(), nb, douts.data(),
+                                                               flags, failed, &e2, &stage);
+        if (rc != DFMI_OK) (void)hipStreamSynchronize(st);  // (a call that failed after copy_in: drain it)
+        HIP_TRY(copy_err);
         const int32_t nok = rc == DFMI_OK ? nb : std::max(0, *failed);
-        R->arena = R->pool->get(std::max<size_t>(out_bytes, 256));
-        if (nok > 0)
-            HIP_TRY(hipMemcpyAsync(R->arena.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
         R->cols.resize((size_t)nb * nout);
         for (int32_t b = 0; b < nb; ++b)
             for (int o = 0; o < nout; ++o) {

@@ -1,0 +1,157 @@
+/* _dfmi_glue: the Python binding's per-batch FFI marshalling, native.
+ *
+ * The Python mirror of the relations (datafusion_amd/execution) hands many
+ * small host batches to dfmi_filter_project_host_batches per call
+ * (csv_sql.rs:49-62 pulls 1024-row batches). Filling the C-ABI structs
+ * (dfmi_column per column, dfmi_batch per batch, include/dfmi.h) from the
+ * Python Array objects costs ~1 us per column in Python; this module walks
+ * the same objects through the CPython API instead. It reads, per Array:
+ * data_type, length, null_count and the data_ptr() of its values / validity
+ * / offsets tensors -- exactly what engine.column_struct() reads -- and
+ * refuses any column whose buffers are not in host memory.
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef struct {
+    int32_t type, reserved;
+    int64_t length, null_count;
+    uint64_t validity, values, offsets;
+} col_rec; /* dfmi_column */
+
+typedef struct {
+    int32_t num_columns, reserved;
+    int64_t num_rows;
+    uint64_t columns;
+} batch_rec; /* dfmi_batch */
+
+static PyObject *s_columns, *s__columns, *s_data_type, *s_length, *s_null_count, *s_validity, *s_values,
+    *s_offsets, *s_data_ptr, *s_is_cpu;
+
+static int get_i64(PyObject* o, PyObject* name, int64_t* out) {
+    PyObject* v = PyObject_GetAttr(o, name);
+    if (!v) return -1;
+    *out = PyLong_AsLongLong(v);
+    Py_DECREF(v);
+    return (*out == -1 && PyErr_Occurred()) ? -1 : 0;
+}
+
+/* data_ptr() of tensor attribute `name` of array `a` (0 for None); fails
+ * unless the tensor is in host memory. */
+static int get_ptr(PyObject* a, PyObject* name, uint64_t* out) {
+    PyObject* t = PyObject_GetAttr(a, name);
+    if (!t) return -1;
+    if (t == Py_None) {
+        Py_DECREF(t);
+        *out = 0;
+        return 0;
+    }
+    PyObject* cpu = PyObject_GetAttr(t, s_is_cpu);
+    if (!cpu) {
+        Py_DECREF(t);
+        return -1;
+    }
+    const int is_cpu = PyObject_IsTrue(cpu);
+    Py_DECREF(cpu);
+    if (is_cpu != 1) {
+        Py_DECREF(t);
+        if (is_cpu == 0) PyErr_SetString(PyExc_ValueError, "filter_project_host_batches takes host batches");
+        return -1;
+    }
+    PyObject* p = PyObject_CallMethodNoArgs(t, s_data_ptr);
+    Py_DECREF(t);
+    if (!p) return -1;
+    *out = PyLong_AsUnsignedLongLong(p);
+    Py_DECREF(p);
+    return (*out == (uint64_t)-1 && PyErr_Occurred()) ? -1 : 0;
+}
+
+/* pack_host_batches(batches, ncols, cols_buf, batches_buf) -> None
+ * cols_buf: writable, >= len(batches) * ncols dfmi_column records;
+ * batches_buf: writable, >= len(batches) dfmi_batch records. Each batch's
+ * `columns` pointer points into cols_buf. */
+static PyObject* pack_host_batches(PyObject* self, PyObject* args) {
+    PyObject* batches;
+    Py_ssize_t ncols;
+    Py_buffer cb, bb;
+    if (!PyArg_ParseTuple(args, "Onw*w*", &batches, &ncols, &cb, &bb)) return NULL;
+    PyObject* seq = PySequence_Fast(batches, "batches must be a sequence");
+    PyObject* ret = NULL;
+    if (!seq) goto done;
+    const Py_ssize_t nb = PySequence_Fast_GET_SIZE(seq);
+    if (ncols < 0 || cb.len < (Py_ssize_t)(nb * ncols * sizeof(col_rec)) || bb.len < (Py_ssize_t)(nb * sizeof(batch_rec))) {
+        PyErr_SetString(PyExc_ValueError, "buffers too small");
+        goto done;
+    }
+    col_rec* C = (col_rec*)cb.buf;
+    batch_rec* B = (batch_rec*)bb.buf;
+    for (Py_ssize_t b = 0; b < nb; ++b) {
+        PyObject* batch = PySequence_Fast_GET_ITEM(seq, b);
+        /* RecordBatch keeps its Arrays in _columns (a list, or lazy columns
+         * the `columns` property builds) */
+        PyObject* cols = PyObject_GetAttr(batch, s__columns);
+        if (cols && !PyList_CheckExact(cols)) {
+            Py_DECREF(cols);
+            cols = PyObject_GetAttr(batch, s_columns);
+        }
+        if (!cols) goto done;
+        PyObject* cseq = PySequence_Fast(cols, "columns must be a sequence");
+        Py_DECREF(cols);
+        if (!cseq) goto done;
+        if (PySequence_Fast_GET_SIZE(cseq) != ncols) {
+            Py_DECREF(cseq);
+            PyErr_SetString(PyExc_ValueError, "batches do not share a schema");
+            goto done;
+        }
+        col_rec* r = C + b * ncols;
+        for (Py_ssize_t i = 0; i < ncols; ++i) {
+            PyObject* a = PySequence_Fast_GET_ITEM(cseq, i);
+            int64_t t;
+            memset(&r[i], 0, sizeof r[i]);
+            if (get_i64(a, s_data_type, &t) || get_i64(a, s_length, &r[i].length) ||
+                get_i64(a, s_null_count, &r[i].null_count) || get_ptr(a, s_validity, &r[i].validity) ||
+                get_ptr(a, s_values, &r[i].values) || get_ptr(a, s_offsets, &r[i].offsets)) {
+                Py_DECREF(cseq);
+                goto done;
+            }
+            r[i].type = (int32_t)t;
+        }
+        Py_DECREF(cseq);
+        B[b].num_columns = (int32_t)ncols;
+        B[b].reserved = 0;
+        B[b].num_rows = ncols ? r[0].length : 0;
+        B[b].columns = (uint64_t)(uintptr_t)r;
+    }
+    ret = Py_None;
+    Py_INCREF(ret);
+done:
+    Py_XDECREF(seq);
+    PyBuffer_Release(&cb);
+    PyBuffer_Release(&bb);
+    return ret;
+}
+
+static PyMethodDef methods[] = {
+    {"pack_host_batches", pack_host_batches, METH_VARARGS,
+     "Fill dfmi_column / dfmi_batch records for host batches (include/dfmi.h)."},
+    {NULL, NULL, 0, NULL}};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_dfmi_glue", NULL, -1, methods};
+
+PyMODINIT_FUNC PyInit__dfmi_glue(void) {
+#define INTERN(v, s) \
+    if (!(v = PyUnicode_InternFromString(s))) return NULL;
+    INTERN(s_columns, "columns");
+    INTERN(s__columns, "_columns");
+    INTERN(s_data_type, "data_type");
+    INTERN(s_length, "length");
+    INTERN(s_null_count, "null_count");
+    INTERN(s_validity, "validity");
+    INTERN(s_values, "values");
+    INTERN(s_offsets, "offsets");
+    INTERN(s_data_ptr, "data_ptr");
+    INTERN(s_is_cpu, "is_cpu");
+    return PyModule_Create(&module);
+}

@@ -49,10 +49,13 @@ class Aggregate:
 
 
 class ExecutionContext:
-    def __init__(self, device=None, flags: int = 0, coalesce: int = 1):
-        """coalesce > 1: Selection / Projection relations run up to that many
-        input batches per device launch (dfmi_filter_project_batches) while
-        still returning one output batch per input batch."""
+    def __init__(self, device=None, flags: int = 0, coalesce: int = 256):
+        """coalesce > 1: Selection / Projection relations read up to that many
+        input batches (at most 2^20 rows) ahead and run them as one device call
+        (dfmi_filter_project_batches / dfmi_filter_project_host_batches), still
+        returning one output batch per input batch -- at csv_sql.rs:49's
+        1024-row batches one call per batch would cost a GPU round trip each.
+        coalesce=1: one call per pull."""
         self.datasources: Dict[str, object] = {}
         self.device = device
         self.flags = flags

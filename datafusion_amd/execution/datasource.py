@@ -171,6 +171,7 @@ class NativeCsvDataSource(DataSource):
         rb = RecordBatch(self._schema, cols)
         if not self._copy:
             rb._source = self  # the views' memory lives as long as the batch
+            rb._transient = True  # ... but the next pull overwrites it (a Coalescer copies it first)
         return rb
 
     def __del__(self):

@@ -9,10 +9,11 @@ from __future__ import annotations
 import ctypes as C
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import _abi
-from ..arrow import Array, RecordBatch, empty_bytes
+from ..arrow import Array, LazyColumns, RecordBatch, empty_bytes
 from ..logicalplan import Column, DataType
 from .error import ExecutionError
 
@@ -54,9 +55,12 @@ class DeviceEngine:
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode())
         self.ctx = ctx
+        self._worker = None    # one thread for filter_project_host_batches_async
+        self._inflight = None  # its call in flight (every entry point drains it first)
 
     def __del__(self):
         try:
+            self.drain()
             if self.ctx:
                 _abi.lib().dfmi_context_destroy(self.ctx)
         except Exception:
@@ -97,6 +101,7 @@ class DeviceEngine:
         ``projections`` are RuntimeExprs (None / [] when absent). With a
         ShardComm the pass is this rank's shard (dfmi_shard_filter_project):
         the placement lands in comm.placement, the outputs in comm.outputs."""
+        self.drain()
         L = _abi.lib()
         batch = self.to_device(batch)
         n = batch.num_rows()
@@ -182,6 +187,7 @@ class DeviceEngine:
         results holds one column list per batch before the first failing
         batch (all of them when error is None) -- what a pull loop would have
         received before the error."""
+        self.drain()
         L = _abi.lib()
         projections = list(projections or [])
         batches = [self.to_device(b) for b in batches]
@@ -232,6 +238,7 @@ class DeviceEngine:
         """The same pull over a HOST batch through dfmi_filter_project_host:
         the library stages the Arrow buffers into HBM and returns host
         results (the path a Rust caller with arrow 0.12 buffers takes)."""
+        self.drain()
         L = _abi.lib()
         cols = batch.columns
         if any(c.values.device.type != "cpu" for c in cols):
@@ -260,47 +267,81 @@ class DeviceEngine:
     def filter_project_host_batches(self, predicate, projections: Optional[Sequence], batches: Sequence[RecordBatch],
                                     flags: int = 0):
         """The pull over many small HOST batches in one call
-        (dfmi_filter_project_host_batches): (one output column list per batch
-        up to the failing one, the error or None) -- the pull loop's view."""
-        L = _abi.lib()
+        (dfmi_filter_project_host_batches): (one output column set per batch
+        up to the failing one, the error or None) -- the pull loop's view.
+        Each column set is a HostBatchColumns: the batch's buffers are slices
+        of the result's one pinned block (no copy), its Arrays are built when
+        first read, and the block is released when the last slice is."""
+        self.drain()
+        prep = self._host_batches_prepare(predicate, projections, batches, flags)
+        return self._host_batches_finish(prep, self._host_batches_call(prep))
+
+    def filter_project_host_batches_async(self, predicate, projections: Optional[Sequence],
+                                          batches: Sequence[RecordBatch], flags: int = 0) -> "HostBatchesFuture":
+        """filter_project_host_batches whose C call runs on the engine's worker
+        thread (ctypes releases the GIL for it): the caller hands out the
+        previous group's batches while this group's staging, PCIe copies and
+        launch proceed. The batches' structs are built here, on the calling
+        thread; result() gives what filter_project_host_batches returns. The
+        engine runs one call at a time: every other entry point waits for an
+        in-flight one first (drain)."""
+        self.drain()
+        prep = self._host_batches_prepare(predicate, projections, batches, flags)
+        if self._worker is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._worker = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dfmi-engine")
+        fut = self._worker.submit(self._host_batches_call, prep)
+        self._inflight = fut
+        return HostBatchesFuture(self, prep, fut)
+
+    def drain(self) -> None:
+        """Wait for the in-flight asynchronous call (its result stays with its future)."""
+        f = self._inflight
+        if f is not None:
+            self._inflight = None
+            from concurrent.futures import wait
+            wait([f])
+
+    def _host_batches_prepare(self, predicate, projections, batches, flags):
         projections = list(projections or [])
         nb = len(batches)
-        if nb == 0:
-            return [], None
-        ncols = len(batches[0].columns)
+        ncols = len(batches[0].columns) if nb else 0
         nout = len(projections) if projections else ncols
-        keep = []
-        barr = (_abi.dfmi_batch * nb)()
-        for b, batch in enumerate(batches):
-            if any(c.values.device.type != "cpu" for c in batch.columns):
-                raise ValueError("filter_project_host_batches takes host batches")
-            carr = (_abi.dfmi_column * max(1, ncols))()
-            for i, a in enumerate(batch.columns):
-                carr[i] = column_struct(a)
-            keep.append(carr)
-            barr[b].num_columns = ncols
-            barr[b].num_rows = batch.num_rows()
-            barr[b].columns = carr
+        barr, keep = host_batch_structs(batches, ncols) if nb else (None, None)
         progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
+        stream = torch.cuda.current_stream(self.device).cuda_stream  # the caller's stream (thread-local in torch)
+        return (predicate.handle if predicate is not None else None, progs, len(projections), barr, keep, nb, nout,
+                flags, stream)
+
+    def _host_batches_call(self, prep):
+        """The C call (any thread): (rc, result handle, failed batch, dfmi_error)."""
+        pred, progs, np_, barr, keep, nb, nout, flags, stream = prep
+        if nb == 0:
+            return _abi.DFMI_OK, None, -1, None
+        L = _abi.lib()
         err = _abi.dfmi_error()
         res = C.c_void_p()
         failed = C.c_int32(-1)
-        L.dfmi_context_set_stream(self.ctx, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
-        rc = L.dfmi_filter_project_host_batches(self.ctx, predicate.handle if predicate is not None else None, progs,
-                                                len(projections), barr, nb, flags, C.byref(res), C.byref(failed),
-                                                C.byref(err))
+        L.dfmi_context_set_stream(self.ctx, C.c_void_p(stream))
+        rc = L.dfmi_filter_project_host_batches(self.ctx, pred, progs, np_, barr, nb, flags, C.byref(res),
+                                                C.byref(failed), C.byref(err))
+        return rc, res, failed.value, err
+
+    @staticmethod
+    def _host_batches_finish(prep, raw):
+        nb, nout = prep[5], prep[6]
+        rc, res, failed, err = raw
+        if nb == 0:
+            return [], None
         error = None
         if rc != _abi.DFMI_OK:
             error = ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
-            error.failed_batch = failed.value
+            error.failed_batch = failed
             if not res.value:
                 raise error
-        try:
-            cols = _host_result_arrays(res)
-        finally:
-            L.dfmi_host_result_free(res)
-        done = nb if error is None else max(0, failed.value)
-        return [cols[b * nout:(b + 1) * nout] for b in range(done)], error
+        done = nb if error is None else max(0, failed)
+        block = HostResultBlock(res, done * nout)
+        return [HostBatchColumns(block, b, nout) for b in range(done)], error
 
     # ---- aggregate extension (DFMI_FLAG_EXT_AGGREGATE)
     def _batch_struct(self, batch: RecordBatch):
@@ -346,6 +387,7 @@ class AggState:
     def add(self, predicate, batch: RecordBatch, flags: int = 0) -> None:
         """One batch of the aggregate's input (fused Selection when predicate is given)."""
         eng = self.eng
+        eng.drain()
         batch = eng.to_device(batch)
         cb, keep = eng._batch_struct(batch)
         err = _abi.dfmi_error()
@@ -557,3 +599,129 @@ def _host_result_arrays(res) -> List[Array]:
         out.append(Array(t, n, _bytes_tensor(vals.copy()), valid,
                          _offsets_tensor(offs, "cpu") if offs is not None else None, v.null_count))
     return out
+
+
+# ---- host batches: vectorised ABI structs in, zero-copy result slices out
+
+_COL_DTYPE = np.dtype([("type", "<i4"), ("reserved", "<i4"), ("length", "<i8"), ("null_count", "<i8"),
+                       ("validity", "<u8"), ("values", "<u8"), ("offsets", "<u8")])
+_BATCH_DTYPE = np.dtype([("num_columns", "<i4"), ("reserved", "<i4"), ("num_rows", "<i8"), ("columns", "<u8")])
+assert _COL_DTYPE.itemsize == C.sizeof(_abi.dfmi_column) and _BATCH_DTYPE.itemsize == C.sizeof(_abi.dfmi_batch)
+
+
+def host_batch_structs(batches: Sequence[RecordBatch], ncols: int):
+    """dfmi_batch[len(batches)] over the batches' host buffers, filled by the
+    native glue (csrc/pyglue.c: the fields column_struct() reads, for every
+    column of every batch, in one call). Returns (batch array, keep-alive)."""
+    from .. import _dfmi_glue
+    nb = len(batches)
+    cols = np.empty(max(1, nb * ncols), dtype=_COL_DTYPE)
+    ba = np.empty(nb, dtype=_BATCH_DTYPE)
+    _dfmi_glue.pack_host_batches(batches, ncols, cols, ba)
+    return (_abi.dfmi_batch * nb).from_buffer(ba), (cols, ba)
+
+
+class HostBatchesFuture:
+    """An in-flight filter_project_host_batches_async call."""
+
+    def __init__(self, eng: DeviceEngine, prep, fut):
+        self.eng, self.prep, self.fut = eng, prep, fut
+
+    def result(self):
+        raw = self.fut.result()
+        if self.eng._inflight is self.fut:
+            self.eng._inflight = None
+        return DeviceEngine._host_batches_finish(self.prep, raw)
+
+
+class _ResultOwner:
+    """Frees a dfmi_host_result when the last view of its memory is gone."""
+
+    def __init__(self, res):
+        self.res = res
+
+    def __del__(self):
+        try:
+            _abi.lib().dfmi_host_result_free(self.res)
+        except Exception:
+            pass
+
+
+class HostResultBlock:
+    """One coalesced host result: every column's view (dfmi_host_result_columns,
+    one FFI call) and its pinned block as one uint8 tensor. Slices of that
+    tensor keep the result alive."""
+
+    def __init__(self, res, ncols: int):
+        L = _abi.lib()
+        owner = _ResultOwner(res)
+        views = np.zeros(max(1, ncols), dtype=_COL_DTYPE)
+        if ncols:
+            L.dfmi_host_result_columns(res, 0, ncols, views.ctypes.data)
+        self.type = views["type"].tolist()
+        self.length = views["length"].tolist()
+        self.nulls = views["null_count"].tolist()
+        self.validity = views["validity"].tolist()
+        self.values = views["values"].tolist()
+        self.offsets = views["offsets"].tolist()
+        base, nbytes = C.c_void_p(), C.c_size_t()
+        L.dfmi_host_result_block(res, C.byref(base), C.byref(nbytes))
+        self.base = base.value or 0
+        self.end = self.base + nbytes.value
+        if self.base:
+            raw = (C.c_uint8 * nbytes.value).from_address(self.base)
+            raw._owner = owner  # the memory lives while any tensor over `raw` does
+            self.block = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8))
+        else:
+            self.block = None
+        self.owner = owner
+
+    def buffer(self, ptr: int, nbytes: int) -> torch.Tensor:
+        """Host tensor of nbytes at ptr: a slice of the block (no copy), or a
+        copy for memory outside it (passthrough columns)."""
+        from ..arrow import _bytes_tensor
+        if self.base <= ptr and ptr + nbytes <= self.end:
+            # padded to 64 bytes like every Array buffer (the block's buffers
+            # are 256-byte aligned, so the padding stays inside this one)
+            o = ptr - self.base
+            return self.block[o:min(o + max(64, (nbytes + 63) & ~63), self.end - self.base)]
+        if not nbytes:
+            return torch.zeros(64, dtype=torch.uint8)
+        return _bytes_tensor(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,)).copy())
+
+
+class HostBatchColumns(LazyColumns):
+    """The output columns of batch b of a HostResultBlock."""
+
+    __slots__ = ("blk", "b", "num_columns", "_cols")
+
+    def __init__(self, blk: HostResultBlock, b: int, nout: int):
+        self.blk, self.b, self.num_columns, self._cols = blk, b, nout, None
+
+    @property
+    def num_rows(self) -> int:
+        return self.blk.length[self.b * self.num_columns] if self.num_columns else 0
+
+    def materialize(self) -> List[Array]:
+        if self._cols is None:
+            self._cols = self._build()
+        return self._cols
+
+    def _build(self) -> List[Array]:
+        k = self.blk
+        out = []
+        for i in range(self.b * self.num_columns, (self.b + 1) * self.num_columns):
+            t = DataType(k.type[i])
+            n = k.length[i]
+            nulls = k.nulls[i]
+            if t == DataType.Utf8:
+                offs = k.buffer(k.offsets[i], 4 * (n + 1)).view(torch.int32)
+                nbytes = int(offs[n]) if n else 0
+                vals = k.buffer(k.values[i], nbytes)
+                out.append(Array(t, n, vals, None, offs, 0))
+                continue
+            nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
+            vals = k.buffer(k.values[i], nb)
+            valid = k.buffer(k.validity[i], (n + 7) // 8) if (nulls and k.validity[i]) else None
+            out.append(Array(t, n, vals, valid, None, nulls))
+        return out

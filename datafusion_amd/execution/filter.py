@@ -9,41 +9,124 @@ from .expression import RuntimeExpr
 from .relation import Relation
 
 
-class Coalescer:
-    """Pulls up to `m` device batches from `source` and runs them as ONE
-    launch (dfmi_filter_project_batches), then hands the results out one
-    batch per next() -- the same output stream as one pull per batch
-    (relation.rs:27-32): one output batch per input batch, in order; on an
-    error the batches before the failing one come first, then the error, and
-    the batches pulled after it are run one at a time if the caller goes on."""
+def is_host_batch(b: RecordBatch) -> bool:
+    return all(c.values.is_cpu for c in b.columns)
 
-    def __init__(self, m: int, source: Relation, run_one: Callable, run_many: Callable, wrap: Callable):
-        self.m, self.source = m, source
-        self.run_one, self.run_many, self.wrap = run_one, run_many, wrap
-        self.ready: List = []      # RecordBatches / an exception, in stream order
-        self.pending: List = []    # pulled input batches still to run one by one
+
+def detach(b: RecordBatch) -> RecordBatch:
+    """A batch that owns its buffers: a source's zero-copy views (e.g.
+    NativeCsvDataSource(copy=False)) are valid only until its next pull."""
+    from ..arrow import Array
+    cl = lambda t: None if t is None else t.clone()
+    return RecordBatch(b.schema, [Array(a.data_type, a.length, cl(a.values), cl(a.validity), cl(a.offsets),
+                                        a.null_count) for a in b.columns])
+
+
+class Coalescer:
+    """Pulls up to `m` batches (and at most `max_rows` rows) from `source`
+    ahead and runs them as ONE call -- device batches as one launch
+    (dfmi_filter_project_batches), host batches as one H2D + launch + D2H
+    (dfmi_filter_project_host_batches) -- then hands the results out one
+    batch per next(): the same output stream as one pull per batch
+    (relation.rs:27-32, csv_sql.rs:60-62). One output batch per input batch,
+    in order; on an error the batches before the failing one come first, then
+    the error, and the batches pulled after it run one at a time if the
+    caller goes on. An error the SOURCE raises while reading ahead comes after
+    the batches read before it, as the pull loop would have seen it.
+
+    With `run_many_host_async`, while one group's results are handed out the
+    next group of host batches is already read and its call runs on the
+    engine's worker thread (staging, PCIe and the launch overlap the pull
+    loop); the stream is the same."""
+
+    def __init__(self, m: int, source: Relation, run_one: Callable, run_many: Callable, wrap: Callable,
+                 run_many_host: Callable = None, max_rows: int = 1 << 20, run_many_host_async: Callable = None):
+        self.m, self.source, self.max_rows = m, source, max_rows
+        self.run_one, self.run_many, self.run_many_host, self.wrap = run_one, run_many, run_many_host, wrap
+        self.run_many_host_async = run_many_host_async
+        self.ready: List = []      # RecordBatches / exceptions, in stream order
+        self.pending: List = []    # pulled input batches (or a source error) still to run one by one
+        self.ahead = None          # the next group read ahead: (future or None, batches, source error)
+
+    def _read_ahead(self):
+        pulled, rows = [], 0
+        while len(pulled) < self.m and rows < self.max_rows:
+            try:
+                b = self.source.next()
+            except Exception as e:  # raised after the batches before it
+                return pulled, e
+            if b is None:
+                break
+            if getattr(b, "_transient", False):
+                b = detach(b)
+            pulled.append(b)
+            rows += b.num_rows()
+        return pulled, None
+
+    def _fetch(self):
+        """Read the next group; start its call now when it can run on the worker."""
+        pulled, src_err = self._read_ahead()
+        fut = None
+        if self.run_many_host_async is not None and len(pulled) > 1 and is_host_batch(pulled[0]):
+            try:
+                fut = self.run_many_host_async(pulled)
+            except ValueError:  # not every batch is in host memory: the synchronous runs
+                fut = None
+        return fut, pulled, src_err
+
+    def _accept(self, pulled, results, err) -> bool:
+        """Results of one coalesced call into ready; after a failing batch the
+        rest go to pending. True when the group had no error."""
+        self.ready.extend(self.wrap(cols) for cols in results)
+        if err is not None:
+            self.ready.append(err)
+            self.pending.extend(pulled[len(results) + 1:])
+            return False
+        return True
+
+    def _run(self, pulled) -> None:
+        """Results of `pulled` (consecutive runs of host / device batches)
+        into self.ready; after a failing batch the rest go to pending."""
+        i = 0
+        while i < len(pulled):
+            host = is_host_batch(pulled[i])
+            j = i + 1
+            while j < len(pulled) and is_host_batch(pulled[j]) == host:
+                j += 1
+            run = pulled[i:j]
+            many = self.run_many_host if host else self.run_many
+            if len(run) == 1:  # (a large batch ends the read-ahead): the single-batch entry point
+                many = None
+            if many is None:  # one call each, in order
+                self.pending.extend(pulled[i:])
+                return
+            results, err = many(run)
+            if not self._accept(pulled[i:], results, err):
+                return
+            i = j
 
     def next(self) -> Optional[RecordBatch]:
         while not self.ready:
             if self.pending:
-                self.ready.append(self.wrap(self.run_one(self.pending.pop(0))))
-                break
-            pulled = []
-            while len(pulled) < self.m:
-                b = self.source.next()
-                if b is None:
-                    break
-                pulled.append(b)
+                item = self.pending.pop(0)
+                if isinstance(item, Exception):
+                    raise item
+                return self.wrap(self.run_one(item))
+            fut, pulled, src_err = self.ahead if self.ahead is not None else self._fetch()
+            self.ahead = None
             if not pulled:
+                if src_err is not None:
+                    raise src_err
                 return None
-            if any(all(c.values.device.type == "cpu" for c in b.columns) for b in pulled):
-                self.pending = pulled  # host batches: the host entry point, one pull each
-                continue
-            results, err = self.run_many(pulled)
-            self.ready = [self.wrap(cols) for cols in results]
-            if err is not None:
-                self.ready.append(err)
-                self.pending = pulled[len(results) + 1:]
+            if fut is not None:
+                results, err = fut.result()
+                self._accept(pulled, results, err)
+            else:
+                self._run(pulled)
+            if src_err is not None:
+                self.pending.append(src_err)
+            elif not self.pending and self.run_many_host_async is not None:
+                self.ahead = self._fetch()  # the next group runs while this one is handed out
         item = self.ready.pop(0)
         if isinstance(item, Exception):
             raise item
@@ -54,7 +137,7 @@ class FilterRelation(Relation):
     """FilterRelation::new(input, expr, schema). next() pulls one batch from
     the input and returns every column filtered by the predicate, in a batch
     whose schema is Schema::empty() (filter.rs:60-61). With coalesce > 1, up
-    to that many input batches run as one device launch (Coalescer)."""
+    to that many input batches run as one device call (Coalescer)."""
 
     def __init__(self, input: Relation, expr: RuntimeExpr, schema: Schema, device=None, flags: int = None,
                  coalesce: int = 1):
@@ -68,7 +151,7 @@ class FilterRelation(Relation):
 
     def run_batch(self, batch: RecordBatch):
         eng = engine(self.device)
-        if all(c.values.device.type == "cpu" for c in batch.columns):
+        if is_host_batch(batch):
             return eng.filter_project_host(self.expr, None, batch, self.flags)
         return eng.filter_project(self.expr, None, batch, self.flags)
 
@@ -78,17 +161,16 @@ class FilterRelation(Relation):
                 self._co = Coalescer(self.coalesce, self.input, self.run_batch,
                                      lambda bs: engine(self.device).filter_project_batches(self.expr, None, bs,
                                                                                            self.flags),
-                                     lambda cols: RecordBatch(Schema.empty(), cols))
+                                     lambda cols: RecordBatch(Schema.empty(), cols),
+                                     lambda bs: engine(self.device).filter_project_host_batches(self.expr, None, bs,
+                                                                                                self.flags),
+                                     run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
+                                         self.expr, None, bs, self.flags))
             return self._co.next()
         batch = self.input.next()
         if batch is None:
             return None
-        eng = engine(self.device)
-        if all(c.values.device.type == "cpu" for c in batch.columns):
-            cols = eng.filter_project_host(self.expr, None, batch, self.flags)  # host batch: host results
-        else:
-            cols = eng.filter_project(self.expr, None, batch, self.flags)
-        return RecordBatch(Schema.empty(), cols)
+        return RecordBatch(Schema.empty(), self.run_batch(batch))  # host batch: host results
 
     def schema(self) -> Schema:
         return self._schema

@@ -12,7 +12,7 @@ from typing import List, Optional
 from ..arrow import Field, RecordBatch, Schema
 from .engine import engine
 from .expression import RuntimeExpr
-from .filter import Coalescer, FilterRelation
+from .filter import Coalescer, FilterRelation, is_host_batch
 from .relation import Relation
 
 
@@ -25,6 +25,7 @@ class ProjectRelation(Relation):
         self.device = device
         self.coalesce = coalesce
         self._co = None
+        self._batch_schema = None
         if flags is None:
             flags = 0
             for e in self.expr:
@@ -39,13 +40,14 @@ class ProjectRelation(Relation):
         return self.input, None
 
     def _wrap(self, cols) -> RecordBatch:
-        schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
-        return RecordBatch(schema, cols)
+        if self._batch_schema is None:  # projection.rs:52-57, the same for every batch
+            self._batch_schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
+        return RecordBatch(self._batch_schema, cols)
 
     def run_batch(self, batch: RecordBatch):
         _, pred = self._source_and_predicate()
         eng = engine(self.device)
-        if all(c.values.device.type == "cpu" for c in batch.columns):
+        if is_host_batch(batch):
             # a host batch (e.g. a CSV source's pinned buffers): the pipelined
             # host entry point, host results -- what a Rust caller gets
             return eng.filter_project_host(pred, self.expr, batch, self.flags)
@@ -58,7 +60,11 @@ class ProjectRelation(Relation):
                 self._co = Coalescer(self.coalesce, source, self.run_batch,
                                      lambda bs: engine(self.device).filter_project_batches(pred, self.expr, bs,
                                                                                            self.flags),
-                                     self._wrap)
+                                     self._wrap,
+                                     lambda bs: engine(self.device).filter_project_host_batches(pred, self.expr, bs,
+                                                                                                self.flags),
+                                     run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
+                                         pred, self.expr, bs, self.flags))
             return self._co.next()
         batch = source.next()
         if batch is None:

@@ -287,6 +287,16 @@ int32_t dfmi_host_result_num_columns(const dfmi_host_result* result);
 /* Host view of result column i; buffers stay valid until the result is freed.
  * `validity` is NULL when null_count == 0 (filtered outputs never have one). */
 int32_t dfmi_host_result_column(const dfmi_host_result* result, int32_t i, dfmi_column* view);
+/* Views of columns [first, first + count) in one call (views[k] as
+ * dfmi_host_result_column(first + k)): a binding that hands out one output
+ * batch per input batch of the coalesced form below reads every batch's
+ * views at once instead of one FFI call per column. */
+int32_t dfmi_host_result_columns(const dfmi_host_result* result, int32_t first, int32_t count, dfmi_column* views);
+/* The one pinned block holding the columns of a coalesced result (NULL / 0
+ * for the single-batch pipelined form): a binding may wrap it once and slice
+ * every column's buffers out of it, keeping the result alive while any such
+ * slice is. Passthrough columns live outside it. */
+int32_t dfmi_host_result_block(const dfmi_host_result* result, const void** base, size_t* bytes);
 void dfmi_host_result_free(dfmi_host_result* result);
 
 /* Coalesced form of dfmi_filter_project_host for many small HOST batches

@@ -156,3 +156,89 @@ def test_relation_coalesces_batches():
     for a, b in zip(*streams):
         for x, y in zip(a, b):
             assert_same(x, y)
+
+
+def _oracle_stream(schema, batches, pred_e, proj_e):
+    """The reference pull loop's view, batch by batch: column lists or errors."""
+    out = []
+    for b in batches:
+        try:
+            out.append([r for _, r in oracle_filter_project(schema, b, pred_e, proj_e, 0)])
+        except ExecutionError as e:
+            out.append(e)
+    return out
+
+
+def _pull_all(rel):
+    """Every next() of a relation until None, continuing after errors."""
+    seen = []
+    for _ in range(100_000):
+        try:
+            b = rel.next()
+        except ExecutionError as e:
+            seen.append(e)
+            continue
+        if b is None:
+            return seen
+        seen.append(b)
+    raise AssertionError("relation did not end")
+
+
+@pytest.mark.parametrize("m", [1, 64, 256])
+def test_relation_host_batches_against_oracle(m):
+    """ctx.sql over csv_sql.rs:49-style HOST batches (1024 rows, plus ragged
+    and empty ones) through the relations: with read-ahead M the
+    ProjectRelation runs M batches per dfmi_filter_project_host_batches call
+    and still hands out the oracle's batch for every pull; a DivideByZero in
+    batch 57 comes after batches 0..56 and the stream goes on after it."""
+    s, bs = make_batches([1024] * 100 + [10, 0, 5000, 1024, 3] + [1024] * 60, seed=11, utf8=False)
+    v = np.array(bs[57].columns[1].cpu().numpy_values())
+    v[500] = 0.0
+    bs[57] = RecordBatch(s, [bs[57].columns[0], Array.from_numpy(DataType.Float64, v), bs[57].columns[2]])
+    c = np.array(bs[57].columns[2].cpu().numpy_values())
+    c[500] = 0.5  # selected
+    bs[57] = RecordBatch(s, [bs[57].columns[0], bs[57].columns[1], Array.from_numpy(DataType.Float64, c)])
+    ctx = ExecutionContext(coalesce=m)
+    ctx.register_datasource("t", MemoryDataSource(s, bs))
+    got = _pull_all(ctx.sql("SELECT a, a / b, c FROM t WHERE c >= 0.25"))
+    pred = BinaryExpr(Column(2), Operator.GtEq, Literal(Float64(0.25)))
+    projs = [Column(0), BinaryExpr(Column(0), Operator.Divide, Column(1)), Column(2)]
+    ref = _oracle_stream(s, bs, pred, projs)
+    assert len(got) == len(ref) == len(bs)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        if isinstance(r, ExecutionError):
+            assert isinstance(g, ExecutionError) and (g.kind, g.message) == (r.kind, r.message), (i, g)
+            continue
+        assert not isinstance(g, ExecutionError), (i, g)
+        assert g.num_rows() == r[0].length
+        for d, x in zip(g.columns, r):
+            assert d.values.device.type == "cpu"  # host batches in, host batches out
+            assert_same(d, x, "batch %d" % i)
+    assert isinstance(got[57], ExecutionError)
+
+
+def test_relation_native_csv_views_coalesced(tmp_path):
+    """NativeCsvDataSource(copy=False) hands out views its next pull
+    overwrites: read-ahead over it must still give the copy=True stream."""
+    from datafusion_amd.execution import NativeCsvDataSource
+    rng = np.random.default_rng(12)
+    n = 1024 * 37 + 5
+    path = tmp_path / "t.csv"
+    a, b, c = rng.random(n), rng.random(n), rng.random(n)
+    with open(path, "w") as f:
+        f.write("a,b,c\n")
+        for i in range(n):
+            f.write("%r,%r,%r\n" % (float(a[i]), float(b[i]), float(c[i])))
+    s = Schema([Field(x, DataType.Float64, False) for x in "abc"])
+    sql = "SELECT a, b, a * b + c FROM t WHERE a > 0.25 AND b < 0.75"
+    streams = []
+    for m, copy in ((1, True), (4, False), (256, False)):
+        ctx = ExecutionContext(coalesce=m)
+        ctx.register_datasource("t", NativeCsvDataSource(s, str(path), True, 1024, copy=copy))
+        streams.append([[col.cpu() for col in rb.columns] for rb in ctx.sql(sql)])
+    assert len(streams[0]) == 38
+    for other in streams[1:]:
+        assert len(other) == len(streams[0])
+        for x, y in zip(streams[0], other):
+            for p, q in zip(x, y):
+                assert_same(p, q)
