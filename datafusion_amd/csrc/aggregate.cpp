@@ -59,7 +59,7 @@ struct dfmi_agg_state {
         __int128 ord;
         bool operator<(const HKey& o) const { return null != o.null ? !null : (!null && ord < o.ord); }
     };
-    std::map<HKey, std::pair<uint64_t, std::vector<Partial_>>> groups;  // key -> (bits, partials)
+    std::map<HKey, std::pair<uint64_t, std::vector<Partial_>>> groups;  // key -> (bits, partials + row count)
     // integer keys: the per-batch key window comes from MIN / MAX of the key
     // over the batch's selected rows (a pre-pass through this same extension)
     dfmi_aggregate* mm[2] = {nullptr, nullptr};
@@ -387,8 +387,9 @@ void flush_groups(dfmi_context* ctx, dfmi_agg_state* st) {
                                              : (is_signed_type(kt) ? (__int128)(int64_t)bits : (__int128)bits);
         }
         auto it = st->groups.find(hk);
-        if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(n))).first;
+        if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(na))).first;
         for (size_t j = 0; j < n; ++j) merge_partial(it->second.second[j], parts[j], st->aggs[j]->fn == DFMI_AGG_MIN);
+        it->second.second[n].count += parts[n].count;  // the hidden count: the group's selected rows
     }
     HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
     st->dirty = false;
@@ -532,7 +533,7 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
             keys[g].type = st->key.type;
             keys[g].is_null = hk.null ? 1 : 0;
             keys[g].bits = hk.null ? 0 : (st->key.type == DFMI_TYPE_BOOLEAN ? v.first : narrow_int(v.first, st->key.type));
-            keys[g].count = 0;
+            keys[g].count = (int64_t)v.second[n].count;  // the group's selected rows
             for (size_t j = 0; j < n; ++j) values[g * n + j] = finish_one(*st->aggs[j], v.second[j]);
             ++g;
         }

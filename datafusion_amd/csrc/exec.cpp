@@ -49,7 +49,20 @@ struct Built {
     jit::Launch X;
     bool any_kernel_out = false;
     int64_t n_tiles = 0;
+    bool low_sel = false;  // in: this query shape selected few rows last time (dfmi_context::sel_hint)
 };
+
+// A numeric predicate over a large batch that selects few rows runs the
+// sub-tile kernel: M sub-tiles of BLOCK * K rows share one scan + look-back
+// (one look-back per 16,384 rows instead of per 4,096), the predicate pass
+// keeps only selection ballots, and the output pass reloads just the columns
+// the outputs read, for the selected rows (jit.cpp "M sub-tiles"). Chosen
+// from the selectivity the same query shape had on its previous large batch
+// on this context (below kLowSel); the first call, and any call after a
+// batch selected more, runs the one-tile kernel, which keeps every loaded
+// value in registers across the look-back.
+constexpr int64_t kSubtileMinRows = (int64_t)1 << 22;
+constexpr double kLowSel = 0.04;
 
 void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
                      dfmi_out_column* outs, uint32_t flags, Built& B);
@@ -228,6 +241,9 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             X.BLOCK = 256;
             X.waves_per_eu = 7;
             X.waves_soft = true;
+        } else if (pred && B.low_sel && !X.pred_slots.empty() && X.utf8_cols.empty() && n >= kSubtileMinRows) {
+            X.BLOCK = 256;
+            X.M = 8;
         }
     }
     // diagnostic knobs (tools/*): read only when DFMI_DIAG is set -- a dozen
@@ -250,6 +266,12 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
+        // the numeric sub-tile kernel at any size (parity tests, A/B runs)
+        if (const char* e = getenv("DFMI_NUMERIC_SUBTILES"))
+            if (atoi(e) > 1 && pred && !X.pred_slots.empty() && X.utf8_cols.empty()) {
+                X.BLOCK = 256;
+                X.M = std::min(8, atoi(e));
+            }
         if (const char* e = getenv("DFMI_OUT_SLICES")) X.KO = atoi(e);
         if (const char* e = getenv("DFMI_SUBTILE_PREFETCH")) X.prefetch = atoi(e) & 1;
         if (const char* e = getenv("DFMI_SUBTILE_SPARSE")) X.sparse = atoi(e) & 1;
@@ -282,6 +304,21 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
 
     B.n_tiles = n_tiles;
+}
+
+// The selectivity hint's key: the programs and the batch's column types /
+// nullability (a performance hint only: results never depend on it).
+uint64_t sel_hint_key(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* in,
+                      uint32_t flags) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    mix((uint64_t)(uintptr_t)pred);
+    mix((uint64_t)np);
+    for (int j = 0; j < np; ++j) mix((uint64_t)(uintptr_t)projs[j]);
+    mix(flags);
+    for (int i = 0; i < in->num_columns; ++i)
+        mix((uint64_t)in->columns[i].type << 1 | (in->columns[i].validity && in->columns[i].null_count > 0));
+    return h;
 }
 
 }  // namespace
@@ -404,6 +441,12 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
         Built B;
+        uint64_t hint_key = 0;
+        if (pred && in->num_rows >= kSubtileMinRows) {
+            hint_key = sel_hint_key(pred, projs, np, in, flags);
+            auto it = ctx->sel_hint.find(hint_key);
+            B.low_sel = it != ctx->sel_hint.end() && it->second < kLowSel;
+        }
         build_plan(pred, projs, np, in, outs, flags, B);
         auto t_b = tnow();
         if (prof) ph[0] += tms(t_a, t_b);
@@ -607,6 +650,10 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         memset(totals, 0, sizeof totals);
         if (launch) memcpy(totals, ctx->host_hdr + kHdrTotals, sizeof totals);
         const int64_t out_rows = pred ? (int64_t)totals[0] : n;
+        if (hint_key && launch) {  // what this shape selected, for its next large batch
+            if (ctx->sel_hint.size() >= 4096) ctx->sel_hint.clear();
+            ctx->sel_hint[hint_key] = (double)out_rows / (double)n;
+        }
         for (int o = 0; o < nout; ++o) {
             dfmi_out_column& oc = outs[o];
             if (oc.passthrough_column >= 0) continue;
@@ -828,49 +875,65 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
             }
             for (int64_t t = 0; t < tiles[b]; ++t) tile_batch[first[b] + t] = b;
         }
-        // ---- launch
+        // ---- launch. A look-back that timed out in any batch (the GPU
+        // time-sliced away from this queue for 2 s) is relaunched once over a
+        // re-zeroed workspace and headers, as dfmi_filter_project does; the
+        // relaunch rewrites every batch's outputs.
         if (stage) stage->copy_in(st);  // (staged: with the table and the zeroed headers)
-        if (T > 0) {
-            if (!staged) {
-                HIP_TRY(hipMemcpyAsync(dev_meta, host_meta, meta_bytes, hipMemcpyHostToDevice, st));
-                HIP_TRY(hipMemsetAsync(dev_hdr, 0, (size_t)nb * kBHdr, st));
+        int mode = 0;
+        if (getenv("DFMI_DIAG"))
+            if (const char* m = getenv("DFMI_DEBUG_MODE")) mode = atoi(m);  // diagnostics only (bit 4: force a timeout)
+        for (int attempt = 0;; ++attempt) {
+            if (T > 0) {
+                if (!staged && attempt == 0) HIP_TRY(hipMemcpyAsync(dev_meta, host_meta, meta_bytes, hipMemcpyHostToDevice, st));
+                if (!staged || attempt > 0) HIP_TRY(hipMemsetAsync(dev_hdr, 0, (size_t)nb * kBHdr, st));
+                const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
+                const size_t status_bytes = (size_t)n_chan * T * 8 * X.spread;
+                Args A;
+                memset(&A, 0, sizeof A);
+                A.n_rows = maxn;
+                A.n_tiles = (int)T;
+                A.mode = mode;
+                memcpy(A.lits, X.args_lits, sizeof A.lits);
+                memcpy(A.str_off, X.str_off, sizeof A.str_off);
+                memcpy(A.str_len, X.str_len, sizeof A.str_len);
+                memcpy(A.str, X.str, sizeof A.str);
+                const WsLease ws = ws_acquire(ctx, status_bytes, st);
+                A.ticket = (unsigned*)(ws.hdr + kHdrTicket);
+                A.err = (unsigned long long*)(ws.hdr + kHdrErr);
+                A.totals = (unsigned long long*)(ws.hdr + kHdrTotals);
+                A.status = (unsigned long long*)ws.status;
+                A.stats = (unsigned long long*)(ws.hdr + kHdrStats);
+                A.clear_status = (unsigned long long*)ws.clear_status;
+                A.clear_words = ws.clear_words;
+                A.clear_hdr = (unsigned long long*)ws.clear_hdr;
+                A.tile_batch = (const int*)(dev_meta + table_bytes);
+                A.batch_ptrs = (void* const*)dev_meta;
+                if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
+                size_t asz = sizeof A;
+                void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+                HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)T, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
+                ws_commit(ctx, ws);
+                if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
+                if (!staged) HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
             }
-            const int n_chan = pred ? 1 + (int)X.utf8_outs.size() : 0;
-            const size_t status_bytes = (size_t)n_chan * T * 8 * X.spread;
-            Args A;
-            memset(&A, 0, sizeof A);
-            A.n_rows = maxn;
-            A.n_tiles = (int)T;
-            memcpy(A.lits, X.args_lits, sizeof A.lits);
-            memcpy(A.str_off, X.str_off, sizeof A.str_off);
-            memcpy(A.str_len, X.str_len, sizeof A.str_len);
-            memcpy(A.str, X.str, sizeof A.str);
-            const WsLease ws = ws_acquire(ctx, status_bytes, st);
-            A.ticket = (unsigned*)(ws.hdr + kHdrTicket);
-            A.err = (unsigned long long*)(ws.hdr + kHdrErr);
-            A.totals = (unsigned long long*)(ws.hdr + kHdrTotals);
-            A.status = (unsigned long long*)ws.status;
-            A.stats = (unsigned long long*)(ws.hdr + kHdrStats);
-            A.clear_status = (unsigned long long*)ws.clear_status;
-            A.clear_words = ws.clear_words;
-            A.clear_hdr = (unsigned long long*)ws.clear_hdr;
-            A.tile_batch = (const int*)(dev_meta + table_bytes);
-            A.batch_ptrs = (void* const*)dev_meta;
-            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
-            size_t asz = sizeof A;
-            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
-            HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)T, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
-            ws_commit(ctx, ws);
-            if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
-            if (!staged) HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
+            for (int32_t b = 0; b < nb; ++b)  // empty batches: Utf8 offsets = [0]
+                if (ins[b].num_rows == 0)
+                    for (int o = 0; o < nout; ++o)
+                        if (plan.outs[o].kind == jit::OutSpec::UTF8 && outs[(size_t)b * nout + o].offsets)
+                            HIP_TRY(hipMemsetAsync(outs[(size_t)b * nout + o].offsets, 0, 4, st));
+            if (stage) stage->copy_out(st);  // (staged: with the headers)
+            HIP_TRY(hipStreamSynchronize(st));
+            bool timed_out = false;
+            for (int32_t b = 0; b < nb && T > 0; ++b) {
+                const uint64_t ew = ins[b].num_rows > 0 ? ((const uint64_t*)(host_hdr + (size_t)b * kBHdr))[24] : 0;
+                if (ew && (int)(~ew & 15) == ERRK_LOOKBACK_TIMEOUT) timed_out = true;
+            }
+            if (!timed_out || attempt > 0) break;
+            ctx->ws_valid = false;  // status words in an unknown state: re-zero all
+            ++ctx->relaunches;
+            mode &= ~16;  // (diagnostic forced timeout: once)
         }
-        for (int32_t b = 0; b < nb; ++b)  // empty batches: Utf8 offsets = [0]
-            if (ins[b].num_rows == 0)
-                for (int o = 0; o < nout; ++o)
-                    if (plan.outs[o].kind == jit::OutSpec::UTF8 && outs[(size_t)b * nout + o].offsets)
-                        HIP_TRY(hipMemsetAsync(outs[(size_t)b * nout + o].offsets, 0, 4, st));
-        if (stage) stage->copy_out(st);  // (staged: with the headers)
-        HIP_TRY(hipStreamSynchronize(st));
         if (T > 0 && ctx->timing) {
             float m1 = 0;
             (void)hipEventElapsedTime(&m1, ctx->ev0, ctx->ev1);

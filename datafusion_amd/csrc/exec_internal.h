@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <string>
+#include <unordered_map>
 
 #include "dfmi_program.h"
 #include "jit.h"
@@ -64,6 +65,9 @@ struct dfmi_context {
     size_t host_bhdr_bytes = 0;
     uint8_t* ones = nullptr;
     size_t ones_bytes = 0;
+    // selectivity of each query shape's last large batch (exec.cpp
+    // kSubtileMinRows): picks the sub-tile kernel for low selectivity
+    std::unordered_map<uint64_t, double> sel_hint;
 };
 
 namespace dfmi {

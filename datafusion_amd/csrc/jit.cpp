@@ -16,6 +16,8 @@
 // serves every instance of a query shape.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -344,14 +346,115 @@ void evict_to(size_t cap) {
 }
 }  // namespace
 
+// ------------------------------------------------------- on-disk code objects
+// A process's first call of a query shape would pay the hipRTC compile
+// (~190 ms); the reference's compile_scalar_expr is a closure build
+// (context.rs:131,152-155). Code objects are therefore also kept on disk,
+// keyed by a hash of the generated source, the compile options, the hipRTC
+// version and the target: DFMI_JIT_CACHE_DIR (empty: off), else
+// $XDG_CACHE_HOME/dfmi-jit, else $HOME/.cache/dfmi-jit. A file holds the full
+// source it was compiled from and is used only when that source matches
+// byte for byte (a hash collision cannot load the wrong code); files are
+// written to a temporary name and renamed, so a reader never sees a partial
+// one, and a damaged or foreign file is ignored (compiled again).
+namespace {
+const char* const kOpts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
+                             "-Wno-unused-variable", "-Wno-unused-but-set-variable"};
+
+const std::string& disk_dir() {
+    static const std::string dir = [] {
+        std::string d;
+        if (const char* e = getenv("DFMI_JIT_CACHE_DIR")) {
+            d = e;  // "" disables
+        } else if (const char* x = getenv("XDG_CACHE_HOME"); x && *x) {
+            d = std::string(x) + "/dfmi-jit";
+        } else if (const char* h = getenv("HOME"); h && *h) {
+            d = std::string(h) + "/.cache/dfmi-jit";
+        }
+        if (!d.empty()) {  // mkdir -p
+            for (size_t i = 1; i <= d.size(); ++i)
+                if (i == d.size() || d[i] == '/') (void)::mkdir(d.substr(0, i).c_str(), 0755);
+            struct stat st;
+            if (::stat(d.c_str(), &st) != 0 || !S_ISDIR(st.st_mode)) d.clear();
+        }
+        return d;
+    }();
+    return dir;
+}
+
+uint64_t fnv1a(const void* p, size_t n, uint64_t h) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
+std::string disk_path(const std::string& src) {
+    int maj = 0, min = 0;
+    hiprtcVersion(&maj, &min);
+    std::string salt = "dfmi-co-1 hiprtc " + std::to_string(maj) + "." + std::to_string(min);
+    for (const char* o : kOpts) salt += std::string(" ") + o;
+    uint64_t h1 = fnv1a(salt.data(), salt.size(), 0xcbf29ce484222325ull);
+    h1 = fnv1a(src.data(), src.size(), h1);
+    uint64_t h2 = fnv1a(src.data(), src.size(), 0x84222325cbf29ce4ull ^ src.size());
+    h2 = fnv1a(salt.data(), salt.size(), h2);
+    char name[64];
+    snprintf(name, sizeof name, "/%016llx%016llx.co", (unsigned long long)h1, (unsigned long long)h2);
+    return disk_dir() + name;
+}
+
+constexpr char kMagic[8] = {'D', 'F', 'M', 'I', 'C', 'O', '1', '\n'};
+
+bool disk_load(const std::string& path, const std::string& src, std::vector<char>& code) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    bool ok = false;
+    char magic[8];
+    uint64_t ns = 0, nc = 0;
+    if (fread(magic, 1, 8, f) == 8 && !memcmp(magic, kMagic, 8) && fread(&ns, 8, 1, f) == 1 && ns == src.size()) {
+        std::string s(ns, '\0');
+        if (fread(&s[0], 1, ns, f) == ns && s == src && fread(&nc, 8, 1, f) == 1 && nc > 0 && nc < ((uint64_t)1 << 30)) {
+            code.resize(nc);
+            ok = fread(code.data(), 1, nc, f) == nc && fgetc(f) == EOF;
+        }
+    }
+    fclose(f);
+    return ok;
+}
+
+void disk_store(const std::string& path, const std::string& src, const std::vector<char>& code) {
+    char tmp[64];
+    snprintf(tmp, sizeof tmp, ".tmp.%d.%llx", (int)getpid(),
+             (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
+    const std::string t = path + tmp;
+    FILE* f = fopen(t.c_str(), "wb");
+    if (!f) return;
+    const uint64_t ns = src.size(), nc = code.size();
+    bool ok = fwrite(kMagic, 1, 8, f) == 8 && fwrite(&ns, 8, 1, f) == 1 && fwrite(src.data(), 1, ns, f) == ns &&
+              fwrite(&nc, 8, 1, f) == 1 && fwrite(code.data(), 1, nc, f) == nc;
+    ok = fclose(f) == 0 && ok;
+    if (!ok || ::rename(t.c_str(), path.c_str()) != 0) ::unlink(t.c_str());
+}
+}  // namespace
+
 std::vector<char> compile_code(const std::string& src, double* compile_ms) {
+    if (compile_ms) *compile_ms = 0;
+    std::string path;
+    if (!disk_dir().empty()) {
+        path = disk_path(src);
+        std::vector<char> code;
+        if (disk_load(path, src, code)) return code;  // no compile: *compile_ms stays 0
+    }
+    std::vector<char> code = compile_code_rtc(src, compile_ms);
+    if (!path.empty()) disk_store(path, src, code);
+    return code;
+}
+
+std::vector<char> compile_code_rtc(const std::string& src, double* compile_ms) {
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "dfmi_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         throw Fail{DFMI_ERR_DEVICE, "hiprtcCreateProgram failed"};
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
-                          "-Wno-unused-variable", "-Wno-unused-but-set-variable"};
     const auto t0 = std::chrono::steady_clock::now();
-    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof *opts), opts);
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof kOpts / sizeof *kOpts), kOpts);
     if (compile_ms)
         *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc != HIPRTC_SUCCESS) {
@@ -455,6 +558,24 @@ static void emit_loads(std::ostream& o, const std::vector<int>& slots, const Lau
         }
     }
     o << "  }\n";
+}
+
+// Numeric / Boolean slots the outputs read (a sub-tile kernel's output pass
+// reloads exactly these for the selected rows).
+static std::vector<int> output_slots(const Plan& P, const Launch& X) {
+    std::vector<int> out;
+    auto add_col = [&](int col) {
+        for (size_t s = 0; s < X.num_cols.size(); ++s)
+            if (X.num_cols[s] == col && std::find(out.begin(), out.end(), (int)s) == out.end()) out.push_back((int)s);
+    };
+    for (const OutSpec& os : P.outs) {
+        if (os.kind == OutSpec::GATHER) add_col(os.col);
+        if (os.kind == OutSpec::EXPR)
+            for (const IrNode& nd : os.prog->ir)
+                if (nd.kind == IR_COL) add_col(nd.col);
+    }
+    std::sort(out.begin(), out.end());
+    return out;
 }
 
 // The predicate of a filtered tile: `unsigned selm` (bit k = row base + k*BLOCK
@@ -741,6 +862,7 @@ std::string generate(const Plan& P, Launch& X) {
                                     std::to_string(X.spread) + ", " + std::to_string(X.window);
         std::vector<int> utf8_out_cols;
         for (const auto& uo : X.utf8_outs) utf8_out_cols.push_back(uo.second);
+        const std::vector<int> out_slots = output_slots(P, X);
         auto offs_name = [&](int u) { return std::to_string(u); };
         // The predicate over the rows at `base`: selm, the projection-only
         // loads (unless late), the selection ballots wm and counts cnt.
@@ -796,7 +918,8 @@ std::string generate(const Plan& P, Launch& X) {
         auto emit_outputs = [&](const std::string& kb, bool prestaged) {
             // byte-light predicates: projection-only columns after the look-back
             // (fewer registers held across it; few rows are selected)
-            if (X.late_proj || X.M > 1) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            if (X.M > 1) emit_loads(o, out_slots, X, "", "base", "(selm >> k) & 1", false);
+            else if (X.late_proj) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
             o << "  const i64 obase = (i64)T.prefix[0];\n  unsigned dst[K];\n#pragma unroll\n"
               << "  for (int k = 0; k < K; ++k) dst[k] = (unsigned)T.excl[0][(" << kb
               << " + k) * WAVES + wave] + dfmi::lane_rank(wm[k]);\n";
@@ -874,7 +997,9 @@ std::string generate(const Plan& P, Launch& X) {
             // ballots and counts (LDS), one scan + look-back covers all of
             // them, and the output pass revisits the sub-tiles with selected
             // rows, reloading the Utf8 offsets and column values they need.
-            if (!X.pred_slots.empty()) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "sub-tiles need a Utf8-only predicate"};
+            // (a numeric predicate loads its columns per sub-tile; its output
+            // pass reloads the columns the outputs read for the selected rows
+            // only -- chosen for low selectivity, exec.cpp)
             o << "  constexpr int M = " << X.M << ";\n"
               << "  __shared__ dfmi::Tile<BLOCK, K * M, NCH> T;\n  __shared__ u64 WS[K * M * WAVES];\n";
             // software pipeline: sub-tile m+1's Utf8 offsets are loaded while
@@ -898,6 +1023,11 @@ std::string generate(const Plan& P, Launch& X) {
                     o << "  int us" << u << "[K], ux" << u << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, " << u
                       << ", base, lane, wave, ~0u, us" << u << ", ux" << u << ");\n";
             g.filtered_cols = false;
+            if (!X.pred_slots.empty()) {
+                o << "  {\n";
+                emit_decls(o, X.pred_slots, X, "", true);
+                emit_loads(o, X.pred_slots, X, "", "base", nullptr, true);
+            }
             emit_predicate(g, o, P, X, "", utf8_out_cols, true);
             o << "  unsigned cnt[NCH][K];\n  u64 wm[K];\n#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
               << "    wm[k] = __ballot((selm >> k) & 1);\n    cnt[0][k] = (selm >> k) & 1;\n  }\n";
@@ -907,7 +1037,9 @@ std::string generate(const Plan& P, Launch& X) {
                   << "[k], ux" << offs_name(u) << "[k], lane); cnt[" << (j + 1) << "][k] = ((selm >> k) & 1) ? "
                   << "(unsigned)(e_ - us" << offs_name(u) << "[k]) : 0u; }\n";
             }
-            o << "  dfmi::subtile_counts<BLOCK, K, NCH>(T, WS, m_ * K, cnt, wm, lane, wave);\n  }\n";
+            o << "  dfmi::subtile_counts<BLOCK, K, NCH>(T, WS, m_ * K, cnt, wm, lane, wave);\n";
+            if (!X.pred_slots.empty()) o << "  }\n";
+            o << "  }\n";
             const std::string sp = std::to_string(X.spread);
             o << "  dfmi::tile_scan_lds<BLOCK, K * M, NCH, " << sp << ">(A, T, t, lane, wave);\n"
               << "  dfmi::tile_resolve<BLOCK, K * M, NCH, " << tparams << ">(A, T, t, lane, wave);\n"
@@ -919,24 +1051,30 @@ std::string generate(const Plan& P, Launch& X) {
             // (not with the two-pass gather: its second kernel reads the source
             // starts only the dense pass's utf8_offsets_src writes)
             bool sparse = X.sparse && X.gather != 3;
-            for (int sl : X.proj_slots) sparse = sparse && X.col_type(X.num_cols[sl]) != DFMI_TYPE_BOOLEAN;
+            for (int sl : out_slots) sparse = sparse && X.col_type(X.num_cols[sl]) != DFMI_TYPE_BOOLEAN;
             if (sparse) {
-                o << "  __shared__ unsigned short SLR[WAVES][64];\n  unsigned tot_ = 0;\n"
+                // Utf8 outputs: one round of 64 rows (their byte offsets come
+                // from one wave scan); numeric outputs: up to 4 rounds
+                const int cap = X.utf8_outs.empty() ? 256 : 64;
+                o << "  constexpr unsigned CAP_ = " << cap << ";\n"
+                  << "  __shared__ unsigned short SLR[WAVES][CAP_];\n  unsigned tot_ = 0;\n"
                   << "  for (int q_ = 0; q_ < M * K; ++q_) {\n"
                   << "    const u64 w_ = dfmi::lds_uniform_u64(&WS[q_ * WAVES + wave]);\n    if (!w_) continue;\n"
-                  << "    if (tot_ + (unsigned)__builtin_popcountll(w_) <= 64u && ((w_ >> lane) & 1))\n"
+                  << "    if (tot_ + (unsigned)__builtin_popcountll(w_) <= CAP_ && ((w_ >> lane) & 1))\n"
                   << "      SLR[wave][tot_ + dfmi::lane_rank(w_)] = (unsigned short)(q_ * 64 + lane);\n"
                   << "    tot_ += (unsigned)__builtin_popcountll(w_);\n  }\n"
-                  << "  if (tot_ <= 64u) {\n  dfmi::wave_lds_fence();\n"
-                  << "  const bool have_ = (unsigned)lane < tot_;\n"
-                  << "  const unsigned e_ = have_ ? (unsigned)SLR[wave][lane] : 0u;\n"
+                  << "  if (tot_ <= CAP_) {\n  dfmi::wave_lds_fence();\n";
+                if (cap > 64) o << "  for (unsigned r_ = 0; r_ < tot_; r_ += 64) {\n";
+                else o << "  { const unsigned r_ = 0;\n";
+                o << "  const bool have_ = r_ + (unsigned)lane < tot_;\n"
+                  << "  const unsigned e_ = have_ ? (unsigned)SLR[wave][r_ + lane] : 0u;\n"
                   << "  const int qs_ = (int)(e_ >> 6), ls_ = (int)(e_ & 63u);\n"
                   << "  const i64 row = ((i64)t * M + qs_ / K) * (BLOCK * K) + (i64)(qs_ % K) * BLOCK + 64 * wave + ls_;\n"
                   << "  const u64 wq_ = have_ ? WS[qs_ * WAVES + wave] : 0ull;\n"
                   << "  const unsigned d = have_ ? (unsigned)T.excl[0][qs_ * WAVES + wave] + "
                      "(unsigned)__builtin_popcountll(wq_ & ((1ull << ls_) - 1ull)) : 0u;\n"
                   << "  const i64 obase = (i64)T.prefix[0];\n  const int k = 0;\n";
-                for (int sl : X.proj_slots) {
+                for (int sl : out_slots) {
                     const std::string ct = ctype(X.col_type(X.num_cols[sl]));
                     o << "  " << ct << " c" << sl << "[1];\n  c" << sl << "[0] = have_ ? ((const " << ct << "*)A.col[" << sl
                       << "])[row] : (" << ct << ")0;\n";
@@ -974,7 +1112,7 @@ std::string generate(const Plan& P, Launch& X) {
                           << oo << "] + ob_, L_);\n    }\n  }\n";
                     }
                 }
-                o << "  } else {\n";
+                o << "  }\n  } else {\n";  // (the rounds; then the dense output pass)
             }
             // output pass in steps of KO slices (fewer registers than K)
             o << "  {\n  constexpr int KS = K, K = " << X.KO << ";  // slices per sub-tile / per output step\n"
@@ -987,7 +1125,7 @@ std::string generate(const Plan& P, Launch& X) {
             for (int u : utf8_out_cols)
                 o << "  int us" << offs_name(u) << "[K], ux" << offs_name(u) << "[K];\n  dfmi::utf8_offs_tile<BLOCK, K>(A, "
                   << u << ", base, lane, wave, need_, us" << offs_name(u) << ", ux" << offs_name(u) << ");\n";
-            emit_decls(o, X.proj_slots, X, "", false);
+            emit_decls(o, out_slots, X, "", false);
             emit_outputs("q_", false);
             o << "  }\n  }\n";
             if (sparse) o << "  }\n";

@@ -150,7 +150,8 @@ size_t cache_size();
 // Bound of the module cache (least recently used evicted); cap > 0 sets it.
 size_t cache_cap(size_t cap);
 // hipRTC compile of a generated source to a gfx950 code object (no device needed).
-std::vector<char> compile_code(const std::string& src, double* compile_ms);
+std::vector<char> compile_code(const std::string& src, double* compile_ms);  // on-disk cache, then hipRTC
+std::vector<char> compile_code_rtc(const std::string& src, double* compile_ms);  // hipRTC only
 
 }  // namespace jit
 }  // namespace dfmi

@@ -221,6 +221,19 @@ struct dfmi_shard_comm {
     Transport* tp = nullptr;
     std::vector<int64_t> rec;  // the last exchange: world x kRec
     int nout = 0;              // outputs of the last exchanged pass
+    // kept across calls (grow-only): the gather's staging on the root and an
+    // all-valid bitmap for a rank without validity; a pinned landing spot for
+    // passthrough Utf8 byte spans
+    uint8_t* stage = nullptr;
+    size_t stage_cap = 0;
+    uint8_t* ones = nullptr;
+    size_t ones_cap = 0;
+    int32_t* pin = nullptr;
+    ~dfmi_shard_comm() {
+        if (stage) (void)hipFree(stage);
+        if (ones) (void)hipFree(ones);
+        if (pin) (void)hipHostFree(pin);
+    }
 };
 
 namespace {
@@ -323,16 +336,22 @@ extern "C" int32_t dfmi_shard_filter_project(dfmi_context* ctx, dfmi_shard_comm*
         if (rc == DFMI_OK) {
             try {
                 mine[2] = nout ? outs[0].length : 0;
+                // passthrough (Arc clone) Utf8 outputs: the input column's byte
+                // span, both ends of every such column in one async round trip
+                bool spans = false;
+                for (int o = 0; o < nout; ++o)
+                    if (outs[o].type == DFMI_TYPE_UTF8 && outs[o].passthrough_column >= 0 && outs[o].length > 0) {
+                        if (!c->pin) HIP_TRY(hipHostMalloc((void**)&c->pin, 2 * kMaxOut * 4, hipHostMallocDefault));
+                        const int32_t* of = in->columns[outs[o].passthrough_column].offsets;
+                        HIP_TRY(hipMemcpyAsync(&c->pin[2 * o], of, 4, hipMemcpyDeviceToHost, ctx->stream));
+                        HIP_TRY(hipMemcpyAsync(&c->pin[2 * o + 1], of + outs[o].length, 4, hipMemcpyDeviceToHost, ctx->stream));
+                        spans = true;
+                    }
+                if (spans) HIP_TRY(hipStreamSynchronize(ctx->stream));
                 for (int o = 0; o < nout; ++o) {
                     int64_t nb = outs[o].type == DFMI_TYPE_UTF8 ? outs[o].data_length : 0;
-                    if (outs[o].type == DFMI_TYPE_UTF8 && outs[o].passthrough_column >= 0 && outs[o].length > 0) {
-                        // passthrough (Arc clone): the input column's byte span
-                        const int32_t* of = in->columns[outs[o].passthrough_column].offsets;
-                        int32_t ends[2];
-                        HIP_TRY(hipMemcpy(&ends[0], of, 4, hipMemcpyDeviceToHost));
-                        HIP_TRY(hipMemcpy(&ends[1], of + outs[o].length, 4, hipMemcpyDeviceToHost));
-                        nb = ends[1] - ends[0];
-                    }
+                    if (outs[o].type == DFMI_TYPE_UTF8 && outs[o].passthrough_column >= 0 && outs[o].length > 0)
+                        nb = c->pin[2 * o + 1] - c->pin[2 * o];
                     mine[3 + o] = nb;
                     mine[3 + kMaxOut + o] = outs[o].null_count;
                 }
@@ -363,7 +382,6 @@ extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm*
         set_err(err, DFMI_ERR_INVALID_ARGUMENT, "bad argument");
         return DFMI_ERR_INVALID_ARGUMENT;
     }
-    std::vector<uint8_t*> stage;
     try {
         HIP_TRY(hipSetDevice(ctx->device));
         hipStream_t st = ctx->stream;
@@ -386,6 +404,7 @@ extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm*
             int o, r;
         };
         std::vector<Piece> pieces;  // (o, r) order, the same on every rank
+        size_t stage_bytes = 0, ones_bytes = 0;
         int32_t code = DFMI_OK;
         std::string msg;
         try {
@@ -432,17 +451,12 @@ extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm*
                             if (r == c->rank && !p.src && p.fix != 2)
                                 throw Fail{DFMI_ERR_INVALID_ARGUMENT, "local output buffer is NULL"};
                             if (c->rank == root && p.fix >= 0) {  // staged on the root, fixed up after
-                                uint8_t* s = nullptr;
-                                HIP_TRY(hipMalloc((void**)&s, p.nb));
-                                stage.push_back(s);
-                                p.dst = s;
+                                p.dst = (void*)(uintptr_t)stage_bytes;  // an offset until the staging is sized
+                                stage_bytes += (p.nb + 255) & ~(size_t)255;
                             }
                             if (r == c->rank && p.fix == 2 && !p.src) {  // no validity here: all valid
-                                uint8_t* ones = nullptr;
-                                HIP_TRY(hipMalloc((void**)&ones, p.nb));
-                                stage.push_back(ones);
-                                HIP_TRY(hipMemsetAsync(ones, 0xff, p.nb, st));
-                                p.src = ones;
+                                ones_bytes = std::max(ones_bytes, p.nb);
+                                p.src = nullptr;  // the comm's all-valid bitmap (below)
                             }
                             pieces.push_back(p);
                         }
@@ -450,6 +464,26 @@ extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm*
                     row0 += n;
                     b0 += rec(r, 3 + o);
                 }
+            }
+            // the staging (root) and the all-valid bitmap, kept in the comm
+            if (stage_bytes > c->stage_cap) {
+                if (c->stage) HIP_TRY(hipFree(c->stage));
+                c->stage = nullptr;
+                c->stage_cap = 0;
+                HIP_TRY(hipMalloc((void**)&c->stage, stage_bytes));
+                c->stage_cap = stage_bytes;
+            }
+            if (ones_bytes > c->ones_cap) {
+                if (c->ones) HIP_TRY(hipFree(c->ones));
+                c->ones = nullptr;
+                c->ones_cap = 0;
+                HIP_TRY(hipMalloc((void**)&c->ones, ones_bytes));
+                HIP_TRY(hipMemsetAsync(c->ones, 0xff, ones_bytes, st));
+                c->ones_cap = ones_bytes;
+            }
+            for (Piece& p : pieces) {
+                if (c->rank == root && p.fix >= 0) p.dst = c->stage + (uintptr_t)p.dst;
+                if (p.r == c->rank && p.fix == 2 && !p.src) p.src = c->ones;
             }
             if (c->rank == root)  // bitmaps are ORed in: start from zero
                 for (int o = 0; o < nout; ++o) {
@@ -493,11 +527,9 @@ extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm*
             }
             HIP_TRY(hipStreamSynchronize(st));
         }
-        for (uint8_t* p : stage) (void)hipFree(p);
         return DFMI_OK;
     } catch (const Fail& f) {
         (void)hipStreamSynchronize(ctx->stream);
-        for (uint8_t* p : stage) (void)hipFree(p);
         set_err(err, f.code, f.msg);
         return f.code;
     }

@@ -1308,6 +1308,7 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
                 fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("aggregate over ") + type_name(args[j].t));
         }
         std::map<GroupKey, std::pair<uint64_t, std::vector<AggState>>> groups;
+        std::map<GroupKey, int64_t> rows_of;  // selected rows per group (keys[g].count)
         if (batch_rows <= 0) batch_rows = std::max<int64_t>(1, input->num_rows);
         for (int64_t r0 = 0; r0 < input->num_rows; r0 += batch_rows) {
             const int64_t rows = std::min(batch_rows, input->num_rows - r0);
@@ -1322,6 +1323,7 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
                 auto it = groups.find(gk);
                 if (it == groups.end()) it = groups.emplace(gk, std::make_pair(bits, proto)).first;
                 for (int j = 0; j < n; ++j) agg_accumulate_row(it->second.second[j], *av[j], i);
+                ++rows_of[gk];
             }
         }
         *num_groups = (int64_t)groups.size();
@@ -1331,7 +1333,7 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
             keys[g].type = key.t;
             keys[g].is_null = gk.null ? 1 : 0;
             keys[g].bits = v.first;
-            keys[g].count = 0;
+            keys[g].count = rows_of[gk];
             for (int j = 0; j < n; ++j) out[g * n + j] = agg_result(v.second[j]);
             ++g;
         }

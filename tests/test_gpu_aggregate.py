@@ -270,7 +270,7 @@ def run_grouped(schema, batch, pred, key, aggs, flags=AGG, batch_rows=0):
         assert (dev_err.kind, dev_err.message) == (ref_err.kind, ref_err.message)
         return None
     (dk, dv), (rk, rv) = dev, ref
-    assert [(k.type, k.is_null, k.bits) for k in dk] == [(k.type, k.is_null, k.bits) for k in rk]
+    assert [(k.type, k.is_null, k.bits, k.count) for k in dk] == [(k.type, k.is_null, k.bits, k.count) for k in rk]
     for g in range(len(rk)):
         for a, d, r in zip(aggs, dv[g], rv[g]):
             assert (d.type, d.is_null, d.count) == (r.type, r.is_null, r.count), (g, repr(a))

@@ -91,3 +91,43 @@ def test_relaunch_after_lookback_timeout(monkeypatch):
     assert L.dfmi_internal_relaunches(eng.ctx) == before + 1
     for d, (_, r) in zip(out, ref):
         assert_same(d.cpu(), r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("host", [False, True])
+def test_batches_relaunch_after_lookback_timeout(monkeypatch, host):
+    """The coalesced entry points (dfmi_filter_project_batches and its host
+    form) relaunch a launch whose look-back timed out once, over re-zeroed
+    workspace and batch headers, like the single-batch path: a forced
+    timeout still returns every batch's oracle result."""
+    import ctypes as C
+
+    from datafusion_amd import _abi
+    from datafusion_amd.arrow import Array, Field, RecordBatch, Schema
+    from datafusion_amd.execution.engine import engine
+    from datafusion_amd.execution.expression import compile_scalar_expr
+    from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Float64, Literal, Operator
+    from oracle_ffi import gen_unit_f64, oracle_filter_project
+    from test_gpu_parity import assert_same
+    s = Schema([Field(c, DataType.Float64, False) for c in "ab"])
+    bs = [RecordBatch(s, [Array.from_numpy(DataType.Float64, gen_unit_f64(9 + i, j, 0, n)) for j in range(2)])
+          for i, n in enumerate([1024, 70_000, 3, 1024])]
+    pred_e = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.5)))
+    proj_e = [Column(1), BinaryExpr(Column(0), Operator.Plus, Column(1))]
+    eng = engine()
+    L = _abi.lib()
+    L.dfmi_internal_relaunches.argtypes = [C.c_void_p]
+    L.dfmi_internal_relaunches.restype = C.c_long
+    before = L.dfmi_internal_relaunches(eng.ctx)
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_DEBUG_MODE", "16")
+    p, cp = compile_scalar_expr(None, pred_e, s), [compile_scalar_expr(None, e, s) for e in proj_e]
+    if host:
+        got, err = eng.filter_project_host_batches(p, cp, bs)
+    else:
+        got, err = eng.filter_project_batches(p, cp, [b.to(eng.device) for b in bs])
+    assert err is None, err
+    assert L.dfmi_internal_relaunches(eng.ctx) == before + 1
+    for b, g in zip(bs, got):
+        for d, (_, r) in zip(g, oracle_filter_project(s, b, pred_e, proj_e)):
+            assert_same(d.cpu(), r)

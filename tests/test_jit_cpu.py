@@ -220,3 +220,26 @@ def test_cast_and_is_null_kernels_compile():
     with pytest.raises(ExecutionError) as e:
         compile_scalar_expr(None, Cast(Column(0), DataType.Int64), sch)
     assert e.value.message == "column reference"
+
+
+@pytest.mark.parametrize("m", [2, 8])
+def test_numeric_subtile_kernel_compiles(m, monkeypatch):
+    """The low-selectivity form of a numeric predicate (exec.cpp kLowSel:
+    sub-tiles sharing one look-back, output pass reloading the selected rows'
+    columns), forced through the diagnostic knob; nullable inputs, a
+    fallible projection and a Q6-style 5-term predicate."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_NUMERIC_SUBTILES", str(m))
+    pred, projs = c2_query()
+    rc, code, msg, src = jit_check(F3, pred, projs, compile_=True)
+    assert rc > 0, msg
+    assert "constexpr int M = %d;" % m in src and "SLR" in src
+    e = BinaryExpr(BinaryExpr(Column(0), Operator.Lt, Literal(Int64(3))), Operator.And,
+                   BinaryExpr(Column(1), Operator.GtEq, Column(4)))
+    rc, code, msg, src = jit_check(S, e, [BinaryExpr(Column(4), Operator.Divide, Column(1)), Column(1), Column(2)],
+                                   compile_=True)
+    assert rc > 0, msg  # (Utf8 output: not a numeric sub-tile kernel, still compiles)
+    rc, code, msg, src = jit_check(S, e, [BinaryExpr(Column(4), Operator.Divide, Column(1)), Column(1)],
+                                   compile_=True)
+    assert rc > 0, msg
+    assert "constexpr int M = %d;" % m in src
