@@ -67,6 +67,7 @@ class dfmi_column(C.Structure):
         ("validity", C.c_void_p),
         ("values", C.c_void_p),
         ("offsets", C.c_void_p),
+        ("offset", C.c_int64),  # arrow ArrayData::offset (a sliced array)
     ]
 
 

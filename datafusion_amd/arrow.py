@@ -102,13 +102,24 @@ class Array:
 
     def __init__(self, data_type: DataType, length: int, values: torch.Tensor,
                  validity: Optional[torch.Tensor] = None, offsets: Optional[torch.Tensor] = None,
-                 null_count: int = 0):
+                 null_count: int = 0, offset: int = 0):
         self.data_type = DataType(data_type)
         self.length = int(length)
         self.values = values
         self.validity = validity if null_count else None
         self.offsets = offsets
         self.null_count = int(null_count)
+        # arrow ArrayData::offset: logical row i is physical slot offset + i
+        # (values, validity / Boolean bits, Utf8 offsets); dfmi_column.offset
+        self.offset = int(offset)
+
+    def slice(self, offset: int, length: int) -> "Array":
+        """Zero-copy slice (arrow Array::slice): same buffers, a larger offset."""
+        assert 0 <= offset and offset + length <= self.length
+        m = self.valid_mask()[offset:offset + length]
+        nulls = int(length - m.sum()) if self.validity is not None else 0
+        return Array(self.data_type, length, self.values, self.validity if nulls else None, self.offsets, nulls,
+                     self.offset + offset)
 
     def __len__(self):
         return self.length
@@ -120,33 +131,33 @@ class Array:
     def to(self, device) -> "Array":
         mv = lambda t: None if t is None else t.to(device)
         return Array(self.data_type, self.length, mv(self.values), mv(self.validity), mv(self.offsets),
-                     self.null_count)
+                     self.null_count, self.offset)
 
     def cpu(self) -> "Array":
         return self.to("cpu")
 
     def data_bytes(self) -> int:
         """Utf8: bytes referenced by the offsets."""
-        off = self.offsets[: self.length + 1].cpu().numpy()
+        off = self.offsets[self.offset: self.offset + self.length + 1].cpu().numpy()
         return int(off[-1] - off[0]) if self.length else 0
 
     # ---- host views -------------------------------------------------------
     def valid_mask(self) -> np.ndarray:
         if self.validity is None:
             return np.ones(self.length, dtype=bool)
-        return unpack_bits(self.validity.cpu().numpy(), self.length)
+        return unpack_bits(self.validity.cpu().numpy(), self.offset + self.length)[self.offset:]
 
     def numpy_values(self) -> np.ndarray:
         """Raw values (fixed width) / bools / list of bytes (Utf8)."""
         v = self.values.cpu().numpy()
-        t = self.data_type
+        t, o = self.data_type, self.offset
         if t == DataType.Boolean:
-            return unpack_bits(v, self.length)
+            return unpack_bits(v, o + self.length)[o:]
         if t == DataType.Utf8:
-            off = self.offsets.cpu().numpy()[: self.length + 1]
+            off = self.offsets.cpu().numpy()[o: o + self.length + 1]
             return [bytes(v[off[i]: off[i + 1]]) for i in range(self.length)]
         w = np.dtype(_NP[t]).itemsize
-        return v[: self.length * w].view(_NP[t])
+        return v[o * w: (o + self.length) * w].view(_NP[t])
 
     def to_pylist(self) -> list:
         vals = self.numpy_values()

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "exec_internal.h"
+#include "slice.h"
 #include "jit_skeleton.hip"
 
 using namespace dfmi;
@@ -587,6 +588,11 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
         if (st->failed) {
             if (err) *err = st->failure;
             return st->failure.code;
+        }
+        Unsliced us_;  // sliced arrays (arrow offsets): offset-0 views / shifted bitmaps (slice.cpp)
+        if (any_offset(in, 1)) {
+            HIP_TRY(hipSetDevice(ctx->device));
+            in = unslice(in, 1, us_, true, ctx->stream);
         }
         AggBuilt B;
         try {

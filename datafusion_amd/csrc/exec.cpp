@@ -36,6 +36,7 @@ using namespace dfmi;
 
 #include "exec_internal.h"
 #include "batch_stage.h"
+#include "slice.h"
 
 using namespace dfmi::xi;
 
@@ -440,6 +441,11 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         if (!ctx || !in || (np > 0 && !projs) || !outs || (in->num_columns > 0 && !in->columns))
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        Unsliced us_;  // sliced arrays (arrow offsets): offset-0 views / shifted bitmaps (slice.cpp)
+        if (any_offset(in, 1)) {
+            HIP_TRY(hipSetDevice(ctx->device));
+            in = unslice(in, 1, us_, true, ctx->stream);
+        }
         Built B;
         uint64_t hint_key = 0;
         if (pred && in->num_rows >= kSubtileMinRows) {
@@ -722,6 +728,11 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
         if (nb == 0) return DFMI_OK;
+        Unsliced us_;  // sliced arrays (slice.cpp)
+        if (any_offset(ins, nb)) {
+            HIP_TRY(hipSetDevice(ctx->device));
+            ins = unslice(ins, nb, us_, true, ctx->stream);
+        }
         const int ncols = ins[0].num_columns;
         const int nout = np > 0 ? np : ncols;
         int64_t maxn = 0;

@@ -41,6 +41,7 @@
 #include "dfmi_program.h"
 #include "jit.h"
 #include "batch_stage.h"
+#include "slice.h"
 
 using dfmi::Fail;
 
@@ -602,6 +603,8 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         *out = nullptr;
         dfmi::ctx_last_err_key(ctx) = ~0ull;
+        dfmi::Unsliced us_;  // sliced arrays (arrow offsets): offset-0 views / shifted bitmaps (slice.cpp)
+        if (dfmi::any_offset(in, 1)) in = dfmi::unslice(in, 1, us_, false, nullptr);
         const int64_t n = in->num_rows;
         const int ncols = in->num_columns;
         if (n < 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "negative row count"};
@@ -1177,6 +1180,8 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         *out = nullptr;
         dfmi::ctx_last_err_key(ctx) = ~0ull;
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        dfmi::Unsliced us_;  // sliced arrays (slice.cpp)
+        if (nb > 0 && dfmi::any_offset(ins, nb)) ins = dfmi::unslice(ins, nb, us_, false, nullptr);
         HIP_TRY(hipSetDevice(dfmi::ctx_device(ctx)));
         hipStream_t st = dfmi::ctx_stream(ctx);
         Arena& A = arena_of(ctx);

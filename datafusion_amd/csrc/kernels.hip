@@ -157,6 +157,28 @@ __global__ void k_place_bits(const uint8_t* src, i64 n, unsigned* dst, i64 dst_b
     }
 }
 
+// ------------------------------------------- sliced arrays (slice.cpp) ---
+// dst word i = bits [bit0 + 64 i, bit0 + 64 i + 64) of src (src_bytes bytes
+// readable): a bitmap at an arrow array offset moved to bit 0.
+__global__ void k_shift_bits(const uint8_t* src, i64 bit0, i64 src_bytes, u64* dst, i64 nwords) {
+    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += (i64)gridDim.x * blockDim.x) {
+        const i64 b = bit0 + i * 64, byte = b >> 3;
+        const int sh = (int)(b & 7);
+        u64 lo = 0, hi = 0;
+        for (int k = 0; k < 8; ++k)
+            if (byte + k < src_bytes) lo |= (u64)src[byte + k] << (8 * k);
+        if (sh && byte + 8 < src_bytes) hi = src[byte + 8];
+        dst[i] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    }
+}
+
+hipError_t launch_shift_bits(const uint8_t* src, i64 bit0, i64 nbits, uint8_t* dst, hipStream_t st) {
+    const i64 nw = (nbits + 63) / 64;
+    const int grid = (int)std::max<i64>(1, std::min<i64>((nw + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_shift_bits, dim3(grid), dim3(256), 0, st, src, bit0, (bit0 + nbits + 7) / 8, (u64*)dst, nw);
+    return hipGetLastError();
+}
+
 hipError_t launch_rebase_offsets(const int32_t* src, i64 n, i64 base, int32_t* dst, hipStream_t st) {
     const int grid = (int)std::max<i64>(1, std::min<i64>((n + 256) / 256, 4096));
     hipLaunchKernelGGL(k_rebase_offsets, dim3(grid), dim3(256), 0, st, src, n, base, dst);

@@ -6,8 +6,8 @@
  * (dfmi_column per column, dfmi_batch per batch, include/dfmi.h) from the
  * Python Array objects costs ~1 us per column in Python; this module walks
  * the same objects through the CPython API instead. It reads, per Array:
- * data_type, length, null_count and the data_ptr() of its values / validity
- * / offsets tensors -- exactly what engine.column_struct() reads -- and
+ * data_type, length, null_count, offset and the data_ptr() of its values /
+ * validity / offsets tensors -- exactly what engine.column_struct() reads -- and
  * refuses any column whose buffers are not in host memory.
  */
 #define PY_SSIZE_T_CLEAN
@@ -19,6 +19,7 @@ typedef struct {
     int32_t type, reserved;
     int64_t length, null_count;
     uint64_t validity, values, offsets;
+    int64_t offset;
 } col_rec; /* dfmi_column */
 
 typedef struct {
@@ -28,7 +29,7 @@ typedef struct {
 } batch_rec; /* dfmi_batch */
 
 static PyObject *s_columns, *s__columns, *s_data_type, *s_length, *s_null_count, *s_validity, *s_values,
-    *s_offsets, *s_data_ptr, *s_is_cpu;
+    *s_offsets, *s_offset, *s_data_ptr, *s_is_cpu;
 
 static int get_i64(PyObject* o, PyObject* name, int64_t* out) {
     PyObject* v = PyObject_GetAttr(o, name);
@@ -112,7 +113,8 @@ static PyObject* pack_host_batches(PyObject* self, PyObject* args) {
             memset(&r[i], 0, sizeof r[i]);
             if (get_i64(a, s_data_type, &t) || get_i64(a, s_length, &r[i].length) ||
                 get_i64(a, s_null_count, &r[i].null_count) || get_ptr(a, s_validity, &r[i].validity) ||
-                get_ptr(a, s_values, &r[i].values) || get_ptr(a, s_offsets, &r[i].offsets)) {
+                get_ptr(a, s_values, &r[i].values) || get_ptr(a, s_offsets, &r[i].offsets) ||
+                get_i64(a, s_offset, &r[i].offset)) {
                 Py_DECREF(cseq);
                 goto done;
             }
@@ -151,6 +153,7 @@ PyMODINIT_FUNC PyInit__dfmi_glue(void) {
     INTERN(s_validity, "validity");
     INTERN(s_values, "values");
     INTERN(s_offsets, "offsets");
+    INTERN(s_offset, "offset");
     INTERN(s_data_ptr, "data_ptr");
     INTERN(s_is_cpu, "is_cpu");
     return PyModule_Create(&module);

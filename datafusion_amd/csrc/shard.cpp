@@ -342,7 +342,8 @@ extern "C" int32_t dfmi_shard_filter_project(dfmi_context* ctx, dfmi_shard_comm*
                 for (int o = 0; o < nout; ++o)
                     if (outs[o].type == DFMI_TYPE_UTF8 && outs[o].passthrough_column >= 0 && outs[o].length > 0) {
                         if (!c->pin) HIP_TRY(hipHostMalloc((void**)&c->pin, 2 * kMaxOut * 4, hipHostMallocDefault));
-                        const int32_t* of = in->columns[outs[o].passthrough_column].offsets;
+                        const dfmi_column& pc = in->columns[outs[o].passthrough_column];
+                        const int32_t* of = pc.offsets + pc.offset;  // (a sliced array's first offset)
                         HIP_TRY(hipMemcpyAsync(&c->pin[2 * o], of, 4, hipMemcpyDeviceToHost, ctx->stream));
                         HIP_TRY(hipMemcpyAsync(&c->pin[2 * o + 1], of + outs[o].length, 4, hipMemcpyDeviceToHost, ctx->stream));
                         spans = true;

@@ -38,6 +38,7 @@ def column_struct(a: Array) -> _abi.dfmi_column:
     c.validity = a.validity.data_ptr() if a.validity is not None else None
     c.values = a.values.data_ptr()
     c.offsets = a.offsets.data_ptr() if a.offsets is not None else None
+    c.offset = a.offset
     return c
 
 
@@ -604,7 +605,7 @@ def _host_result_arrays(res) -> List[Array]:
 # ---- host batches: vectorised ABI structs in, zero-copy result slices out
 
 _COL_DTYPE = np.dtype([("type", "<i4"), ("reserved", "<i4"), ("length", "<i8"), ("null_count", "<i8"),
-                       ("validity", "<u8"), ("values", "<u8"), ("offsets", "<u8")])
+                       ("validity", "<u8"), ("values", "<u8"), ("offsets", "<u8"), ("offset", "<i8")])
 _BATCH_DTYPE = np.dtype([("num_columns", "<i4"), ("reserved", "<i4"), ("num_rows", "<i8"), ("columns", "<u8")])
 assert _COL_DTYPE.itemsize == C.sizeof(_abi.dfmi_column) and _BATCH_DTYPE.itemsize == C.sizeof(_abi.dfmi_batch)
 

@@ -87,6 +87,11 @@ typedef struct dfmi_column {
     const uint8_t* validity; /* NULL => all valid */
     const void* values;
     const int32_t* offsets;  /* Utf8 only */
+    /* arrow 0.12 ArrayData::offset (a sliced array): logical row i is physical
+     * slot offset + i -- values[offset + i], validity / Boolean bit offset + i,
+     * Utf8 offsets[offset + i] -- as value(i) / is_null(i) read it
+     * (filter.rs:88-89,99-100). 0 for an unsliced array. */
+    int64_t offset;
 } dfmi_column;
 
 typedef struct dfmi_batch {

@@ -232,9 +232,18 @@ struct Array {
     const int32_t* offsets = nullptr;
     std::vector<uint8_t> own_validity, own_values, own_data;
     std::vector<int32_t> own_offsets;
+    // arrow ArrayData offset (< 8 after wrap_input's byte shift) of the
+    // bitmaps: validity and Boolean values read bit bit_off + i
+    int64_t bit_off = 0;
 
-    bool is_null(int64_t i) const { return validity && !((validity[i >> 3] >> (i & 7)) & 1); }
-    bool bool_value(int64_t i) const { return (values[i >> 3] >> (i & 7)) & 1; }
+    bool is_null(int64_t i) const {
+        const int64_t j = i + bit_off;
+        return validity && !((validity[j >> 3] >> (j & 7)) & 1);
+    }
+    bool bool_value(int64_t i) const {
+        const int64_t j = i + bit_off;
+        return (values[j >> 3] >> (j & 7)) & 1;
+    }
     template <typename T> T value(int64_t i) const {
         T v;
         memcpy(&v, values + i * (int64_t)sizeof(T), sizeof(T));
@@ -840,18 +849,22 @@ Batch wrap_input(const dfmi_batch* in, int64_t row0, int64_t rows) {
         auto a = std::make_shared<Array>();
         a->type = c.type;
         a->len = rows;
-        if (row0 & 7) fail(DFMI_ERR_INVALID_ARGUMENT, "batch slices must start at a multiple of 8 rows");
+        // logical row i of the column is physical slot offset + i (arrow
+        // ArrayData::offset, which value(i) / is_null(i) honour)
+        if (c.offset < 0) fail(DFMI_ERR_INVALID_ARGUMENT, "negative array offset");
+        const int64_t r0 = row0 + c.offset;
         const int w = type_width(c.type);
         a->values = (const uint8_t*)c.values;
+        a->bit_off = r0 & 7;
         if (c.type == DFMI_TYPE_UTF8) {
-            a->offsets = c.offsets + row0;
+            a->offsets = c.offsets + r0;
         } else if (c.type == DFMI_TYPE_BOOLEAN) {
-            a->values += row0 / 8;
+            a->values += r0 / 8;
         } else {
-            a->values += row0 * w;
+            a->values += r0 * w;
         }
         if (c.validity) {
-            a->validity = c.validity + row0 / 8;
+            a->validity = c.validity + r0 / 8;
             int64_t nc = 0;
             for (int64_t r = 0; r < rows; ++r) nc += a->is_null(r);
             a->null_count = nc;
@@ -1215,6 +1228,7 @@ int32_t oracle_result_column(const oracle_result* r, int32_t i, dfmi_column* v, 
     v->validity = a.null_count ? a.validity : nullptr;
     v->values = a.values;
     v->offsets = a.offsets;
+    v->offset = a.bit_off;  // (a passed-through input column keeps its bit offset)
     if (name) *name = r->names[i].c_str();
     return DFMI_OK;
 }

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from datafusion_amd import _abi
-from datafusion_amd.arrow import Array, Field, RecordBatch, Schema, _bytes_tensor, _offsets_tensor
+from datafusion_amd.arrow import Array, Field, RecordBatch, Schema, _bytes_tensor, _offsets_tensor, pack_bits, unpack_bits
 from datafusion_amd.logicalplan import DataType, Expr
 from datafusion_amd.execution.error import ExecutionError
 
@@ -69,6 +69,7 @@ def _host_column(a: Array) -> _abi.dfmi_column:
     c.validity = a.validity.data_ptr() if a.validity is not None else None
     c.values = a.values.data_ptr()
     c.offsets = a.offsets.data_ptr() if a.offsets is not None else None
+    c.offset = a.offset
     return c
 
 
@@ -82,13 +83,21 @@ def _copy_out(col: _abi.dfmi_column) -> Array:
         values = _bytes_tensor(data)
         offsets = _offsets_tensor(offs, "cpu")
     else:
-        nbytes = (n + 7) // 8 if t == DataType.Boolean else n * t.width
+        # the oracle's views: buffers start at the slice, bitmaps may start at
+        # bit `offset` (< 8) of their first byte (a passed-through sliced input)
+        bo = col.offset if t == DataType.Boolean else 0
+        nbytes = (bo + n + 7) // 8 if t == DataType.Boolean else n * t.width
         raw = np.ctypeslib.as_array(C.cast(col.values, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes].copy()
+        if bo:
+            raw = pack_bits(unpack_bits(raw, bo + n)[bo:])
         values = _bytes_tensor(raw)
         offsets = None
     validity = None
     if col.null_count:
-        vb = np.ctypeslib.as_array(C.cast(col.validity, C.POINTER(C.c_uint8)), shape=((n + 7) // 8,)).copy()
+        vo = col.offset
+        vb = np.ctypeslib.as_array(C.cast(col.validity, C.POINTER(C.c_uint8)), shape=((vo + n + 7) // 8,)).copy()
+        if vo:
+            vb = pack_bits(unpack_bits(vb, vo + n)[vo:])
         validity = _bytes_tensor(vb)
     return Array(t, n, values, validity, offsets, col.null_count)
 

@@ -36,7 +36,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_match_header():
     # layout of the ABI structs (x86-64 / LP64)
-    assert C.sizeof(_abi.dfmi_column) == 48
+    assert C.sizeof(_abi.dfmi_column) == 56
     assert C.sizeof(_abi.dfmi_batch) == 24
     assert C.sizeof(_abi.dfmi_expr_node) == 48
     assert C.sizeof(_abi.dfmi_out_column) == 72
