@@ -11,12 +11,14 @@
 // host merges the accumulator copies exactly and rounds once at the end.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "exec_internal.h"
@@ -396,6 +398,194 @@ void flush_groups(dfmi_context* ctx, dfmi_agg_state* st) {
     st->dirty = false;
 }
 
+// ---- GROUP BY over keys wider than the device window: the host merge.
+// One value (row i, non-null) of aggregate `a` into p -- the per-row rules
+// of the aggregate kernels (jit.cpp generate_agg / generate_agg_grouped,
+// jit_skeleton.hip agg_key / agg_sum_flags / fsum_add), restated on the host.
+template <typename T>
+uint64_t host_agg_key(T v) {
+    if constexpr (std::is_same<T, float>::value) {
+        uint32_t b;
+        memcpy(&b, &v, 4);
+        return (b >> 31) ? (uint64_t)(~b) : (uint64_t)(b | 0x80000000u);
+    } else if constexpr (std::is_same<T, double>::value) {
+        uint64_t b;
+        memcpy(&b, &v, 8);
+        return (b >> 63) ? ~b : (b | (1ull << 63));
+    } else if constexpr (std::is_signed<T>::value) {
+        return (uint64_t)(int64_t)v ^ (1ull << 63);
+    } else {
+        return (uint64_t)v;
+    }
+}
+
+void host_fsum_add(Partial& p, double v) {  // finite, non-zero v (fsum_add's digit split)
+    uint64_t b;
+    memcpy(&b, &v, 8);
+    const int e = (int)((b >> 52) & 0x7ff);
+    const uint64_t m = (b & ((1ull << 52) - 1)) | (e ? (1ull << 52) : 0ull);
+    const int pos = (e ? e : 1) - 1;
+    const int d = pos >> 5, sh = pos & 31;
+    const uint64_t x0 = (m & 0xffffffffull) << sh, x1 = (m >> 32) << sh;
+    int64_t c0 = (int64_t)(x0 & 0xffffffffull);
+    int64_t c1 = (int64_t)((x0 >> 32) + (x1 & 0xffffffffull));
+    int64_t c2 = (int64_t)(x1 >> 32);
+    if (b >> 63) {
+        c0 = -c0;
+        c1 = -c1;
+        c2 = -c2;
+    }
+    p.limbs[d] += c0;
+    p.limbs[d + 1] += c1;
+    p.limbs[d + 2] += c2;
+}
+
+template <typename T>
+void host_accumulate_t(Partial& p, int fn, T v) {
+    ++p.count;
+    if (fn == DFMI_AGG_COUNT) return;
+    if (fn == DFMI_AGG_SUM) {
+        if constexpr (std::is_floating_point<T>::value) {
+            const unsigned f = v != v ? AGGF_NAN
+                                      : (std::isinf(v) ? (v > 0 ? AGGF_PINF : AGGF_NINF)
+                                                       : ((v == 0 && std::signbit(v)) ? 0u : AGGF_NONNEGZERO));
+            p.flags |= f;
+            if (f == AGGF_NONNEGZERO && v != 0) host_fsum_add(p, (double)v);
+        } else {
+            p.isum += std::is_signed<T>::value ? (uint64_t)(int64_t)v : (uint64_t)v;
+        }
+        return;
+    }
+    // MIN / MAX
+    if constexpr (std::is_floating_point<T>::value)
+        if (v != v) {
+            p.flags |= AGGF_NAN;
+            return;
+        }
+    const uint64_t k = host_agg_key(v);
+    if (!(p.flags & AGGF_VALUE)) p.key = k;
+    else p.key = fn == DFMI_AGG_MIN ? std::min(p.key, k) : std::max(p.key, k);
+    p.flags |= AGGF_VALUE;
+}
+
+void host_accumulate(Partial& p, int fn, int t, const uint8_t* vals, int64_t i) {
+    switch (t) {
+        case DFMI_TYPE_INT8: return host_accumulate_t(p, fn, ((const int8_t*)vals)[i]);
+        case DFMI_TYPE_INT16: return host_accumulate_t(p, fn, ((const int16_t*)vals)[i]);
+        case DFMI_TYPE_INT32: return host_accumulate_t(p, fn, ((const int32_t*)vals)[i]);
+        case DFMI_TYPE_INT64: return host_accumulate_t(p, fn, ((const int64_t*)vals)[i]);
+        case DFMI_TYPE_UINT8: return host_accumulate_t(p, fn, ((const uint8_t*)vals)[i]);
+        case DFMI_TYPE_UINT16: return host_accumulate_t(p, fn, ((const uint16_t*)vals)[i]);
+        case DFMI_TYPE_UINT32: return host_accumulate_t(p, fn, ((const uint32_t*)vals)[i]);
+        case DFMI_TYPE_UINT64: return host_accumulate_t(p, fn, ((const uint64_t*)vals)[i]);
+        case DFMI_TYPE_FLOAT32: return host_accumulate_t(p, fn, ((const float*)vals)[i]);
+        case DFMI_TYPE_FLOAT64: return host_accumulate_t(p, fn, ((const double*)vals)[i]);
+        default: ++p.count;  // COUNT of a Boolean / Utf8 argument: non-null values only
+    }
+}
+
+// A batch whose selected keys span more than the device window: the key and
+// every argument evaluated on the device as one fused Selection + Projection
+// pass (dfmi_filter_project: projections [key, args...] -- the same
+// evaluation order, ordinals and errors as the grouped kernel), the
+// compacted columns copied back, and each row merged into its group on the
+// host with the kernels' per-row rules.
+void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in,
+                         uint32_t flags) {
+    const size_t n = st->aggs.size();
+    const int no = (int)n + 1;
+    const int64_t rows = in->num_rows;
+    std::vector<const dfmi_program*> progs(no);
+    progs[0] = &st->key;
+    for (size_t j = 0; j < n; ++j) progs[j + 1] = &st->aggs[j]->arg;
+    std::vector<dfmi_out_column> outs(no);
+    std::vector<void*> dev;
+    struct Free {
+        std::vector<void*>& v;
+        ~Free() {
+            for (void* p : v) (void)hipFree(p);
+        }
+    } free_{dev};
+    auto dalloc = [&](size_t b) {
+        void* p = nullptr;
+        HIP_TRY(hipMalloc(&p, std::max<size_t>(b, 64)));
+        dev.push_back(p);
+        return p;
+    };
+    for (int o = 0; o < no; ++o) {
+        dfmi_out_column& c = outs[o];
+        memset(&c, 0, sizeof c);
+        const int t = progs[o]->type;
+        if (t == DFMI_TYPE_UTF8) {
+            const IrNode& root = progs[o]->ir[progs[o]->root];
+            size_t cap = 8;
+            if (root.kind == IR_COL && root.col >= 0 && root.col < in->num_columns && in->columns[root.col].offsets) {
+                int32_t last = 0;
+                HIP_TRY(hipMemcpy(&last, in->columns[root.col].offsets + rows, 4, hipMemcpyDeviceToHost));
+                cap = std::max<size_t>(cap, (size_t)std::max(0, last));
+            }
+            c.offsets = (int32_t*)dalloc((size_t)(rows + 1) * 4);
+            c.data = (uint8_t*)dalloc(cap);
+            c.data_capacity = (int64_t)cap;
+        } else {
+            const int w = jit::type_width(t);
+            c.values = dalloc(t == DFMI_TYPE_BOOLEAN ? (size_t)(rows + 63) / 64 * 8 : (size_t)rows * std::max(w, 1));
+        }
+        c.validity = (uint8_t*)dalloc((size_t)(rows + 63) / 64 * 8);
+    }
+    dfmi_error e{};
+    if (dfmi_filter_project(ctx, pred, progs.data(), no, in, outs.data(), flags, &e) != DFMI_OK) {
+        st->failed = true;
+        st->failure = e;
+        throw Fail{e.code, e.message};
+    }
+    const int64_t m = outs[0].length;  // selected rows
+    // host copies of values (fixed width) and validity
+    std::vector<std::vector<uint8_t>> hv(no), hb(no);
+    for (int o = 0; o < no; ++o) {
+        const dfmi_out_column& c = outs[o];
+        const int t = progs[o]->type;
+        const dfmi_column* src = c.passthrough_column >= 0 ? &in->columns[c.passthrough_column] : nullptr;
+        const int w = jit::type_width(t);
+        const size_t vb = t == DFMI_TYPE_BOOLEAN ? (size_t)(m + 7) / 8 : (size_t)m * w;
+        if (vb && t != DFMI_TYPE_UTF8) {
+            hv[o].resize(vb);
+            HIP_TRY(hipMemcpy(hv[o].data(), src ? src->values : c.values, vb, hipMemcpyDeviceToHost));
+        }
+        const uint8_t* vsrc = src ? (src->null_count > 0 ? src->validity : nullptr) : (c.null_count > 0 ? c.validity : nullptr);
+        if (vsrc && m) {
+            hb[o].resize((size_t)(m + 7) / 8);
+            HIP_TRY(hipMemcpy(hb[o].data(), vsrc, hb[o].size(), hipMemcpyDeviceToHost));
+        }
+    }
+    auto valid = [&](int o, int64_t i) { return hb[o].empty() || ((hb[o][i >> 3] >> (i & 7)) & 1); };
+    const int kt = st->key.type;
+    for (int64_t i = 0; i < m; ++i) {
+        dfmi_agg_state::HKey hk{!valid(0, i), 0};
+        uint64_t bits = 0;
+        if (!hk.null) {
+            if (kt == DFMI_TYPE_BOOLEAN) {
+                bits = (hv[0][i >> 3] >> (i & 7)) & 1;
+                hk.ord = (__int128)bits;
+            } else {
+                const int w = jit::type_width(kt);
+                uint64_t raw = 0;
+                memcpy(&raw, hv[0].data() + (size_t)i * w, w);
+                bits = is_signed_type(kt) ? (uint64_t)(int64_t)narrow_int(raw, kt) : narrow_int(raw, kt);
+                hk.ord = is_signed_type(kt) ? (__int128)(int64_t)bits : (__int128)bits;
+            }
+        }
+        auto it = st->groups.find(hk);
+        if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(n + 1))).first;
+        std::vector<Partial>& g = it->second.second;
+        ++g[n].count;  // the group's selected rows
+        for (size_t j = 0; j < n; ++j)
+            if (valid((int)j + 1, i)) host_accumulate(g[j], st->aggs[j]->fn, progs[j + 1]->type, hv[j + 1].data(), i);
+    }
+    for (auto& kv : st->groups)
+        for (Partial& p : kv.second.second) normalize(p);
+}
+
 }  // namespace
 
 extern "C" int32_t dfmi_compile_aggregate(const char* name, const dfmi_program* arg, int32_t return_type,
@@ -628,9 +818,14 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
                     wbase = st->win_base;
                 } else {
                     wbase = mm[0].count ? mm[0].bits : 0;
-                    if (mm[0].count && mm[1].bits - mm[0].bits >= (uint64_t)wwidth)
-                        throw Fail{DFMI_ERR_NOT_IMPLEMENTED,
-                                   "GROUP BY: more than 16 consecutive key values in one batch"};
+                    if (mm[0].count && mm[1].bits - mm[0].bits >= (uint64_t)wwidth) {
+                        // wider than the device window: the host merge (its
+                        // fused pass raises the same first error in the same
+                        // evaluation order as the grouped kernel would)
+                        flush_groups(ctx, st);
+                        group_batch_on_host(ctx, st, pred, in, flags);
+                        return DFMI_OK;
+                    }
                 }
             }
             if (st->win_width != wwidth || st->win_base != wbase) {

@@ -333,10 +333,11 @@ def test_group_by_random_keys():
 
 
 def test_group_by_errors():
-    """A batch whose selected keys span more than 16 consecutive values is
-    NotImplemented on the device (the oracle has no such limit: only the
-    device raises); an error in the key expression is raised by both, before
-    any aggregate's, in the reference's evaluation order."""
+    """A batch whose selected keys span more than the device's 16-value window
+    is merged on the host (aggregate.cpp group_batch_on_host) with the
+    kernel's rules: the oracle's groups; an error in the key expression is
+    raised by both, before any aggregate's, in the reference's evaluation
+    order -- in the window path and in the wide one."""
     n = 4096
     s = Schema([Field("k", DataType.Int64, False), Field("d", DataType.Int64, False), Field("x", DataType.Float64, False)])
     k = np.arange(n, dtype=np.int64) % 40
@@ -344,14 +345,45 @@ def test_group_by_errors():
     d[1000] = 0
     b = RecordBatch(s, [Array.from_numpy(DataType.Int64, k), Array.from_numpy(DataType.Int64, d),
                         Array.from_numpy(DataType.Float64, np.arange(n, dtype=np.float64))])
-    cs = [compile_expr(None, agg("SUM", Column(2), s), s, AGG)]
-    st = engine().grouped_agg_state(compile_scalar_expr(None, Column(0), s, AGG), cs)
-    with pytest.raises(ExecutionError) as e:
-        st.add(None, b.to(engine().device), AGG)
-    assert e.value.kind == "NotImplemented"
+    out = run_grouped(s, b, None, Column(0), [agg("SUM", Column(2), s), agg("MIN", Column(1), s)])
+    assert out is not None and len(out[0]) == 40
     # key = k / d: DivideByZero at row 1000, before the aggregate's own error
     key = BinaryExpr(Column(0), Operator.Divide, Column(1))
     bad = [agg("SUM", BinaryExpr(Column(2), Operator.Divide, Literal(Float64(0.0))), s)]
     pred = BinaryExpr(Column(0), Operator.Lt, Literal(Int64(10)))
     run_grouped(s, b, pred, key, bad)
     run_grouped(s, b, pred, Column(0), bad)
+    wide = BinaryExpr(Column(0), Operator.Lt, Literal(Int64(30)))  # 30 key values: the host merge
+    assert run_grouped(s, b, wide, key, bad) is None
+    assert run_grouped(s, b, wide, Column(0), bad) is None
+
+
+@pytest.mark.parametrize("batch_rows", [0, 7000])
+def test_group_by_random_keys_wide(batch_rows):
+    """10,000 distinct Int64 keys (and Int32 / UInt16 keys spanning thousands
+    of values), nullable keys and arguments, with and without a predicate,
+    over one batch or many: every batch is wider than the device window, so
+    every row goes through the host merge -- bit-exact against the oracle:
+    exact float SUM, MIN/MAX (NaN, -0.0), COUNT, wrapping integer SUM, and
+    the per-group row counts."""
+    rng = np.random.default_rng(21)
+    n = 60_001
+    s = Schema([Field("k64", DataType.Int64, True), Field("k32", DataType.Int32, False),
+                Field("ku16", DataType.UInt16, False), Field("x", DataType.Float64, True),
+                Field("f", DataType.Float32, True), Field("v", DataType.Int64, True)])
+    keys = rng.integers(-5000, 5000, n).astype(np.int64)
+    cols = [Array.from_numpy(DataType.Int64, keys, rng.random(n) >= 0.01),
+            Array.from_numpy(DataType.Int32, rng.integers(-2 ** 31, 2 ** 31 - 1, n).astype(np.int32) // 1_000_000),
+            Array.from_numpy(DataType.UInt16, rng.integers(0, 65535, n).astype(np.uint16)),
+            Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.1),
+            Array.from_numpy(DataType.Float32, rng.standard_normal(n).astype(np.float32), rng.random(n) >= 0.1),
+            Array.from_numpy(DataType.Int64, rng.integers(-2 ** 62, 2 ** 62, n).astype(np.int64), rng.random(n) >= 0.1)]
+    b = RecordBatch(s, cols)
+    aggs = [agg("SUM", Column(3), s), agg("MIN", Column(3), s), agg("MAX", Column(4), s), agg("COUNT", Column(3), s),
+            agg("SUM", Column(5), s), agg("SUM", Column(4), s)]
+    pred = BinaryExpr(Column(3), Operator.Lt, Literal(Float64(0.8)))
+    fl = AGG | _abi.DFMI_FLAG_EXT_GATHER_ALL
+    for c in range(3):
+        for p in (None, pred):
+            out = run_grouped(s, b, p, Column(c), aggs, fl, batch_rows=batch_rows)
+            assert out is not None and len(out[0]) > 1000
