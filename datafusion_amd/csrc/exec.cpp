@@ -268,10 +268,11 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         // the numeric sub-tile kernel at any size (parity tests, A/B runs)
+        // (1: the one-tile kernel even where the selectivity hint picks sub-tiles)
         if (const char* e = getenv("DFMI_NUMERIC_SUBTILES"))
-            if (atoi(e) > 1 && pred && !X.pred_slots.empty() && X.utf8_cols.empty()) {
-                X.BLOCK = 256;
-                X.M = std::min(8, atoi(e));
+            if (pred && !X.pred_slots.empty() && X.utf8_cols.empty()) {
+                X.BLOCK = atoi(e) > 1 ? 256 : 512;
+                X.M = std::max(1, std::min(8, atoi(e)));
             }
         if (const char* e = getenv("DFMI_OUT_SLICES")) X.KO = atoi(e);
         if (const char* e = getenv("DFMI_SUBTILE_PREFETCH")) X.prefetch = atoi(e) & 1;

@@ -28,11 +28,11 @@ from oracle_ffi import oracle_filter_project
 torch.cuda.set_device(0)
 (torch.zeros(1, device="cuda") + 1).sum().item()  # runtime initialised before the timed call
 eng = engine("cuda:0")
-s = Schema([Field("a", DataType.Float64, True), Field("b", DataType.Int32, False), Field("c", DataType.Float64, False)])
+s = Schema([Field("a", DataType.Float64, True), Field("b", DataType.Float64, False), Field("c", DataType.Float64, False)])
 rng = np.random.default_rng(3)
 n = 50_000
 b = RecordBatch(s, [Array.from_numpy(DataType.Float64, rng.random(n), rng.random(n) > 0.1),
-                    Array.from_numpy(DataType.Int32, rng.integers(-9, 9, n).astype(np.int32)),
+                    Array.from_numpy(DataType.Float64, rng.standard_normal(n)),
                     Array.from_numpy(DataType.Float64, rng.random(n))])
 db = b.to("cuda:0")
 pred = BinaryExpr(BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.61))), Operator.Or,
