@@ -103,7 +103,7 @@ class Array:
     def __init__(self, data_type: DataType, length: int, values: torch.Tensor,
                  validity: Optional[torch.Tensor] = None, offsets: Optional[torch.Tensor] = None,
                  null_count: int = 0, offset: int = 0):
-        self.data_type = DataType(data_type)
+        self.data_type = data_type if type(data_type) is DataType else DataType(data_type)
         self.length = int(length)
         self.values = values
         self.validity = validity if null_count else None

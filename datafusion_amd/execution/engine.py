@@ -659,7 +659,7 @@ class HostResultBlock:
         views = np.zeros(max(1, ncols), dtype=_COL_DTYPE)
         if ncols:
             L.dfmi_host_result_columns(res, 0, ncols, views.ctypes.data)
-        self.type = views["type"].tolist()
+        self.type = [DataType(t) for t in views["type"].tolist()]
         self.length = views["length"].tolist()
         self.nulls = views["null_count"].tolist()
         self.validity = views["validity"].tolist()
@@ -712,7 +712,7 @@ class HostBatchColumns(LazyColumns):
         k = self.blk
         out = []
         for i in range(self.b * self.num_columns, (self.b + 1) * self.num_columns):
-            t = DataType(k.type[i])
+            t = k.type[i]
             n = k.length[i]
             nulls = k.nulls[i]
             if t == DataType.Utf8:

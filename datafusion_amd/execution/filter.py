@@ -1,7 +1,8 @@
 """FilterRelation (src/execution/filter.rs:30-111) on the MI355X path."""
 from __future__ import annotations
 
-from typing import Callable, List, Optional
+from collections import deque
+from typing import Callable, Optional
 
 from ..arrow import RecordBatch, Schema
 from .engine import engine
@@ -44,8 +45,8 @@ class Coalescer:
         self.m, self.source, self.max_rows = m, source, max_rows
         self.run_one, self.run_many, self.run_many_host, self.wrap = run_one, run_many, run_many_host, wrap
         self.run_many_host_async = run_many_host_async
-        self.ready: List = []      # RecordBatches / exceptions, in stream order
-        self.pending: List = []    # pulled input batches (or a source error) still to run one by one
+        self.ready = deque()       # RecordBatches / exceptions, in stream order
+        self.pending = deque()     # pulled input batches (or a source error) still to run one by one
         self.ahead = None          # the next group read ahead: (future or None, batches, source error)
 
     def _read_ahead(self):
@@ -108,7 +109,7 @@ class Coalescer:
     def next(self) -> Optional[RecordBatch]:
         while not self.ready:
             if self.pending:
-                item = self.pending.pop(0)
+                item = self.pending.popleft()
                 if isinstance(item, Exception):
                     raise item
                 return self.wrap(self.run_one(item))
@@ -127,7 +128,7 @@ class Coalescer:
                 self.pending.append(src_err)
             elif not self.pending and self.run_many_host_async is not None:
                 self.ahead = self._fetch()  # the next group runs while this one is handed out
-        item = self.ready.pop(0)
+        item = self.ready.popleft()
         if isinstance(item, Exception):
             raise item
         return item
