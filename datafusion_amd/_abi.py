@@ -168,12 +168,16 @@ EXPORTED = [
     "dfmi_agg_state_reset",
     "dfmi_agg_state_create_grouped",
     "dfmi_agg_state_finish_grouped",
+    "dfmi_agg_state_grouped_partial_bytes",
+    "dfmi_agg_state_grouped_partial",
+    "dfmi_agg_merge_grouped_partials",
     "dfmi_shard_unique_id",
     "dfmi_shard_comm_init",
     "dfmi_shard_comm_destroy",
     "dfmi_shard_filter_project",
     "dfmi_shard_gather_to_root",
     "dfmi_shard_agg_finish",
+    "dfmi_shard_agg_finish_grouped",
     "dfmi_agg_state_free",
     "dfmi_generate_column",  # include/dfmi_datasource.h
     "dfmi_csv_open",
@@ -352,6 +356,17 @@ def lib() -> C.CDLL:
     L.dfmi_shard_agg_finish.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_void_p), C.c_int32,
                                         P(dfmi_agg_value), P(dfmi_error)]
     L.dfmi_shard_agg_finish.restype = C.c_int32
+    L.dfmi_shard_agg_finish_grouped.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_void_p), C.c_int32, C.c_int64,
+                                                P(dfmi_agg_value), P(dfmi_agg_value), P(C.c_int64), P(dfmi_error)]
+    L.dfmi_shard_agg_finish_grouped.restype = C.c_int32
+    L.dfmi_agg_state_grouped_partial_bytes.argtypes = [C.c_void_p, C.c_void_p, P(dfmi_error)]
+    L.dfmi_agg_state_grouped_partial_bytes.restype = C.c_int64
+    L.dfmi_agg_state_grouped_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, P(dfmi_error)]
+    L.dfmi_agg_state_grouped_partial.restype = C.c_int32
+    L.dfmi_agg_merge_grouped_partials.argtypes = [P(C.c_void_p), C.c_int32, P(C.c_void_p), P(C.c_int64), C.c_int32,
+                                                  C.c_int64, P(dfmi_agg_value), P(dfmi_agg_value), P(C.c_int64),
+                                                  P(dfmi_error)]
+    L.dfmi_agg_merge_grouped_partials.restype = C.c_int32
     L.dfmi_agg_state_free.argtypes = [C.c_void_p]
     L.dfmi_agg_state_free.restype = None
     _LIB = L

@@ -586,6 +586,34 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
         for (Partial& p : kv.second.second) normalize(p);
 }
 
+using GroupMap = std::map<dfmi_agg_state::HKey, std::pair<uint64_t, std::vector<Partial>>>;
+
+// Groups in key order as dfmi_agg_state_finish_grouped outputs them.
+void emit_groups(const GroupMap& groups, int kt, const dfmi_aggregate* const* aggs, size_t n, int64_t cap,
+                 dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups) {
+    *num_groups = (int64_t)groups.size();
+    if (*num_groups > cap) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "group capacity too small"};
+    if (*num_groups > 0 && (!keys || !values)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+    int64_t g = 0;
+    for (const auto& [hk, v] : groups) {
+        keys[g].type = kt;
+        keys[g].is_null = hk.null ? 1 : 0;
+        keys[g].bits = hk.null ? 0 : (kt == DFMI_TYPE_BOOLEAN ? v.first : narrow_int(v.first, kt));
+        keys[g].count = (int64_t)v.second[n].count;  // the group's selected rows
+        for (size_t j = 0; j < n; ++j) values[g * n + j] = finish_one(*aggs[j], v.second[j]);
+        ++g;
+    }
+}
+
+// Serialised per-group partials (multi-GPU GROUP BY): a header, then per group
+// {null, key bits} and its n + 1 partials (aggregates, then the row count).
+struct GroupedHdr {
+    uint64_t magic, ngroups, naggs;
+    int64_t key_type;
+};
+constexpr uint64_t kGroupedMagic = 0x31505247494d4644ull;  // "DFMIGRP1"
+size_t grouped_bytes(size_t ngroups, size_t n) { return sizeof(GroupedHdr) + ngroups * (16 + (n + 1) * sizeof(Partial)); }
+
 }  // namespace
 
 extern "C" int32_t dfmi_compile_aggregate(const char* name, const dfmi_program* arg, int32_t return_type,
@@ -715,19 +743,7 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
         }
         HIP_TRY(hipSetDevice(ctx->device));
         flush_groups(ctx, st);
-        *num_groups = (int64_t)st->groups.size();
-        if (*num_groups > cap) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "group capacity too small"};
-        if (*num_groups > 0 && (!keys || !values)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
-        const size_t n = st->aggs.size();
-        int64_t g = 0;
-        for (const auto& [hk, v] : st->groups) {
-            keys[g].type = st->key.type;
-            keys[g].is_null = hk.null ? 1 : 0;
-            keys[g].bits = hk.null ? 0 : (st->key.type == DFMI_TYPE_BOOLEAN ? v.first : narrow_int(v.first, st->key.type));
-            keys[g].count = (int64_t)v.second[n].count;  // the group's selected rows
-            for (size_t j = 0; j < n; ++j) values[g * n + j] = finish_one(*st->aggs[j], v.second[j]);
-            ++g;
-        }
+        emit_groups(st->groups, st->key.type, st->aggs.data(), st->aggs.size(), cap, keys, values, num_groups);
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -962,6 +978,103 @@ extern "C" int32_t dfmi_agg_state_partial(dfmi_context* ctx, dfmi_agg_state* st,
         if (st->grouped) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "partial state of a GROUP BY aggregate"};
         const std::vector<Partial> parts = merge_copies(st, read_acc(ctx, st));
         memcpy(host_out, parts.data(), parts.size() * sizeof(Partial));
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int64_t dfmi_agg_state_grouped_partial_bytes(dfmi_context* ctx, dfmi_agg_state* st, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (!st->grouped) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return -(int64_t)st->failure.code;
+        }
+        HIP_TRY(hipSetDevice(ctx->device));
+        flush_groups(ctx, st);
+        return (int64_t)grouped_bytes(st->groups.size(), st->aggs.size());
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return -(int64_t)f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_state_grouped_partial(dfmi_context* ctx, dfmi_agg_state* st, void* host_out, int64_t bytes,
+                                                  dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !st || !host_out) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (!st->grouped) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return st->failure.code;
+        }
+        HIP_TRY(hipSetDevice(ctx->device));
+        flush_groups(ctx, st);
+        const size_t n = st->aggs.size();
+        if ((size_t)bytes < grouped_bytes(st->groups.size(), n)) throw Fail{DFMI_ERR_CAPACITY, "partial buffer too small"};
+        uint8_t* p = (uint8_t*)host_out;
+        const GroupedHdr h{kGroupedMagic, (uint64_t)st->groups.size(), (uint64_t)n, (int64_t)st->key.type};
+        memcpy(p, &h, sizeof h);
+        p += sizeof h;
+        for (const auto& [hk, v] : st->groups) {
+            const uint64_t rec[2] = {hk.null ? 1ull : 0ull, v.first};
+            memcpy(p, rec, 16);
+            p += 16;
+            memcpy(p, v.second.data(), (n + 1) * sizeof(Partial));
+            p += (n + 1) * sizeof(Partial);
+        }
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_merge_grouped_partials(const dfmi_aggregate* const* aggs, int32_t n,
+                                                   const void* const* partials, const int64_t* sizes, int32_t nparts,
+                                                   int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* values,
+                                                   int64_t* num_groups, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!aggs || n <= 0 || !partials || !sizes || nparts <= 0 || !num_groups)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        GroupMap groups;
+        int64_t kt = -1;
+        for (int r = 0; r < nparts; ++r) {
+            const uint8_t* p = (const uint8_t*)partials[r];
+            GroupedHdr h;
+            if (!p || sizes[r] < (int64_t)sizeof h) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+            memcpy(&h, p, sizeof h);
+            if (h.magic != kGroupedMagic || h.naggs != (uint64_t)n || (kt >= 0 && h.key_type != kt) ||
+                (size_t)sizes[r] < grouped_bytes(h.ngroups, (size_t)n))
+                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+            kt = h.key_type;
+            p += sizeof h;
+            for (uint64_t g = 0; g < h.ngroups; ++g) {
+                uint64_t rec[2];
+                memcpy(rec, p, 16);
+                p += 16;
+                dfmi_agg_state::HKey hk{rec[0] != 0, 0};
+                if (!hk.null)
+                    hk.ord = kt == DFMI_TYPE_BOOLEAN ? (__int128)rec[1]
+                                                     : (is_signed_type((int)kt) ? (__int128)(int64_t)rec[1] : (__int128)rec[1]);
+                auto it = groups.find(hk);
+                if (it == groups.end()) it = groups.emplace(hk, std::make_pair(rec[1], std::vector<Partial>(n + 1))).first;
+                for (int j = 0; j <= n; ++j) {
+                    Partial q;
+                    memcpy(&q, p + (size_t)j * sizeof(Partial), sizeof q);
+                    if (j < n) merge_partial(it->second.second[j], q, aggs[j]->fn == DFMI_AGG_MIN);
+                    else it->second.second[n].count += q.count;
+                }
+                p += (size_t)(n + 1) * sizeof(Partial);
+            }
+        }
+        emit_groups(groups, (int)std::max<int64_t>(kt, 0), aggs, (size_t)n, cap, keys, values, num_groups);
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);

@@ -536,6 +536,53 @@ extern "C" int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm*
     }
 }
 
+extern "C" int32_t dfmi_shard_agg_finish_grouped(dfmi_context* ctx, dfmi_shard_comm* c, dfmi_agg_state* state,
+                                                 const dfmi_aggregate* const* aggs, int32_t n, int64_t cap,
+                                                 dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups,
+                                                 dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!ctx || !c || !state || !aggs || !num_groups) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        // round 1: [status | bytes | message] of every rank (a failed state
+        // still takes part; every rank reports the first failing rank's error)
+        const size_t rec = 16 + kMsg;
+        std::vector<uint8_t> mine(rec, 0), all(rec * c->world);
+        dfmi_error local{};
+        const int64_t nb = dfmi_agg_state_grouped_partial_bytes(ctx, state, &local);
+        std::vector<uint8_t> part(nb > 0 ? (size_t)nb : 0);
+        int32_t rc = nb < 0 ? (int32_t)-nb : DFMI_OK;
+        if (!rc) rc = dfmi_agg_state_grouped_partial(ctx, state, part.data(), nb, &local);
+        memcpy(mine.data(), &rc, 4);
+        const int64_t mb = rc ? 0 : nb;
+        memcpy(mine.data() + 8, &mb, 8);
+        if (rc) snprintf((char*)mine.data() + 16, kMsg, "%s", local.message);
+        c->tp->all_gather(ctx, mine.data(), all.data(), rec);
+        int64_t maxb = 0;
+        std::vector<int64_t> sizes(c->world);
+        for (int r = 0; r < c->world; ++r) {
+            int32_t rr;
+            memcpy(&rr, &all[(size_t)r * rec], 4);
+            if (rr) {
+                all[(size_t)r * rec + 16 + kMsg - 1] = 0;
+                throw Fail{rr, std::string((const char*)&all[(size_t)r * rec + 16])};
+            }
+            memcpy(&sizes[r], &all[(size_t)r * rec + 8], 8);
+            maxb = std::max(maxb, sizes[r]);
+        }
+        // round 2: every rank's partial, padded to the largest
+        part.resize((size_t)maxb, 0);
+        std::vector<uint8_t> parts_all((size_t)maxb * c->world);
+        c->tp->all_gather(ctx, part.data(), parts_all.data(), (size_t)maxb);
+        std::vector<const void*> parts(c->world);
+        for (int r = 0; r < c->world; ++r) parts[r] = &parts_all[(size_t)r * maxb];
+        return dfmi_agg_merge_grouped_partials(aggs, n, parts.data(), sizes.data(), c->world, cap, keys, values,
+                                               num_groups, err);
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
 extern "C" int32_t dfmi_shard_agg_finish(dfmi_context* ctx, dfmi_shard_comm* c, dfmi_agg_state* state,
                                          const dfmi_aggregate* const* aggs, int32_t n, dfmi_agg_value* out,
                                          dfmi_error* err) {

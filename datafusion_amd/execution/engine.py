@@ -443,22 +443,50 @@ class GroupedAggState(AggState):
         super().__init__(eng, aggs, key)
 
     def finish(self):
+        return _grouped_call(len(self.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_state_finish_grouped(
+            self.eng.ctx, self.handle, cap, keys, vals, ng, err))
+
+    def partial(self) -> bytes:
+        """The exact per-group partial state (dfmi_agg_state_grouped_partial)."""
         L = _abi.lib()
-        n = len(self.aggs)
-        ng = C.c_int64()
         err = _abi.dfmi_error()
-        cap = 64
-        while True:
-            keys = (_abi.dfmi_agg_value * cap)()
-            vals = (_abi.dfmi_agg_value * (cap * n))()
-            rc = L.dfmi_agg_state_finish_grouped(self.eng.ctx, self.handle, cap, keys, vals, C.byref(ng), C.byref(err))
-            if rc == _abi.DFMI_ERR_INVALID_ARGUMENT and ng.value > cap:
-                cap = ng.value
-                continue
-            if rc != _abi.DFMI_OK:
-                raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
-            g = ng.value
-            return list(keys[:g]), [list(vals[i * n:(i + 1) * n]) for i in range(g)]
+        nb = L.dfmi_agg_state_grouped_partial_bytes(self.eng.ctx, self.handle, C.byref(err))
+        if nb < 0:
+            raise ExecutionError.from_status(int(-nb), err.message.decode("utf-8", errors="replace"))
+        buf = C.create_string_buffer(max(int(nb), 1))
+        rc = L.dfmi_agg_state_grouped_partial(self.eng.ctx, self.handle, buf, nb, C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        return buf.raw[:nb]
+
+
+def _grouped_call(n: int, fn):
+    """(keys, per-group values) from a grouped finish entry point, growing
+    the capacity to the group count it reports."""
+    ng = C.c_int64()
+    err = _abi.dfmi_error()
+    cap = 64
+    while True:
+        keys = (_abi.dfmi_agg_value * cap)()
+        vals = (_abi.dfmi_agg_value * (cap * n))()
+        rc = fn(cap, keys, vals, C.byref(ng), C.byref(err))
+        if rc == _abi.DFMI_ERR_INVALID_ARGUMENT and ng.value > cap:
+            cap = ng.value
+            continue
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        g = ng.value
+        return list(keys[:g]), [list(vals[i * n:(i + 1) * n]) for i in range(g)]
+
+
+def merge_grouped_partials(aggs: Sequence, partials: Sequence[bytes]):
+    """Every shard's per-group partial merged: (keys, per-group values)."""
+    arr = (C.c_void_p * len(aggs))(*[a.handle.value for a in aggs])
+    bufs = [C.create_string_buffer(p, len(p)) for p in partials]
+    parr = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+    sizes = (C.c_int64 * len(bufs))(*[len(p) for p in partials])
+    return _grouped_call(len(aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_merge_grouped_partials(
+        arr, len(aggs), parr, sizes, len(bufs), cap, keys, vals, ng, err))
 
 
 def merge_agg_partials(aggs: Sequence, partials: Sequence[bytes]) -> List[_abi.dfmi_agg_value]:
@@ -562,6 +590,12 @@ class ShardComm:
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
         return list(out)
+
+    def agg_finish_grouped(self, state: "GroupedAggState"):
+        """Every rank's per-group partials merged (collective): (keys, values)."""
+        arr = (C.c_void_p * len(state.aggs))(*[a.handle.value for a in state.aggs])
+        return _grouped_call(len(state.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_shard_agg_finish_grouped(
+            self.eng.ctx, self.handle, state.handle, arr, len(state.aggs), cap, keys, vals, ng, err))
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -445,6 +445,18 @@ int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key
  * `capacity` (then DFMI_ERR_INVALID_ARGUMENT and nothing is written). */
 int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_state* state, int64_t capacity, dfmi_agg_value* keys,
                                       dfmi_agg_value* values, int64_t* num_groups, dfmi_error* err);
+/* Multi-GPU GROUP BY: the exact per-group partial state (key, the group's
+ * selected rows, every aggregate's partial) as host bytes -- size first
+ * (negative: -status) -- and the merge of every shard's bytes into the groups
+ * one state over all the shards' rows would hold, in key order (output as
+ * dfmi_agg_state_finish_grouped). */
+int64_t dfmi_agg_state_grouped_partial_bytes(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
+int32_t dfmi_agg_state_grouped_partial(dfmi_context* ctx, dfmi_agg_state* state, void* host_out, int64_t bytes,
+                                       dfmi_error* err);
+int32_t dfmi_agg_merge_grouped_partials(const dfmi_aggregate* const* aggs, int32_t num_aggs,
+                                        const void* const* partials, const int64_t* sizes, int32_t num_partials,
+                                        int64_t capacity, dfmi_agg_value* keys, dfmi_agg_value* values,
+                                        int64_t* num_groups, dfmi_error* err);
 /* Back to the empty state (asynchronous on the context stream): re-running the query. */
 int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
 void dfmi_agg_state_free(dfmi_agg_state* state);
@@ -497,6 +509,13 @@ int32_t dfmi_shard_gather_to_root(dfmi_context* ctx, dfmi_shard_comm* comm, cons
 int32_t dfmi_shard_agg_finish(dfmi_context* ctx, dfmi_shard_comm* comm, dfmi_agg_state* state,
                               const dfmi_aggregate* const* aggs, int32_t num_aggs, dfmi_agg_value* out,
                               dfmi_error* err);
+/* ... with a GROUP BY key (collective): every rank's per-group partials
+ * all_gathered and merged; output as dfmi_agg_state_finish_grouped (every
+ * rank gets the same groups; *num_groups set even past `capacity`). */
+int32_t dfmi_shard_agg_finish_grouped(dfmi_context* ctx, dfmi_shard_comm* comm, dfmi_agg_state* state,
+                                      const dfmi_aggregate* const* aggs, int32_t num_aggs, int64_t capacity,
+                                      dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups,
+                                      dfmi_error* err);
 
 #ifdef __cplusplus
 }

@@ -277,3 +277,38 @@ def test_loopback_aggregate_finish():
     out = loop_world(3, fn)
     for got in out:
         assert got == [(r.bits, r.count, r.is_null) for r in ref], got
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_loopback_grouped_aggregate_finish(world):
+    """GROUP BY across ranks (dfmi_shard_agg_finish_grouped): every rank's
+    per-group partials all_gathered and merged -- the oracle's groups over
+    the whole table, keys (with row counts) and values bit-identical, on
+    every rank; keys both within one device window and far wider."""
+    from oracle_ffi import oracle_aggregate_grouped
+    rng = np.random.default_rng(17)
+    n = 60_000
+    s = Schema([Field("k", DataType.Int64, True), Field("x", DataType.Float64, True), Field("v", DataType.Int32, False)])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Int64, rng.integers(-900, 900, n), rng.random(n) > 0.02),
+                        Array.from_numpy(DataType.Float64, rng.standard_normal(n) * 1e6, rng.random(n) > 0.1),
+                        Array.from_numpy(DataType.Int32, rng.integers(-2 ** 31, 2 ** 31 - 1, n).astype(np.int32))])
+    fl = _abi.DFMI_FLAG_EXT_AGGREGATE
+    aggs_e = [agg("SUM", Column(1), s), agg("MIN", Column(1), s), agg("SUM", Column(2), s), agg("COUNT", Column(1), s)]
+    for key_e in (BinaryExpr(Column(1), Operator.Gt, Literal(Float64(0.0))), Column(0)):
+        rk, rv = oracle_aggregate_grouped(s, b, None, key_e, aggs_e, fl, 0)
+
+        def fn(rank, eng, comm):
+            aggs = [compile_expr(None, a, s, fl) for a in aggs_e]
+            st = eng.grouped_agg_state(compile_scalar_expr(None, key_e, s, fl), aggs)
+            st.add(None, shard_of(b, rank, world), fl)
+            k, v = comm.agg_finish_grouped(st)
+            return [(x.is_null, x.bits, x.count) for x in k], [[(y.is_null, y.bits, y.count) for y in g] for g in v]
+
+        out = loop_world(world, fn)
+        assert not [o for o in out if isinstance(o, Exception)], out
+        want = ([(x.is_null, x.bits, x.count) for x in rk], [[(y.is_null, y.bits, y.count) for y in g] for g in rv])
+        for got in out:
+            assert got[0] == want[0]
+            for g, (dg, rg) in enumerate(zip(got[1], want[1])):
+                for d, r in zip(dg, rg):
+                    assert d[0] == r[0] and d[2] == r[2] and (r[0] or d[1] == r[1]), (g, d, r)
