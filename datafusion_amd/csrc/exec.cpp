@@ -245,6 +245,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         } else if (pred && B.low_sel && !X.pred_slots.empty() && X.utf8_cols.empty() && n >= kSubtileMinRows) {
             X.BLOCK = 256;
             X.M = 8;
+            X.KO = 2;  // the (rare) dense output pass two slices at a time: fewer registers
         }
     }
     // diagnostic knobs (tools/*): read only when DFMI_DIAG is set -- a dozen
@@ -273,6 +274,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             if (pred && !X.pred_slots.empty() && X.utf8_cols.empty()) {
                 X.BLOCK = atoi(e) > 1 ? 256 : 512;
                 X.M = std::max(1, std::min(8, atoi(e)));
+                X.KO = X.M > 1 ? 2 : 0;
             }
         if (const char* e = getenv("DFMI_OUT_SLICES")) X.KO = atoi(e);
         if (const char* e = getenv("DFMI_SUBTILE_PREFETCH")) X.prefetch = atoi(e) & 1;

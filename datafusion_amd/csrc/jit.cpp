@@ -815,7 +815,10 @@ static void emit_batched_prologue(std::ostream& o, const Plan& P, const Launch& 
       << "  const u64 tt_ = (u64)bp_[1];\n"
       << "  A.n_tiles = (int)(unsigned)tt_;\n"
       << "  const unsigned tile_ = blockIdx.x - (unsigned)(tt_ >> 32);\n"
-      << "  A.totals = (u64*)bp_[2];\n  A.err = (u64*)bp_[3];\n";
+      << "  A.totals = (u64*)bp_[2];\n  A.err = (u64*)bp_[3];\n"
+      // diagnostics (mode bit 4): the forced look-back timeout in the first
+      // batch's own error word, which the coalesced launch's host reads
+      << "  if ((A.mode & 16) && blockIdx.x == 0 && tid == 0) atomicMax(A.err, ~(u64)3);\n";
     if (P.pred)  // [ch][tile] status words of this batch's tiles
         o << "  A.status = A0.status + (i64)(tt_ >> 32) * " << (1 + X.utf8_outs.size()) * (size_t)X.spread << ";\n";
     for (size_t s = 0; s < X.num_cols.size(); ++s)

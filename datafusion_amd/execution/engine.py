@@ -749,14 +749,14 @@ class HostBatchColumns(LazyColumns):
             t = k.type[i]
             n = k.length[i]
             nulls = k.nulls[i]
+            valid = k.buffer(k.validity[i], (n + 7) // 8) if (nulls and k.validity[i]) else None
             if t == DataType.Utf8:
                 offs = k.buffer(k.offsets[i], 4 * (n + 1)).view(torch.int32)
-                nbytes = int(offs[n]) if n else 0
+                nbytes = int(offs[n]) if n else 0  # (a passthrough slice's offsets need not start at 0)
                 vals = k.buffer(k.values[i], nbytes)
-                out.append(Array(t, n, vals, None, offs, 0))
+                out.append(Array(t, n, vals, valid, offs, nulls))
                 continue
             nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
             vals = k.buffer(k.values[i], nb)
-            valid = k.buffer(k.validity[i], (n + 7) // 8) if (nulls and k.validity[i]) else None
             out.append(Array(t, n, vals, valid, None, nulls))
         return out
