@@ -219,7 +219,7 @@ def oracle_aggregate(schema: Schema, batch: RecordBatch, pred: Optional[Expr], a
 
 
 def oracle_aggregate_grouped(schema: Schema, batch: RecordBatch, pred: Optional[Expr], key: Expr, aggs: Sequence,
-                             flags: int = None, batch_rows: int = 0, cap: int = 4096):
+                             flags: int = None, batch_rows: int = 0, cap: int = 0):
     """Aggregate{group_expr: [key]}(Selection?(scan)) on the oracle: returns
     (keys, values) -- one dfmi_agg_value key per group (key order, null
     last) and per group the list of aggregate values -- or raises
@@ -238,6 +238,7 @@ def oracle_aggregate_grouped(schema: Schema, batch: RecordBatch, pred: Optional[
                                                           for x in arg_nodes])
     lens = (C.c_int32 * max(1, n))(*[x.length for x in arg_nodes])
     rts = (C.c_int32 * max(1, n))(*[int(a.return_type) for a in aggs])
+    cap = cap or batch.num_rows() + 1  # at most one group per row (+ the null key)
     keys = (_abi.dfmi_agg_value * cap)()
     out = (_abi.dfmi_agg_value * (cap * max(1, n)))()
     ng = C.c_int64()

@@ -103,6 +103,52 @@ def test_c3_full_batch_against_torch():
     valid = ((vb.unsqueeze(1) >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1).reshape(-1)[:n].bool()
     mask = ~valid | (vals < 0.5)
     rows = torch.nonzero(mask).squeeze(1)
+    _check_gather(got, s, vals, rows)
+    del got, s, v
+    torch.cuda.empty_cache()
+
+
+def test_c3_full_batch_equality_against_torch():
+    """One C3 batch through bench.py's equality query: SELECT s, v WHERE
+    s = <word 17> (DFMI_FLAG_EXT_UTF8_COMPARE; the reference compares the
+    strings' bytes, filter.rs:99-100 reading get_string). The torch mask
+    compares every row's length and bytes with the literal's."""
+    from datafusion_amd.logicalplan import Utf8
+    dev = torch.device("cuda", 0)
+    eng = engine(dev)
+    words = bench._utf8_dictionary(bench.SEED)
+    import numpy as np
+    dict_bytes = torch.tensor(np.frombuffer(b"".join(words), dtype=np.uint8), device=dev)
+    dict_len = torch.tensor([len(w) for w in words], dtype=torch.int64, device=dev)
+    dict_off = torch.cumsum(dict_len, 0) - dict_len
+    g = torch.Generator(device=dev)
+    g.manual_seed(bench.SEED + 1000)
+    n = bench.C3_ROWS // bench.C3_BATCHES
+    (s, v), _ = bench._c3_batch(dev, g, n, dict_bytes, dict_off, dict_len)
+    schema = Schema([Field("s", DataType.Utf8, False), Field("v", DataType.Float64, True)])
+    w = words[17]
+    fl = _abi.DFMI_FLAG_EXT_UTF8_COMPARE
+    pred = compile_scalar_expr(None, BinaryExpr(Column(0), Operator.Eq, Literal(Utf8(w.decode()))), schema, fl)
+    projs = [compile_scalar_expr(None, Column(c), schema, fl) for c in (0, 1)]
+    got = eng.filter_project(pred, projs, RecordBatch(schema, [s, v]), fl)
+    offs = s.offsets.to(torch.int64)
+    lens = offs[1:] - offs[:-1]
+    rows = torch.nonzero(lens == len(w)).squeeze(1)
+    lit = torch.tensor(list(w), dtype=torch.uint8, device=dev)
+    keep = torch.ones(rows.numel(), dtype=torch.bool, device=dev)
+    for j in range(len(w)):  # byte j of every row of the literal's length
+        keep &= s.values[offs[rows] + j] == lit[j]
+    rows = rows[keep]
+    assert 0 < rows.numel() < n // 100
+    _check_gather(got, s, v.values.view(torch.float64), rows)
+    del got, s, v
+    torch.cuda.empty_cache()
+
+
+def _check_gather(got, s, vals, rows):
+    """SELECT s, v over the selected `rows`: bit-exact v slots (no validity in
+    the filtered batch) and s as rebased offsets + concatenated bytes."""
+    dev = vals.device
     sel = rows.numel()
     assert got[0].length == got[1].length == sel
     # v: the selected slots' bits, no validity in the filtered batch
@@ -124,8 +170,6 @@ def test_c3_full_batch_against_torch():
         within = torch.arange(k.numel(), device=dev) - (want_offs[k] - want_offs[r0])
         want = s.values[offs[rows[k]] + within]
         assert torch.equal(gb[want_offs[r0]:want_offs[r1]], want), (r0, r1)
-    del got, s, v
-    torch.cuda.empty_cache()
 
 
 def test_q6_full_size_exact_sum():

@@ -8,7 +8,7 @@ K=${2:-}
 mkdir -p gpurun_out
 ARGS=(${FILES:-tests/test_gpu_batches.py tests/test_gpu_parity.py})
 [ -n "$K" ] && ARGS+=(-k "$K")
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread "${ARGS[@]}" \
+timeout -k 10 ${PT_TIMEOUT:-600} python -u -m pytest -x -v --timeout 120 --timeout-method thread "${ARGS[@]}" \
     > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; tail -5 gpurun_out/pytest_$TAG.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --no-cpu --sweep "" --extra ${EXTRA:-batches,c3} --gather 0 \
