@@ -267,9 +267,20 @@ class LazyColumns:
 class RecordBatch:
     """arrow::record_batch::RecordBatch"""
 
+    _transient = False  # a source's zero-copy view, valid until its next pull (datasource.py)
+
     def __init__(self, schema: Schema, columns):
         self.schema = schema
         self._columns = columns if isinstance(columns, LazyColumns) else list(columns)
+
+    @classmethod
+    def lazy(cls, schema: Schema, columns: LazyColumns) -> "RecordBatch":
+        """A batch over LazyColumns, built without __init__'s checks (one
+        per output batch of a coalesced call)."""
+        b = object.__new__(cls)
+        b.schema = schema
+        b._columns = columns
+        return b
 
     @property
     def columns(self) -> List[Array]:

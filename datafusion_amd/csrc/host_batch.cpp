@@ -397,6 +397,7 @@ void finish_bitmap(uint8_t* b, int64_t n) {
 constexpr int kSlots = 3;
 // a host batch up to this size skips the chunk pipeline (one H2D, one
 // launch, one D2H, one synchronisation: dfmi_filter_project_host)
+constexpr size_t kZeroCopyBytes = 0;  // inputs + batch table read in place up to this size (DFMI_HOST_ZC)
 constexpr int64_t kSmallRows = 1 << 16;
 constexpr size_t kSmallBytes = (size_t)4 << 20;
 
@@ -612,7 +613,8 @@ extern "C" int32_t dfmi_filter_project_host(dfmi_context* ctx, const dfmi_progra
         // copy streams or host threads -- the one-batch form of the
         // host-batches path: pack into pinned memory, one H2D, the launch and
         // one D2H of the output region on the context stream, one sync
-        if (n <= kSmallRows && !getenv("DFMI_HOST_CHUNK_ROWS")) {
+        static const bool chunk_env = getenv("DFMI_HOST_CHUNK_ROWS") != nullptr;
+        if (n <= kSmallRows && !chunk_env) {
             size_t bytes = 0;
             for (int i = 0; i < ncols; ++i) {
                 const dfmi_column& c = in->columns[i];
@@ -1293,9 +1295,20 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
             A.pool->run(tasks);
         }
         memset(A.pin, 0, H);
+        // zero-copy inputs (small calls): the kernel reads the inputs and the
+        // batch table straight from the pinned staging region over PCIe -- no
+        // H2D copy on the call's critical path; only the headers are cleared
+        // on the device
+        static const int zc_env = [] {
+            const char* e = getenv("DFMI_HOST_ZC");
+            return e ? atoi(e) : -1;
+        }();
+        const bool zc = zc_env > 0 || (zc_env < 0 && in_bytes + MB <= kZeroCopyBytes);
+        uint8_t* pin_dev = nullptr;
+        if (zc) HIP_TRY(hipHostGetDevicePointer((void**)&pin_dev, A.pin, 0));
         uint8_t* const dout = A.dev;
         uint8_t* const dhdr = A.dev + OB;
-        uint8_t* const dev = dhdr + H;  // inputs
+        uint8_t* const dev = zc ? pin_dev + H : dhdr + H;  // inputs
         std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
         std::vector<dfmi_batch> dins(nb);
         for (int32_t b = 0; b < nb; ++b) {
@@ -1341,7 +1354,8 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         };
         stage.copy_in = [&](hipStream_t s) {
             const size_t nbytes = meta_used ? H + IB + meta_used : H + in_bytes;
-            const hipError_t e = hipMemcpyAsync(dhdr, A.pin, nbytes, hipMemcpyHostToDevice, s);
+            const hipError_t e = zc ? hipMemsetAsync(dhdr, 0, H, s)
+                                    : hipMemcpyAsync(dhdr, A.pin, nbytes, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) copy_err = e;
         };
         stage.copy_out = [&](hipStream_t s) {

@@ -186,6 +186,7 @@ class MemoryDataSource(DataSource):
         self._schema = schema
         self._batches = list(batches)
         self._pos = 0
+        self._ends = None  # rows before each batch's end (next_many), built on first use
 
     def schema(self) -> Schema:
         return self._schema
@@ -196,3 +197,17 @@ class MemoryDataSource(DataSource):
         b = self._batches[self._pos]
         self._pos += 1
         return b
+
+    def next_many(self, m: int, max_rows: int) -> List[RecordBatch]:
+        """What up to m next() calls return, stopping once max_rows rows are
+        out (the batch that reaches max_rows is the last one)."""
+        import bisect
+        if self._ends is None:
+            self._ends = np.cumsum([b.num_rows() for b in self._batches], dtype=np.int64).tolist()
+        i = self._pos
+        end = min(len(self._batches), i + m)
+        if i < end:
+            before = self._ends[i - 1] if i else 0
+            end = min(end, bisect.bisect_left(self._ends, before + max_rows, i, end) + 1)
+        self._pos = end
+        return self._batches[i:end]

@@ -341,7 +341,7 @@ class DeviceEngine:
             if not res.value:
                 raise error
         done = nb if error is None else max(0, failed)
-        block = HostResultBlock(res, done * nout)
+        block = HostResultBlock(res, done * nout, nout)
         return [HostBatchColumns(block, b, nout) for b in range(done)], error
 
     # ---- aggregate extension (DFMI_FLAG_EXT_AGGREGATE)
@@ -687,13 +687,16 @@ class HostResultBlock:
     one FFI call) and its pinned block as one uint8 tensor. Slices of that
     tensor keep the result alive."""
 
-    def __init__(self, res, ncols: int):
+    def __init__(self, res, ncols: int, nout: int = 0):
         L = _abi.lib()
         owner = _ResultOwner(res)
         views = np.zeros(max(1, ncols), dtype=_COL_DTYPE)
         if ncols:
             L.dfmi_host_result_columns(res, 0, ncols, views.ctypes.data)
-        self.type = [DataType(t) for t in views["type"].tolist()]
+        if nout and ncols % nout == 0:  # batch after batch of the same nout output types
+            self.type = [DataType(t) for t in views["type"][:nout].tolist()] * (ncols // nout)
+        else:
+            self.type = [DataType(t) for t in views["type"].tolist()]
         self.length = views["length"].tolist()
         self.nulls = views["null_count"].tolist()
         self.validity = views["validity"].tolist()

@@ -4,7 +4,7 @@ from __future__ import annotations
 from collections import deque
 from typing import Callable, Optional
 
-from ..arrow import RecordBatch, Schema
+from ..arrow import LazyColumns, RecordBatch, Schema
 from .engine import engine
 from .expression import RuntimeExpr
 from .relation import Relation
@@ -41,24 +41,33 @@ class Coalescer:
     loop); the stream is the same."""
 
     def __init__(self, m: int, source: Relation, run_one: Callable, run_many: Callable, wrap: Callable,
-                 run_many_host: Callable = None, max_rows: int = 1 << 20, run_many_host_async: Callable = None):
+                 run_many_host: Callable = None, max_rows: int = 1 << 20, run_many_host_async: Callable = None,
+                 wrap_many: Callable = None):
         self.m, self.source, self.max_rows = m, source, max_rows
         self.run_one, self.run_many, self.run_many_host, self.wrap = run_one, run_many, run_many_host, wrap
+        self.wrap_many = wrap_many if wrap_many is not None else (lambda rs: [wrap(c) for c in rs])
         self.run_many_host_async = run_many_host_async
         self.ready = deque()       # RecordBatches / exceptions, in stream order
         self.pending = deque()     # pulled input batches (or a source error) still to run one by one
         self.ahead = None          # the next group read ahead: (future or None, batches, source error)
 
     def _read_ahead(self):
+        many = getattr(self.source, "next_many", None)
+        if many is not None:  # a source that hands out many batches at once (MemoryDataSource)
+            try:
+                return many(self.m, self.max_rows), None
+            except Exception as e:
+                return [], e
         pulled, rows = [], 0
+        nxt = self.source.next
         while len(pulled) < self.m and rows < self.max_rows:
             try:
-                b = self.source.next()
+                b = nxt()
             except Exception as e:  # raised after the batches before it
                 return pulled, e
             if b is None:
                 break
-            if getattr(b, "_transient", False):
+            if b._transient:
                 b = detach(b)
             pulled.append(b)
             rows += b.num_rows()
@@ -78,7 +87,8 @@ class Coalescer:
     def _accept(self, pulled, results, err) -> bool:
         """Results of one coalesced call into ready; after a failing batch the
         rest go to pending. True when the group had no error."""
-        self.ready.extend(self.wrap(cols) for cols in results)
+        if results:
+            self.ready.extend(self.wrap_many(results))
         if err is not None:
             self.ready.append(err)
             self.pending.extend(pulled[len(results) + 1:])
@@ -107,6 +117,12 @@ class Coalescer:
             i = j
 
     def next(self) -> Optional[RecordBatch]:
+        ready = self.ready
+        if ready:  # the common case: a result of the current group
+            item = ready.popleft()
+            if isinstance(item, Exception):
+                raise item
+            return item
         while not self.ready:
             if self.pending:
                 item = self.pending.popleft()
@@ -157,12 +173,16 @@ class FilterRelation(Relation):
         return eng.filter_project(self.expr, None, batch, self.flags)
 
     def next(self) -> Optional[RecordBatch]:
+        co = self._co
+        if co is not None:
+            return co.next()
         if self.coalesce > 1:
             if self._co is None:
                 self._co = Coalescer(self.coalesce, self.input, self.run_batch,
                                      lambda bs: engine(self.device).filter_project_batches(self.expr, None, bs,
                                                                                            self.flags),
-                                     lambda cols: RecordBatch(Schema.empty(), cols),
+                                     lambda cols: (RecordBatch.lazy(Schema.empty(), cols) if isinstance(cols, LazyColumns)
+                                                   else RecordBatch(Schema.empty(), cols)),
                                      lambda bs: engine(self.device).filter_project_host_batches(self.expr, None, bs,
                                                                                                 self.flags),
                                      run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 from typing import List, Optional
 
-from ..arrow import Field, RecordBatch, Schema
+from ..arrow import Field, LazyColumns, RecordBatch, Schema
 from .engine import engine
 from .expression import RuntimeExpr
 from .filter import Coalescer, FilterRelation, is_host_batch
@@ -42,7 +42,15 @@ class ProjectRelation(Relation):
     def _wrap(self, cols) -> RecordBatch:
         if self._batch_schema is None:  # projection.rs:52-57, the same for every batch
             self._batch_schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
+        if isinstance(cols, LazyColumns):
+            return RecordBatch.lazy(self._batch_schema, cols)
         return RecordBatch(self._batch_schema, cols)
+
+    def _wrap_many(self, results) -> list:
+        if self._batch_schema is None:
+            self._wrap(results[0])
+        sch, lazy = self._batch_schema, RecordBatch.lazy
+        return [lazy(sch, c) if isinstance(c, LazyColumns) else RecordBatch(sch, c) for c in results]
 
     def run_batch(self, batch: RecordBatch):
         _, pred = self._source_and_predicate()
@@ -54,6 +62,9 @@ class ProjectRelation(Relation):
         return eng.filter_project(pred, self.expr, batch, self.flags)
 
     def next(self) -> Optional[RecordBatch]:
+        co = self._co
+        if co is not None:
+            return co.next()
         source, pred = self._source_and_predicate()
         if self.coalesce > 1:  # up to `coalesce` input batches per device launch
             if self._co is None:
@@ -64,7 +75,7 @@ class ProjectRelation(Relation):
                                      lambda bs: engine(self.device).filter_project_host_batches(pred, self.expr, bs,
                                                                                                 self.flags),
                                      run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
-                                         pred, self.expr, bs, self.flags))
+                                         pred, self.expr, bs, self.flags), wrap_many=self._wrap_many)
             return self._co.next()
         batch = source.next()
         if batch is None:

@@ -33,5 +33,15 @@ class DataSourceRelation(Relation):
     def next(self) -> Optional[RecordBatch]:
         return self.ds.next()
 
+    @property
+    def next_many(self):
+        """The source's next_many(m, max_rows), when it has one: up to m
+        batches (fewer once max_rows rows are out) in one call -- what m next()
+        calls would return, for a Coalescer's read-ahead."""
+        nm = getattr(self.ds, "next_many", None)
+        if nm is None:
+            raise AttributeError("next_many")
+        return nm
+
     def schema(self) -> Schema:
         return self._schema
