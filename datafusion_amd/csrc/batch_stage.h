@@ -1,8 +1,10 @@
 // How a caller of the coalesced-batches launch (exec.cpp) stages its small
 // per-call data: the host-batches entry point (host_batch.cpp) moves its
-// packed inputs, the batch table and the zeroed per-batch headers with ONE
-// H2D copy, and the outputs with the headers with ONE D2H copy, so a call is
-// one copy in, one launch, one copy out and one synchronisation.
+// packed inputs and the batch table with ONE H2D copy (none for small calls,
+// whose kernel reads them from pinned memory), and the outputs with the
+// per-batch headers with ONE D2H copy; the headers are zeroed by the
+// previous call's kernel (clear_bhdr), so a call is at most one copy in, one
+// launch, one copy out and one synchronisation.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -28,6 +30,11 @@ struct BatchStage {
     std::function<void(hipStream_t)> copy_in;
     // Issued after the launch(es), before the call's synchronisation.
     std::function<void(hipStream_t)> copy_out;
+    // Words the coalesced kernel zeroes (the previous call's headers), and
+    // set true once a kernel that does so is enqueued.
+    uint64_t* clear_bhdr = nullptr;
+    int64_t clear_bhdr_words = 0;
+    bool* cleared = nullptr;
 };
 
 // dfmi_filter_project_batches with a caller's staging (NULL: none).

@@ -923,11 +923,16 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
                 A.clear_hdr = (unsigned long long*)ws.clear_hdr;
                 A.tile_batch = (const int*)(dev_meta + table_bytes);
                 A.batch_ptrs = (void* const*)dev_meta;
+                if (stage) {
+                    A.clear_bhdr = (unsigned long long*)stage->clear_bhdr;
+                    A.clear_bhdr_words = stage->clear_bhdr_words;
+                }
                 if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
                 size_t asz = sizeof A;
                 void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
                 HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)T, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
                 ws_commit(ctx, ws);
+                if (stage && stage->cleared) *stage->cleared = true;
                 if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
                 if (!staged) HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
             }

@@ -397,7 +397,7 @@ void finish_bitmap(uint8_t* b, int64_t n) {
 constexpr int kSlots = 3;
 // a host batch up to this size skips the chunk pipeline (one H2D, one
 // launch, one D2H, one synchronisation: dfmi_filter_project_host)
-constexpr size_t kZeroCopyBytes = 0;  // inputs + batch table read in place up to this size (DFMI_HOST_ZC)
+constexpr size_t kZeroCopyBytes = 256 << 10;  // inputs + batch table read in place up to this size (DFMI_HOST_ZC)
 constexpr int64_t kSmallRows = 1 << 16;
 constexpr size_t kSmallBytes = (size_t)4 << 20;
 
@@ -421,6 +421,7 @@ struct Arena {
     uint8_t* dev = nullptr;
     size_t dev_cap = 0;
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;  // the device's address of pin (zero-copy reads)
     size_t pin_cap = 0;
     hipStream_t h2d = nullptr, d2h = nullptr;
     hipEvent_t h2d_done[kSlots] = {}, d2h_done[kSlots] = {}, kdone[kSlots] = {};
@@ -447,6 +448,29 @@ struct Arena {
         HIP_TRY(hipMalloc((void**)&dev, need));
         dev_cap = need;
     }
+    // dfmi_filter_project_host_batches' device region: two halves of
+    // [headers (right-aligned in hcap) | outputs (ocap)], used alternately,
+    // then the inputs + batch table (icap). A call's kernel zeroes the
+    // headers the previous call left in the other half (hb_dirty: bytes at
+    // the end of a half's header room that are not known to be zero).
+    uint8_t* hb = nullptr;
+    size_t hb_hcap = 0, hb_ocap = 0, hb_icap = 0, hb_dirty[2] = {0, 0};
+    int hb_half = 0;
+    void reserve_hb(size_t H, size_t OB, size_t IM, hipStream_t st) {
+        if (hb && H <= hb_hcap && OB <= hb_ocap && IM <= hb_icap) return;
+        if (hb) {
+            HIP_TRY(hipStreamSynchronize(st));  // (earlier calls synchronised: nothing uses it)
+            (void)hipFree(hb);
+        }
+        hb = nullptr;
+        hb_hcap = std::max(H, std::max(hb_hcap, (size_t)64 << 10));
+        hb_ocap = std::max(OB, hb_ocap);
+        hb_icap = std::max(IM, hb_icap);
+        HIP_TRY(hipMalloc((void**)&hb, 2 * (hb_hcap + hb_ocap) + hb_icap));
+        for (int h = 0; h < 2; ++h) HIP_TRY(hipMemsetAsync(hb + h * (hb_hcap + hb_ocap), 0, hb_hcap, st));
+        hb_dirty[0] = hb_dirty[1] = 0;
+    }
+    uint8_t* hb_half_base(int h) const { return hb + (size_t)h * (hb_hcap + hb_ocap); }
     void reserve_pin(size_t need) {
         if (need <= pin_cap) return;
         if (pin) (void)hipHostFree(pin);
@@ -454,11 +478,13 @@ struct Arena {
         pin_cap = 0;
         HIP_TRY(hipHostMalloc((void**)&pin, need, hipHostMallocDefault));
         pin_cap = need;
+        HIP_TRY(hipHostGetDevicePointer((void**)&pin_dev, pin, 0));
     }
     void release() {
         if (h2d) (void)hipStreamSynchronize(h2d);
         if (d2h) (void)hipStreamSynchronize(d2h);
         if (dev) (void)hipFree(dev);
+        if (hb) (void)hipFree(hb);
         if (pin) (void)hipHostFree(pin);
         for (int s = 0; s < kSlots; ++s) {
             if (h2d_done[s]) (void)hipEventDestroy(h2d_done[s]);
@@ -1266,18 +1292,20 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                     out_bytes += align256(std::max<size_t>(L.ndat, 1));
                 }
             }
-        // ---- regions. Device: [outputs | per-batch headers | inputs | batch
-        // table]; pinned staging: [zeros for the headers | inputs | table]
-        // (ONE H2D); the result's block: [outputs | headers] (ONE D2H).
+        // ---- regions. Device (Arena::hb): this call's half [headers |
+        // outputs], the other half's headers zeroed by this call's kernel,
+        // and [inputs | batch table]; pinned staging: [inputs | table] (ONE
+        // H2D, or none: small calls read it in place); the result's block:
+        // [headers | outputs] (ONE D2H).
         const size_t OB = align256(std::max<size_t>(out_bytes, 256)), H = align256((size_t)nb * 256),
                      IB = align256(std::max<size_t>(in_bytes, 256));
         size_t MB = 256;  // bound on the launch's batch table + tile map (exec.cpp)
         for (int32_t b = 0; b < nb; ++b)
             MB += (size_t)(4 + 3 * ncols + 5 * nout) * 8 + (size_t)((ins[b].num_rows + 63) / 64 + 1) * 4;
         MB = align256(MB);
-        A.reserve_pin(H + IB + MB);
-        A.reserve_dev(OB + H + IB + MB);
-        uint8_t* const pin_in = A.pin + H;
+        A.reserve_pin(IB + MB);
+        A.reserve_hb(H, OB, IB + MB, st);
+        uint8_t* const pin_in = A.pin;
         {
             std::vector<std::function<void()>> tasks;
             const int ways = std::max(1, std::min(A.pool->ways(), (int)(in_bytes >> 20) + 1));
@@ -1294,21 +1322,18 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                 });
             A.pool->run(tasks);
         }
-        memset(A.pin, 0, H);
         // zero-copy inputs (small calls): the kernel reads the inputs and the
         // batch table straight from the pinned staging region over PCIe -- no
-        // H2D copy on the call's critical path; only the headers are cleared
-        // on the device
+        // copy in at all on the call's critical path
         static const int zc_env = [] {
             const char* e = getenv("DFMI_HOST_ZC");
             return e ? atoi(e) : -1;
         }();
         const bool zc = zc_env > 0 || (zc_env < 0 && in_bytes + MB <= kZeroCopyBytes);
-        uint8_t* pin_dev = nullptr;
-        if (zc) HIP_TRY(hipHostGetDevicePointer((void**)&pin_dev, A.pin, 0));
-        uint8_t* const dout = A.dev;
-        uint8_t* const dhdr = A.dev + OB;
-        uint8_t* const dev = zc ? pin_dev + H : dhdr + H;  // inputs
+        const int half = A.hb_half, other = 1 - half;
+        uint8_t* const dout = A.hb_half_base(half) + A.hb_hcap;
+        uint8_t* const dhdr = dout - H;
+        uint8_t* const dev = zc ? A.pin_dev : A.hb + 2 * (A.hb_hcap + A.hb_ocap);  // inputs
         std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
         std::vector<dfmi_batch> dins(nb);
         for (int32_t b = 0; b < nb; ++b) {
@@ -1337,10 +1362,11 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                 d.data_capacity = (int64_t)L.ndat;
             }
         }
-        // ---- one H2D, the coalesced launch, one D2H, one synchronisation
-        R->arena = R->pool->get(OB + H);
+        // ---- (one H2D), the coalesced launch, one D2H, one synchronisation
+        R->arena = R->pool->get(H + OB);
         size_t meta_used = 0;
         hipError_t copy_err = hipSuccess;
+        bool cleared = false;
         dfmi::BatchStage stage;
         stage.locate = [&](size_t meta_bytes, size_t hdr_bytes, uint8_t** host_meta, uint8_t** dev_meta,
                            uint8_t** dev_hdr, const uint8_t** host_hdr) {
@@ -1349,23 +1375,34 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
             *host_meta = pin_in + IB;
             *dev_meta = dev + IB;
             *dev_hdr = dhdr;
-            *host_hdr = R->arena.p + OB;
+            *host_hdr = R->arena.p;
             return true;
         };
         stage.copy_in = [&](hipStream_t s) {
-            const size_t nbytes = meta_used ? H + IB + meta_used : H + in_bytes;
-            const hipError_t e = zc ? hipMemsetAsync(dhdr, 0, H, s)
-                                    : hipMemcpyAsync(dhdr, A.pin, nbytes, hipMemcpyHostToDevice, s);
+            hipError_t e = hipSuccess;
+            if (A.hb_dirty[half])  // headers the other half's last kernel did not zero (an earlier failed call)
+                e = hipMemsetAsync(dout - A.hb_dirty[half], 0, A.hb_dirty[half], s);
+            if (e == hipSuccess && !zc)
+                e = hipMemcpyAsync(dev, pin_in, meta_used ? IB + meta_used : in_bytes, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) copy_err = e;
+            else A.hb_dirty[half] = 0;
         };
         stage.copy_out = [&](hipStream_t s) {
-            const hipError_t e = hipMemcpyAsync(R->arena.p, dout, OB + H, hipMemcpyDeviceToHost, s);
+            const hipError_t e = hipMemcpyAsync(R->arena.p, dhdr, H + OB, hipMemcpyDeviceToHost, s);
             if (e != hipSuccess) copy_err = e;
         };
+        stage.clear_bhdr = (uint64_t*)(A.hb_half_base(other) + A.hb_hcap - A.hb_dirty[other]);
+        stage.clear_bhdr_words = (int64_t)(A.hb_dirty[other] / 8);
+        stage.cleared = &cleared;
         dfmi_error e2{};
         const int32_t rc = dfmi::filter_project_batches_staged(ctx, pred, projs, np, dins.data(), nb, douts.data(),
                                                                flags, failed, &e2, &stage);
         if (rc != DFMI_OK) (void)hipStreamSynchronize(st);  // (a call that failed after copy_in: drain it)
+        if (cleared) {  // this kernel zeroed the other half's headers; this half's are dirty now
+            A.hb_dirty[other] = 0;
+            A.hb_dirty[half] = std::max(A.hb_dirty[half], H);
+            A.hb_half = other;
+        }
         HIP_TRY(copy_err);
         const int32_t nok = rc == DFMI_OK ? nb : std::max(0, *failed);
         R->cols.resize((size_t)nb * nout);
@@ -1401,9 +1438,10 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                 c.length = d.length;
                 c.null_count = d.null_count;
                 c.data_length = d.data_length;
-                c.v_values = R->arena.p + (otype[o] == DFMI_TYPE_UTF8 ? L.dat : L.val);
-                c.v_offsets = otype[o] == DFMI_TYPE_UTF8 ? (const int32_t*)(R->arena.p + L.off) : nullptr;
-                c.v_validity = R->arena.p + L.vld;
+                uint8_t* const ob = R->arena.p + H;  // the outputs, after the headers
+                c.v_values = ob + (otype[o] == DFMI_TYPE_UTF8 ? L.dat : L.val);
+                c.v_offsets = otype[o] == DFMI_TYPE_UTF8 ? (const int32_t*)(ob + L.off) : nullptr;
+                c.v_validity = ob + L.vld;
             }
         *out = R;
         R = nullptr;

@@ -60,6 +60,10 @@ struct Args {
     u64* clear_status;                 // previous launch's status words ...
     i64 clear_words;                   // ... [0, clear_words) to zero
     u64* clear_hdr;                    // previous launch's 512-byte header
+    // coalesced host batches (host_batch.cpp): the per-batch headers of the
+    // previous call, in the other half of its ping-pong device region
+    u64* clear_bhdr;
+    i64 clear_bhdr_words;
     u64* agg;                          // aggregate extension: [copies][aggs][kAggWords] accumulators
     // coalesced batches (dfmi_filter_project_batches): block -> batch, and
     // per batch a row of pointers / sizes the kernel's prologue loads into a
@@ -80,6 +84,10 @@ __device__ __forceinline__ void clear_previous(const Args& A, unsigned block, in
     const i64 w1 = w0 + per < A.clear_words ? w0 + per : A.clear_words;
     for (i64 w = w0 + tid; w < w1; w += BLOCK) A.clear_status[w] = 0;
     if (block == 0 && tid < 64) A.clear_hdr[tid] = 0;
+    const i64 bper = (A.clear_bhdr_words + A.n_tiles - 1) / A.n_tiles;
+    const i64 b0 = (i64)block * bper;
+    const i64 b1 = b0 + bper < A.clear_bhdr_words ? b0 + bper : A.clear_bhdr_words;
+    for (i64 w = b0 + tid; w < b1; w += BLOCK) A.clear_bhdr[w] = 0;
     // diagnostics (mode bit 4): report a look-back timeout once, to test the
     // host's relaunch (exec.cpp)
     if ((A.mode & 16) && block == 0 && tid == 0) atomicMax(A.err, ~(u64)3);
