@@ -8,8 +8,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <functional>
 
 #include "../../include/dfmi.h"
@@ -35,6 +38,36 @@ struct BatchStage {
     uint64_t* clear_bhdr = nullptr;
     int64_t clear_bhdr_words = 0;
     bool* cleared = nullptr;
+};
+
+// Diagnostics (DFMI_DIAG + DFMI_CALL_PROFILE): host time per phase of an
+// entry point, averaged over 1000 calls and printed on stderr. mark(i) ends
+// phase i; done() ends a call.
+struct CallProf {
+    const char* name;
+    double ph[8] = {};
+    long n = 0;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit CallProf(const char* nm) : name(nm), on(getenv("DFMI_DIAG") && getenv("DFMI_CALL_PROFILE")) {}
+    void start() {
+        if (on) t = std::chrono::steady_clock::now();
+    }
+    void mark(int i) {
+        if (!on) return;
+        const auto u = std::chrono::steady_clock::now();
+        ph[i] += std::chrono::duration<double, std::micro>(u - t).count();
+        t = u;
+    }
+    void done() {
+        if (!on || ++n % 1000) return;
+        fprintf(stderr, "dfmi call profile %s (us/call):", name);
+        for (double& x : ph) {
+            fprintf(stderr, " %.2f", x / 1000);
+            x = 0;
+        }
+        fprintf(stderr, "\n");
+    }
 };
 
 // dfmi_filter_project_batches with a caller's staging (NULL: none).

@@ -721,6 +721,9 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
                                             const dfmi_program* const* projs, int32_t np, const dfmi_batch* ins,
                                             int32_t nb, dfmi_out_column* outs, uint32_t flags, int32_t* failed,
                                             dfmi_error* err, const BatchStage* stage) {
+    // phases: checks + plan, kernel lookup, batch table, enqueue, synchronisation, results
+    static thread_local CallProf prof("batches_staged");
+    prof.start();
     set_err(err, DFMI_OK, "");
     int32_t dummy_failed;
     if (!failed) failed = &dummy_failed;
@@ -793,8 +796,10 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
         hipStream_t st = ctx->stream;
         ctx->timed = false;
         ctx->last_compile_ms = 0;
+        prof.mark(0);
         const hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
         ctx->last_kernel = X.kname;
+        prof.mark(1);
 
         // ---- batch table
         const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
@@ -893,7 +898,8 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
         // time-sliced away from this queue for 2 s) is relaunched once over a
         // re-zeroed workspace and headers, as dfmi_filter_project does; the
         // relaunch rewrites every batch's outputs.
-        if (stage) stage->copy_in(st);  // (staged: with the table and the zeroed headers)
+        prof.mark(2);
+        if (stage) stage->copy_in(st);  // (staged: with the table; headers zeroed by the previous call)
         int mode = 0;
         if (getenv("DFMI_DIAG"))
             if (const char* m = getenv("DFMI_DEBUG_MODE")) mode = atoi(m);  // diagnostics only (bit 4: force a timeout)
@@ -942,7 +948,9 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
                         if (plan.outs[o].kind == jit::OutSpec::UTF8 && outs[(size_t)b * nout + o].offsets)
                             HIP_TRY(hipMemsetAsync(outs[(size_t)b * nout + o].offsets, 0, 4, st));
             if (stage) stage->copy_out(st);  // (staged: with the headers)
+            prof.mark(3);
             HIP_TRY(hipStreamSynchronize(st));
+            prof.mark(4);
             bool timed_out = false;
             for (int32_t b = 0; b < nb && T > 0; ++b) {
                 const uint64_t ew = ins[b].num_rows > 0 ? ((const uint64_t*)(host_hdr + (size_t)b * kBHdr))[24] : 0;
@@ -995,6 +1003,8 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
                         if (X.utf8_outs[j].first == o) oc.data_length = (int64_t)h[1 + j];
             }
         }
+        prof.mark(5);
+        prof.done();
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);

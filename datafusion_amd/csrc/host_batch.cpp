@@ -1197,6 +1197,9 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                                                     const dfmi_program* const* projs, int32_t np,
                                                     const dfmi_batch* ins, int32_t nb, uint32_t flags,
                                                     dfmi_host_result** out, int32_t* failed, dfmi_error* err) {
+    // phases: checks + layout, packing into pinned memory, structs, the staged call, result views
+    static thread_local dfmi::CallProf prof("host_batches");
+    prof.start();
     set_err(err, DFMI_OK, "");
     int32_t dummy_failed;
     if (!failed) failed = &dummy_failed;
@@ -1306,6 +1309,7 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         A.reserve_pin(IB + MB);
         A.reserve_hb(H, OB, IB + MB, st);
         uint8_t* const pin_in = A.pin;
+        prof.mark(0);
         {
             std::vector<std::function<void()>> tasks;
             const int ways = std::max(1, std::min(A.pool->ways(), (int)(in_bytes >> 20) + 1));
@@ -1330,6 +1334,7 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
             return e ? atoi(e) : -1;
         }();
         const bool zc = zc_env > 0 || (zc_env < 0 && in_bytes + MB <= kZeroCopyBytes);
+        prof.mark(1);
         const int half = A.hb_half, other = 1 - half;
         uint8_t* const dout = A.hb_half_base(half) + A.hb_hcap;
         uint8_t* const dhdr = dout - H;
@@ -1395,9 +1400,11 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         stage.clear_bhdr_words = (int64_t)(A.hb_dirty[other] / 8);
         stage.cleared = &cleared;
         dfmi_error e2{};
+        prof.mark(2);
         const int32_t rc = dfmi::filter_project_batches_staged(ctx, pred, projs, np, dins.data(), nb, douts.data(),
                                                                flags, failed, &e2, &stage);
         if (rc != DFMI_OK) (void)hipStreamSynchronize(st);  // (a call that failed after copy_in: drain it)
+        prof.mark(3);
         if (cleared) {  // this kernel zeroed the other half's headers; this half's are dirty now
             A.hb_dirty[other] = 0;
             A.hb_dirty[half] = std::max(A.hb_dirty[half], H);
@@ -1449,6 +1456,8 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
             if (err) *err = e2;
             return rc;
         }
+        prof.mark(4);
+        prof.done();
         return DFMI_OK;
     } catch (const Fail& f) {
         delete R;
