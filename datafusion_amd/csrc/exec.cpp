@@ -243,8 +243,14 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             X.waves_per_eu = 7;
             X.waves_soft = true;
         } else if (pred && B.low_sel && !X.pred_slots.empty() && X.utf8_cols.empty() && n >= kSubtileMinRows) {
+            // a numeric predicate that selected < 4% last time: M sub-tiles
+            // share one look-back, a sparse output pass re-reads only the
+            // selected rows (same-box A/B, profiles/r04/ab_subtiles*.log: C2
+            // s = 1% (2 predicate columns) 4.17 / 3.12 / 3.00 / 3.03 ms and C4
+            // (4) 3.01 / 2.76 / 2.60 / 2.51 ms at M = 1 / 8 / 4 / 2: more
+            // predicate registers per sub-tile, fewer sub-tiles)
             X.BLOCK = 256;
-            X.M = 8;
+            X.M = X.pred_slots.size() >= 3 ? 2 : 4;
             X.KO = 2;  // the (rare) dense output pass two slices at a time: fewer registers
         }
     }

@@ -3,7 +3,7 @@
 # sub-tiles") on the low-selectivity lines: C2 at s = 1% and C4, forced per
 # variant with the diagnostic knob (DFMI_DIAG=1 DFMI_NUMERIC_SUBTILES=M; M=1:
 # the one-tile kernel, the adaptive choice disabled with DFMI_NUMERIC_SUBTILES=1),
-# alternating variants twice on the same box.
+# alternating variants twice on the same box; variant d = the adaptive default.
 # usage: tools/ab_subtiles.sh [out file] [variants...]
 set -o pipefail
 OUT=${1:-gpurun_out/ab_subtiles.log}
@@ -13,7 +13,8 @@ mkdir -p $(dirname $OUT)
 : > $OUT
 for rep in 1 2; do
   for m in $VARIANTS; do
-    DFMI_DIAG=1 DFMI_NUMERIC_SUBTILES=$m timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --sel 0.01 \
+    if [ "$m" = d ]; then E=""; else E="DFMI_DIAG=1 DFMI_NUMERIC_SUBTILES=$m"; fi  # d: the adaptive default
+    env $E timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --sel 0.01 \
         --sweep 0.01 --no-cpu --extra c4 --gather 0 > gpurun_out/ab_sub_$m.json 2> gpurun_out/ab_sub_$m.err \
         || { tail gpurun_out/ab_sub_$m.err; exit 1; }
     python3 - $m $rep >> $OUT <<'EOF'
