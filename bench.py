@@ -99,7 +99,7 @@ class FusedStep:
         return self.outs[0].length
 
 
-PROFILE_TAG = "profiles/r03"
+PROFILE_TAG = "profiles/r04"
 PROFILE_DIR = os.path.join(ROOT, PROFILE_TAG)
 
 
@@ -109,7 +109,7 @@ def kernel_name(eng):
 
 
 def profiled(kernel, run="main"):
-    """The committed rocprofv3 record of `kernel` (tools/profile_r03.sh: kernel
+    """The committed rocprofv3 record of `kernel` (tools/profile_r04.sh: kernel
     trace + separate FETCH_SIZE / WRITE_SIZE passes of the same bench command,
     tools/traffic.py): the entry of its largest grid in PROFILE_DIR/<run>, or None."""
     try:
