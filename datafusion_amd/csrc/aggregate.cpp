@@ -242,7 +242,7 @@ struct AggBuilt {
 };
 
 void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in, uint32_t flags,
-                    AggBuilt& B) {
+                    AggBuilt& B, bool low_sel = false) {
     Err& se = B.se;
     jit::Launch& X = B.X;
     const int64_t n = in->num_rows;
@@ -327,8 +327,18 @@ void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const df
         if (const char* kk = getenv("DFMI_ROWS_PER_THREAD")) X.K = atoi(kk);
         if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
     }
+    // a predicate that selected < 4% of the rows the last time this state
+    // ran the query (dfmi_aggregate_batch keeps the kernel's count): M
+    // sub-tiles per block, the arguments loaded by one lane per selected row
+    // (jit.cpp generate_agg; numeric, non-Boolean arguments)
+    bool can_sub = pred && !st->grouped && X.utf8_cols.empty();
+    for (int s : X.proj_slots) can_sub = can_sub && X.col_type(X.num_cols[s]) != DFMI_TYPE_BOOLEAN;
+    for (int s : X.pred_slots) can_sub = can_sub && X.col_type(X.num_cols[s]) != DFMI_TYPE_BOOLEAN;
+    if (can_sub && low_sel && in->num_rows >= (1 << 22)) X.M = X.pred_slots.size() >= 3 ? 2 : 4;
+    if (getenv("DFMI_DIAG"))  // diagnostics: force M
+        if (const char* e = getenv("DFMI_AGG_SUBTILES")) X.M = can_sub ? std::max(1, std::min(16, atoi(e))) : 1;
     if (X.K < 1 || X.K > 32) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
-    const int64_t tile_rows = (int64_t)X.BLOCK * X.K;
+    const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
     B.n_tiles = (n + tile_rows - 1) / tile_rows;
     if (B.n_tiles > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
 }
@@ -800,9 +810,13 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             HIP_TRY(hipSetDevice(ctx->device));
             in = unslice(in, 1, us_, true, ctx->stream);
         }
+        // the query's selectivity last time (this state, this predicate)
+        const uint64_t hint_key = (uint64_t)(uintptr_t)st * 1099511628211ull ^ (uint64_t)(uintptr_t)pred;
+        const auto hint = ctx->sel_hint.find(hint_key);
+        const bool low_sel = hint != ctx->sel_hint.end() && hint->second < 0.04;
         AggBuilt B;
         try {
-            build_agg_plan(st, pred, in, flags, B);
+            build_agg_plan(st, pred, in, flags, B, low_sel);
         } catch (const Fail& f) {
             if (f.code == DFMI_ERR_NOT_IMPLEMENTED && B.se.set) throw Fail{B.se.code, B.se.msg};
             throw;
@@ -910,6 +924,11 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             HIP_TRY(hipStreamSynchronize(stream));
             uint64_t ew;
             memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
+            if (pred && !st->grouped) {  // the kernel's count of selected rows
+                uint64_t sel;
+                memcpy(&sel, ctx->host_hdr + kHdrTotals, 8);
+                ctx->sel_hint[hint_key] = (double)sel / (double)n;
+            }
             if (ew) {
                 dev_key = ~ew;
                 dev_kind = (int)(dev_key & 15);

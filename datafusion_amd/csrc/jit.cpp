@@ -620,10 +620,31 @@ static std::vector<int> emit_predicate(Gen& g, std::ostringstream& o, const Plan
     return offs_loaded;
 }
 
-// Fused Selection + Aggregate kernel (DFMI_FLAG_EXT_AGGREGATE): one block per
-// tile, no compaction and no look-back -- the selected rows' argument values
-// are reduced in registers, the block's partial goes to a global accumulator
-// copy (jit_skeleton.hip "aggregate extension").
+// Numeric slots the aggregates' arguments read (the sub-tile form's
+// accumulation passes reload exactly these for the selected rows).
+static std::vector<int> agg_arg_slots(const Plan& P, const Launch& X) {
+    std::vector<int> out;
+    for (const AggSpec& a : P.aggs)
+        for (const IrNode& nd : a.prog->ir)
+            if (nd.kind == IR_COL)
+                for (size_t s = 0; s < X.num_cols.size(); ++s)
+                    if (X.num_cols[s] == nd.col && std::find(out.begin(), out.end(), (int)s) == out.end())
+                        out.push_back((int)s);
+    std::sort(out.begin(), out.end());
+    return out;
+}
+
+// Fused Selection + Aggregate kernel (DFMI_FLAG_EXT_AGGREGATE): no compaction
+// and no look-back -- the selected rows' argument values are reduced in
+// registers, the block's partial goes to a global accumulator copy
+// (jit_skeleton.hip "aggregate extension"). One tile per block; or, for a
+// predicate that selected few rows last time (aggregate.cpp, Launch::M > 1),
+// M sub-tiles per block: the predicate passes keep only each wave's ballots
+// (LDS) and a list of its selected rows, then one lane per selected row loads
+// the arguments and accumulates -- one dependent round of loads for the M
+// sub-tiles instead of one per tile (a wave whose list overflows reloads its
+// arguments per sub-tile, lane-masked). The kernel also counts the selected
+// rows (totals[0]), which the host keeps as the query shape's selectivity.
 static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X) {
     const int NA = (int)P.aggs.size();
     int NF = 0;
@@ -644,60 +665,123 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     o << "};\n";
     o << "  if (wave == 0) dfmi::agg_lds_init<NA, NF>(S, is_min, lane);\n";
     o << "  const unsigned t = tile_;\n";
-    emit_decls(o, X.pred_slots, X, "", true);
-    emit_decls(o, X.proj_slots, X, "", !P.pred);
-    emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
-    o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
-    if (P.pred) {
-        g.filtered_cols = false;
-        // proj_dense: argument-only columns loaded for every row, in the
-        // predicate's memory round trip
-        if (X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", nullptr, false);
-        emit_predicate(g, o, P, X, "", {});
-        // argument-only columns, loaded only where selected
-        if (!X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
-    } else {
-        o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) selm |= (unsigned)(base + k * BLOCK "
-             "+ tid < A.n_rows) << k;\n";
-        emit_loads(o, X.proj_slots, X, "", "base", nullptr, true);
-    }
-    // arguments over the filtered batch (no validity) or the batch itself
-    g.filtered_cols = P.pred != nullptr;
-    for (int j = 0; j < NA; ++j)
-        o << "  unsigned acnt" << j << " = 0, afl" << j << " = 0;\n  u64 asum" << j << " = 0, akey" << j << " = "
-          << (P.aggs[j].fn == DFMI_AGG_MIN ? "~0ull" : "0ull") << ";\n";
-    o << "  dfmi::lds_sync();\n";
-    o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
-      << "    const i64 row = base + k * BLOCK + tid;\n    const bool sel = (selm >> k) & 1;\n";
-    for (int j = 0; j < NA; ++j) {
-        const AggSpec& a = P.aggs[j];
-        const Val v = g.emit(a.prog, a.prog->root, a.ord_base, "sel");
-        const std::string ok = "ok" + std::to_string(j) + "_";
-        o << "    { const bool " << ok << " = sel && (" << v.n << ");\n";
-        o << "      acnt" << j << " += " << ok << " ? 1u : 0u;\n";
-        if (a.fn == DFMI_AGG_SUM && a.fslot < 0) {
-            o << "      asum" << j << " += " << ok << " ? (u64)(" << (is_signed_int(a.arg_type) ? "i64" : "u64") << ")("
-              << v.v << ") : 0ull;\n";
-        } else if (a.fn == DFMI_AGG_SUM) {
-            o << "      afl" << j << " |= " << ok << " ? dfmi::agg_sum_flags(" << v.v << ") : 0u;\n"
-              << "      const bool fin_ = " << ok << " && (dfmi::agg_sum_flags(" << v.v << ") == dfmi::AGGF_NONNEGZERO) && ("
-              << v.v << ") != 0;\n"
-              << "      dfmi::fsum_add(S.limbs[" << a.fslot << "], &S.dlo[" << a.fslot << "], &S.dhi[" << a.fslot
-              << "], (double)(" << v.v << "), fin_, lane);\n";
-        } else if (a.fn == DFMI_AGG_MIN || a.fn == DFMI_AGG_MAX) {
-            const char* cmp = a.fn == DFMI_AGG_MIN ? "<" : ">";
-            o << "      const bool nan_ = dfmi::agg_isnan(" << v.v << ");\n"
-              << "      afl" << j << " |= " << ok << " ? (nan_ ? (unsigned)dfmi::AGGF_NAN : (unsigned)dfmi::AGGF_VALUE) : 0u;\n"
-              << "      if (" << ok << " && !nan_) { const u64 k_ = dfmi::agg_key(" << v.v << "); if (k_ " << cmp << " akey" << j
-              << ") akey" << j << " = k_; }\n";
+    // the reduction of row `row` (selected: `sel`) at register index k
+    auto emit_accumulate = [&]() {
+        for (int j = 0; j < NA; ++j) {
+            const AggSpec& a = P.aggs[j];
+            const Val v = g.emit(a.prog, a.prog->root, a.ord_base, "sel");
+            const std::string ok = "ok" + std::to_string(j) + "_";
+            o << "    { const bool " << ok << " = sel && (" << v.n << ");\n";
+            o << "      acnt" << j << " += " << ok << " ? 1u : 0u;\n";
+            if (a.fn == DFMI_AGG_SUM && a.fslot < 0) {
+                o << "      asum" << j << " += " << ok << " ? (u64)(" << (is_signed_int(a.arg_type) ? "i64" : "u64") << ")("
+                  << v.v << ") : 0ull;\n";
+            } else if (a.fn == DFMI_AGG_SUM) {
+                o << "      afl" << j << " |= " << ok << " ? dfmi::agg_sum_flags(" << v.v << ") : 0u;\n"
+                  << "      const bool fin_ = " << ok << " && (dfmi::agg_sum_flags(" << v.v
+                  << ") == dfmi::AGGF_NONNEGZERO) && (" << v.v << ") != 0;\n"
+                  << "      dfmi::fsum_add(S.limbs[" << a.fslot << "], &S.dlo[" << a.fslot << "], &S.dhi[" << a.fslot
+                  << "], (double)(" << v.v << "), fin_, lane);\n";
+            } else if (a.fn == DFMI_AGG_MIN || a.fn == DFMI_AGG_MAX) {
+                const char* cmp = a.fn == DFMI_AGG_MIN ? "<" : ">";
+                o << "      const bool nan_ = dfmi::agg_isnan(" << v.v << ");\n"
+                  << "      afl" << j << " |= " << ok
+                  << " ? (nan_ ? (unsigned)dfmi::AGGF_NAN : (unsigned)dfmi::AGGF_VALUE) : 0u;\n"
+                  << "      if (" << ok << " && !nan_) { const u64 k_ = dfmi::agg_key(" << v.v << "); if (k_ " << cmp
+                  << " akey" << j << ") akey" << j << " = k_; }\n";
+            }
+            o << "    }\n";
         }
-        o << "    }\n";
+    };
+    auto emit_acc_decls = [&]() {
+        for (int j = 0; j < NA; ++j)
+            o << "  unsigned acnt" << j << " = 0, afl" << j << " = 0;\n  u64 asum" << j << " = 0, akey" << j << " = "
+              << (P.aggs[j].fn == DFMI_AGG_MIN ? "~0ull" : "0ull") << ";\n";
+    };
+    // selected rows of this wave's K slices, summed for the host's hint
+    auto emit_count = [&]() {
+        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) nsel_ += (unsigned)__builtin_popcountll(__ballot((selm >> k) & 1));\n";
+    };
+    if (X.M > 1 && P.pred) {
+        const std::vector<int> arg_slots = agg_arg_slots(P, X);
+        o << "  constexpr int M = " << X.M << ";\n  constexpr unsigned CAP_ = 256;\n"
+          << "  __shared__ unsigned short SLA[WAVES][CAP_];\n  __shared__ u64 WSA[M * K * WAVES];\n"
+          << "  unsigned tot_ = 0, nsel_ = 0;\n";
+        emit_acc_decls();
+        o << "  dfmi::lds_sync();\n";
+        // predicate passes: ballots and the list of selected rows
+        o << "  for (int m_ = 0; m_ < M; ++m_) {\n  const i64 base = ((i64)t * M + m_) * (BLOCK * K);\n  {\n";
+        g.filtered_cols = false;
+        emit_decls(o, X.pred_slots, X, "", true);
+        emit_loads(o, X.pred_slots, X, "", "base", nullptr, true);
+        emit_predicate(g, o, P, X, "", {});
+        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+          << "    const u64 w_ = __ballot((selm >> k) & 1);\n"
+          << "    if (lane == 0) WSA[(m_ * K + k) * WAVES + wave] = w_;\n"
+          << "    if (tot_ + (unsigned)__builtin_popcountll(w_) <= CAP_ && ((w_ >> lane) & 1))\n"
+          << "      SLA[wave][tot_ + dfmi::lane_rank(w_)] = (unsigned short)((m_ * K + k) * 64 + lane);\n"
+          << "    tot_ += (unsigned)__builtin_popcountll(w_);\n  }\n  }\n  }\n"
+          << "  nsel_ = tot_;\n  dfmi::wave_lds_fence();\n";
+        // sparse: one lane per selected row
+        g.filtered_cols = true;
+        o << "  if (tot_ <= CAP_) {\n  for (unsigned r_ = 0; r_ < tot_; r_ += 64) {\n"
+          << "    const bool sel = r_ + (unsigned)lane < tot_;\n"
+          << "    const unsigned e_ = sel ? (unsigned)SLA[wave][r_ + lane] : 0u;\n"
+          << "    const int q_ = (int)(e_ >> 6), ls_ = (int)(e_ & 63u);\n"
+          << "    const i64 row = ((i64)t * M + q_ / K) * (BLOCK * K) + (i64)(q_ % K) * BLOCK + 64 * wave + ls_;\n"
+          << "    const int k = 0;\n";
+        for (int sl : arg_slots) {
+            const std::string ct = ctype(X.col_type(X.num_cols[sl]));
+            o << "    " << ct << " c" << sl << "[1];\n    c" << sl << "[0] = sel ? ((const " << ct << "*)A.col[" << sl
+              << "])[row] : (" << ct << ")0;\n";
+        }
+        emit_accumulate();
+        o << "  }\n  } else {\n";
+        // dense: each sub-tile's arguments reloaded where selected
+        o << "  for (int m_ = 0; m_ < M; ++m_) {\n  const i64 base = ((i64)t * M + m_) * (BLOCK * K);\n"
+          << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k)\n"
+          << "    selm |= (unsigned)((dfmi::lds_uniform_u64(&WSA[(m_ * K + k) * WAVES + wave]) >> lane) & 1) << k;\n"
+          << "  if (!__ballot(selm != 0)) continue;\n";
+        emit_decls(o, arg_slots, X, "", false);
+        emit_loads(o, arg_slots, X, "", "base", "(selm >> k) & 1", false);
+        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+          << "    const i64 row = base + k * BLOCK + tid;\n    const bool sel = (selm >> k) & 1;\n";
+        emit_accumulate();
+        o << "  }\n  }\n  }\n";
+    } else {
+        emit_decls(o, X.pred_slots, X, "", true);
+        emit_decls(o, X.proj_slots, X, "", !P.pred);
+        emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
+        o << "  unsigned nsel_ = 0;\n  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
+        if (P.pred) {
+            g.filtered_cols = false;
+            // proj_dense: argument-only columns loaded for every row, in the
+            // predicate's memory round trip
+            if (X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", nullptr, false);
+            emit_predicate(g, o, P, X, "", {});
+            // argument-only columns, loaded only where selected
+            if (!X.proj_dense) emit_loads(o, X.proj_slots, X, "", "base", "(selm >> k) & 1", false);
+            emit_count();
+        } else {
+            o << "  unsigned selm = 0;\n#pragma unroll\n  for (int k = 0; k < K; ++k) selm |= (unsigned)(base + k * BLOCK "
+                 "+ tid < A.n_rows) << k;\n";
+            emit_loads(o, X.proj_slots, X, "", "base", nullptr, true);
+        }
+        // arguments over the filtered batch (no validity) or the batch itself
+        g.filtered_cols = P.pred != nullptr;
+        emit_acc_decls();
+        o << "  dfmi::lds_sync();\n";
+        o << "#pragma unroll\n  for (int k = 0; k < K; ++k) {\n"
+          << "    const i64 row = base + k * BLOCK + tid;\n    const bool sel = (selm >> k) & 1;\n";
+        emit_accumulate();
+        o << "  }\n";
     }
-    o << "  }\n";
     for (int j = 0; j < NA; ++j)
         o << "  dfmi::agg_wave_flush<NA, NF>(S, " << j << ", acnt" << j << ", asum" << j << ", akey" << j << ", "
           << (P.aggs[j].fn == DFMI_AGG_MIN ? "true" : "false") << ", afl" << j << ", lane);\n";
-    o << "  dfmi::lds_sync();\n  dfmi::agg_block_flush<NA, NF>(A, S, fslot, is_min, tid);\n  }\n";
+    if (P.pred) o << "  if (lane == 0 && nsel_) atomicAdd(A.totals, (u64)nsel_);\n";
+    o << "  dfmi::lds_sync();\n  dfmi::agg_block_flush<NA, NF>(A, S, fslot, is_min, tid);\n";
+    if (!(X.M > 1 && P.pred)) o << "  }\n";
 }
 
 // GROUP BY form of the aggregate kernel (one Boolean / integer key): every
