@@ -924,10 +924,13 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             HIP_TRY(hipStreamSynchronize(stream));
             uint64_t ew;
             memcpy(&ew, ctx->host_hdr + kHdrErr, 8);
-            if (pred && !st->grouped) {  // the kernel's count of selected rows
+            if (pred && !st->grouped) {  // the kernel's count of selected rows in every 64th block
                 uint64_t sel;
                 memcpy(&sel, ctx->host_hdr + kHdrTotals, 8);
-                ctx->sel_hint[hint_key] = (double)sel / (double)n;
+                const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
+                int64_t sampled = 0;
+                for (int64_t b = 0; b < B.n_tiles; b += 64) sampled += std::min(tile_rows, n - b * tile_rows);
+                ctx->sel_hint[hint_key] = sampled ? (double)sel / (double)sampled : 1.0;
             }
             if (ew) {
                 dev_key = ~ew;

@@ -664,6 +664,7 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     }
     o << "};\n";
     o << "  if (wave == 0) dfmi::agg_lds_init<NA, NF>(S, is_min, lane);\n";
+    if (P.pred) o << "  __shared__ unsigned NSEL_;\n  if (tid == 0) NSEL_ = 0;\n";
     o << "  const unsigned t = tile_;\n";
     // the reduction of row `row` (selected: `sel`) at register index k
     auto emit_accumulate = [&]() {
@@ -779,8 +780,11 @@ static void generate_agg(Gen& g, std::ostringstream& o, const Plan& P, Launch& X
     for (int j = 0; j < NA; ++j)
         o << "  dfmi::agg_wave_flush<NA, NF>(S, " << j << ", acnt" << j << ", asum" << j << ", akey" << j << ", "
           << (P.aggs[j].fn == DFMI_AGG_MIN ? "true" : "false") << ", afl" << j << ", lane);\n";
-    if (P.pred) o << "  if (lane == 0 && nsel_) atomicAdd(A.totals, (u64)nsel_);\n";
+    // the selected-row count, sampled: every 64th block adds its count (one
+    // global atomic per 64 blocks -- a counter every wave hit would serialise)
+    if (P.pred) o << "  if (lane == 0 && nsel_) atomicAdd(&NSEL_, nsel_);\n";
     o << "  dfmi::lds_sync();\n  dfmi::agg_block_flush<NA, NF>(A, S, fslot, is_min, tid);\n";
+    if (P.pred) o << "  if (tid == 0 && NSEL_ && (blockIdx.x & 63u) == 0) atomicAdd(A.totals, (u64)NSEL_);\n";
     if (!(X.M > 1 && P.pred)) o << "  }\n";
 }
 
