@@ -334,7 +334,8 @@ void build_agg_plan(const dfmi_agg_state* st, const dfmi_program* pred, const df
     bool can_sub = pred && !st->grouped && X.utf8_cols.empty();
     for (int s : X.proj_slots) can_sub = can_sub && X.col_type(X.num_cols[s]) != DFMI_TYPE_BOOLEAN;
     for (int s : X.pred_slots) can_sub = can_sub && X.col_type(X.num_cols[s]) != DFMI_TYPE_BOOLEAN;
-    if (can_sub && low_sel && in->num_rows >= (1 << 22)) X.M = X.pred_slots.size() >= 3 ? 2 : 4;
+    // (Q6, same-box A/B profiles/r04/q6_ab.log: M = 1 / 2 / 4 -> 2.88 / 2.57 / 2.54 ms)
+    if (can_sub && low_sel && in->num_rows >= (1 << 22)) X.M = 4;
     if (getenv("DFMI_DIAG"))  // diagnostics: force M
         if (const char* e = getenv("DFMI_AGG_SUBTILES")) X.M = can_sub ? std::max(1, std::min(16, atoi(e))) : 1;
     if (X.K < 1 || X.K > 32) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
