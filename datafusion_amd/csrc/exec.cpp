@@ -208,8 +208,11 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
     }
     if ((int)X.num_cols.size() > kArgCols || X.utf8_cols.size() > (size_t)kArgUtf8)
         throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: too many input columns"};
-    // rows per thread: keep the tile's column data resident in VGPRs
-    const size_t nload = X.num_cols.size();
+    // rows per thread: keep the tile's column data resident in VGPRs (a
+    // Utf8 column holds its offsets per row; a kernel gathering many Utf8
+    // columns at K = 8 is also a ~35 s hipRTC compile -- 11 Utf8 outputs:
+    // 35 / 15 / 6.6 s at K = 8 / 4 / 2)
+    const size_t nload = X.num_cols.size() + X.utf8_cols.size();
     X.BLOCK = 512;
     X.K = nload <= 4 ? 8 : (nload <= 8 ? 4 : 2);
     // a predicate over Utf8 columns only reads ~4 B/row of offsets: its tiles
