@@ -38,6 +38,11 @@ struct BatchStage {
     uint64_t* clear_bhdr = nullptr;
     int64_t clear_bhdr_words = 0;
     bool* cleared = nullptr;
+    // Device-visible address of *host_hdr: when every batch is one tile, the
+    // kernel's blocks write the finished headers there themselves
+    // (Launch::hdr_out), and *hdr_written is set -- no header copy needed.
+    uint64_t* hdr_out = nullptr;
+    bool* hdr_written = nullptr;
 };
 
 // Diagnostics (DFMI_DIAG + DFMI_CALL_PROFILE): host time per phase of an

@@ -805,21 +805,25 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
         hipStream_t st = ctx->stream;
         ctx->timed = false;
         ctx->last_compile_ms = 0;
+        // ---- tiles per batch
+        const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
+        std::vector<int64_t> first(nb), tiles(nb);
+        int64_t T = 0, max_tiles = 0;
+        for (int32_t b = 0; b < nb; ++b) {
+            tiles[b] = (ins[b].num_rows + tile_rows - 1) / tile_rows;
+            first[b] = T;
+            T += tiles[b];
+            max_tiles = std::max(max_tiles, tiles[b]);
+        }
+        if (T > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
+        // one tile per batch and a caller that can take the headers in place
+        X.hdr_out = stage && stage->hdr_out && max_tiles <= 1;
         prof.mark(0);
         const hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
         ctx->last_kernel = X.kname;
         prof.mark(1);
 
         // ---- batch table
-        const int64_t tile_rows = (int64_t)X.BLOCK * X.K * X.M;
-        std::vector<int64_t> first(nb), tiles(nb);
-        int64_t T = 0;
-        for (int32_t b = 0; b < nb; ++b) {
-            tiles[b] = (ins[b].num_rows + tile_rows - 1) / tile_rows;
-            first[b] = T;
-            T += tiles[b];
-        }
-        if (T > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
         const int NPW = jit::batch_words(X, nout);
         const size_t table_bytes = (size_t)nb * NPW * 8, meta_bytes = table_bytes + (size_t)T * 4;
         // the table and the per-batch headers: in the caller's staging (one
@@ -941,6 +945,7 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
                 if (stage) {
                     A.clear_bhdr = (unsigned long long*)stage->clear_bhdr;
                     A.clear_bhdr_words = stage->clear_bhdr_words;
+                    if (X.hdr_out) A.hdr_out = (unsigned long long*)stage->hdr_out;
                 }
                 if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, st));
                 size_t asz = sizeof A;
@@ -948,6 +953,7 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
                 HIP_TRY(hipModuleLaunchKernel(fn, (unsigned)T, 1, 1, X.BLOCK, 1, 1, 0, st, nullptr, cfg));
                 ws_commit(ctx, ws);
                 if (stage && stage->cleared) *stage->cleared = true;
+                if (X.hdr_out && stage->hdr_written) *stage->hdr_written = true;
                 if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, st));
                 if (!staged) HIP_TRY(hipMemcpyAsync(ctx->host_bhdr, ctx->bhdr, (size_t)nb * kBHdr, hipMemcpyDeviceToHost, st));
             }

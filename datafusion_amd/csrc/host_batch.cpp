@@ -1336,8 +1336,14 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         const bool zc = zc_env > 0 || (zc_env < 0 && in_bytes + MB <= kZeroCopyBytes);
         prof.mark(1);
         const int half = A.hb_half, other = 1 - half;
-        uint8_t* const dout = A.hb_half_base(half) + A.hb_hcap;
-        uint8_t* const dhdr = dout - H;
+        // the result's pinned block [headers | outputs]; a small call's kernel
+        // writes its outputs there directly (and, one tile per batch, the
+        // finished headers too: Launch::hdr_out) -- no copy back at all
+        R->arena = R->pool->get(H + OB);
+        uint8_t* res_dev = nullptr;
+        if (zc) HIP_TRY(hipHostGetDevicePointer((void**)&res_dev, R->arena.p, 0));
+        uint8_t* const dhdr = A.hb_half_base(half) + A.hb_hcap - H;  // the kernel's header atomics
+        uint8_t* const dout = zc ? res_dev + H : A.hb_half_base(half) + A.hb_hcap;
         uint8_t* const dev = zc ? A.pin_dev : A.hb + 2 * (A.hb_hcap + A.hb_ocap);  // inputs
         std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
         std::vector<dfmi_batch> dins(nb);
@@ -1367,11 +1373,10 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                 d.data_capacity = (int64_t)L.ndat;
             }
         }
-        // ---- (one H2D), the coalesced launch, one D2H, one synchronisation
-        R->arena = R->pool->get(H + OB);
+        // ---- (one H2D), the coalesced launch, (one D2H), one synchronisation
         size_t meta_used = 0;
         hipError_t copy_err = hipSuccess;
-        bool cleared = false;
+        bool cleared = false, hdr_written = false;
         dfmi::BatchStage stage;
         stage.locate = [&](size_t meta_bytes, size_t hdr_bytes, uint8_t** host_meta, uint8_t** dev_meta,
                            uint8_t** dev_hdr, const uint8_t** host_hdr) {
@@ -1386,16 +1391,21 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         stage.copy_in = [&](hipStream_t s) {
             hipError_t e = hipSuccess;
             if (A.hb_dirty[half])  // headers the other half's last kernel did not zero (an earlier failed call)
-                e = hipMemsetAsync(dout - A.hb_dirty[half], 0, A.hb_dirty[half], s);
+                e = hipMemsetAsync(A.hb_half_base(half) + A.hb_hcap - A.hb_dirty[half], 0, A.hb_dirty[half], s);
             if (e == hipSuccess && !zc)
                 e = hipMemcpyAsync(dev, pin_in, meta_used ? IB + meta_used : in_bytes, hipMemcpyHostToDevice, s);
             if (e != hipSuccess) copy_err = e;
             else A.hb_dirty[half] = 0;
         };
         stage.copy_out = [&](hipStream_t s) {
-            const hipError_t e = hipMemcpyAsync(R->arena.p, dhdr, H + OB, hipMemcpyDeviceToHost, s);
+            if (zc && hdr_written) return;  // outputs and headers are in place
+            const hipError_t e = hipMemcpyAsync(R->arena.p, dhdr, zc ? H : H + OB, hipMemcpyDeviceToHost, s);
             if (e != hipSuccess) copy_err = e;
         };
+        if (zc) {
+            stage.hdr_out = (uint64_t*)res_dev;
+            stage.hdr_written = &hdr_written;
+        }
         stage.clear_bhdr = (uint64_t*)(A.hb_half_base(other) + A.hb_hcap - A.hb_dirty[other]);
         stage.clear_bhdr_words = (int64_t)(A.hb_dirty[other] / 8);
         stage.cleared = &cleared;

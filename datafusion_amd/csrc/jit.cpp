@@ -1257,6 +1257,15 @@ std::string generate(const Plan& P, Launch& X) {
                 o << "  if (lane == 0 && nulls[" << oi << "]) atomicAdd(&A.totals[8 + " << oi << "], (u64)nulls[" << oi
                   << "]);\n";
     }
+    if (X.batched && X.hdr_out)
+        // one tile per batch: this block made its batch's whole header (row /
+        // byte totals, null counts, error word) -- once every wave's atomics
+        // are done, copy it out (the host's pinned result block: no copy
+        // back after the kernel) and leave it zero for the next call
+        o << "  __threadfence();\n  __syncthreads();\n"
+          << "  if (tid < 32) {\n    u64* h_ = (u64*)bp_[2];\n"
+          << "    const u64 v_ = __hip_atomic_load(h_ + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+          << "    A0.hdr_out[(i64)b_ * 32 + tid] = v_;\n    h_[tid] = 0;\n  }\n";
     o << "}\n";
     // kernel name: the plan kind and a hash of the generated body, so that
     // rocprofv3 reports every query shape as its own kernel
@@ -1317,7 +1326,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

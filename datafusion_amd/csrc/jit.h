@@ -64,6 +64,9 @@ struct Launch {
     // (64 cost ~9% of the C2 kernel in polling traffic)
     int window = 8;
     int late_proj = 0;  // projection-only columns loaded after the look-back (byte-light predicates)
+    // coalesced batches of one tile each (host_batch.cpp small calls): every
+    // block copies its batch's finished header to Args::hdr_out and zeroes it
+    int hdr_out = 0;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

@@ -64,6 +64,7 @@ struct Args {
     // previous call, in the other half of its ping-pong device region
     u64* clear_bhdr;
     i64 clear_bhdr_words;
+    u64* hdr_out;  // Launch::hdr_out: [batch][32] finished headers (host memory)
     u64* agg;                          // aggregate extension: [copies][aggs][kAggWords] accumulators
     // coalesced batches (dfmi_filter_project_batches): block -> batch, and
     // per batch a row of pointers / sizes the kernel's prologue loads into a
