@@ -397,7 +397,8 @@ void finish_bitmap(uint8_t* b, int64_t n) {
 constexpr int kSlots = 3;
 // a host batch up to this size skips the chunk pipeline (one H2D, one
 // launch, one D2H, one synchronisation: dfmi_filter_project_host)
-constexpr size_t kZeroCopyBytes = 256 << 10;  // inputs + batch table read in place up to this size (DFMI_HOST_ZC)
+constexpr size_t kZeroCopyBytes = 8 << 20;  // inputs + batch table read in place up to this size (DFMI_HOST_ZC;
+                                             // 256 x 1024-row batches: 1.28 -> 1.00 us per batch, profiles/r04/zc_ab2.log)
 constexpr int64_t kSmallRows = 1 << 16;
 constexpr size_t kSmallBytes = (size_t)4 << 20;
 
