@@ -275,6 +275,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 6;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
         if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_TICKET")) X.ticket = atoi(e) & 1;  // ticket-ordered tiles from the start
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         // the numeric sub-tile kernel at any size (parity tests, A/B runs)
@@ -644,6 +645,10 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                     A.mode &= ~16;          // (diagnostic forced timeout: once)
                     dev_kind = 0;
                     dev_key = ~0ull;
+                    // relaunched with ticket-ordered tiles: every look-back then
+                    // waits only on running blocks, whatever else holds the CUs
+                    X.ticket = 1;
+                    fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
                     continue;
                 }
                 break;
@@ -819,7 +824,7 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
         // one tile per batch and a caller that can take the headers in place
         X.hdr_out = stage && stage->hdr_out && max_tiles <= 1;
         prof.mark(0);
-        const hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
+        hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
         ctx->last_kernel = X.kname;
         prof.mark(1);
 
@@ -975,6 +980,8 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
             ctx->ws_valid = false;  // status words in an unknown state: re-zero all
             ++ctx->relaunches;
             mode &= ~16;  // (diagnostic forced timeout: once)
+            X.ticket = 1;  // ticket-ordered tiles (see dfmi_filter_project)
+            fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
         }
         if (T > 0 && ctx->timing) {
             float m1 = 0;

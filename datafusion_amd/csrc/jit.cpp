@@ -896,13 +896,13 @@ static void generate_agg_grouped(Gen& g, std::ostringstream& o, const Plan& P, L
 // with constants, so it lives in registers: no scratch).
 static void emit_batched_prologue(std::ostream& o, const Plan& P, const Launch& X) {
     const int np = batch_words(X, (int)P.outs.size());
-    o << "  const int b_ = A0.tile_batch[blockIdx.x];\n"
+    o << "  const int b_ = A0.tile_batch[bid_];\n"
       << "  void* const* bp_ = A0.batch_ptrs + (i64)b_ * " << np << ";\n"
       << "  dfmi::Args A = A0;\n"
       << "  A.n_rows = (i64)(u64)bp_[0];\n"
       << "  const u64 tt_ = (u64)bp_[1];\n"
       << "  A.n_tiles = (int)(unsigned)tt_;\n"
-      << "  const unsigned tile_ = blockIdx.x - (unsigned)(tt_ >> 32);\n"
+      << "  const unsigned tile_ = bid_ - (unsigned)(tt_ >> 32);\n"
       << "  A.totals = (u64*)bp_[2];\n  A.err = (u64*)bp_[3];\n"
       // diagnostics (mode bit 4): the forced look-back timeout in the first
       // batch's own error word, which the coalesced launch's host reads
@@ -936,11 +936,16 @@ std::string generate(const Plan& P, Launch& X) {
     o << "  constexpr int BLOCK = " << BLOCK << ", K = " << K << ", WAVES = BLOCK / 64;\n";
     o << "  const int tid = threadIdx.x, lane = tid & 63, wave = dfmi::uni(tid >> 6);\n";
     o << "  dfmi::clear_previous<BLOCK>(A0, blockIdx.x, tid);\n";
+    if (X.ticket && P.pred && P.aggs.empty())
+        o << "  __shared__ unsigned tk_;\n  if (tid == 0) tk_ = atomicAdd(A0.ticket, 1u);\n  __syncthreads();\n"
+          << "  const unsigned bid_ = tk_;\n";
+    else
+        o << "  const unsigned bid_ = blockIdx.x;\n";
     if (X.batched) {
         if (!P.aggs.empty()) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batched launch of an aggregate"};
         emit_batched_prologue(o, P, X);
     } else {
-        o << "  const dfmi::Args& A = A0;\n  const unsigned tile_ = blockIdx.x;\n";
+        o << "  const dfmi::Args& A = A0;\n  const unsigned tile_ = bid_;\n";
     }
     if (!P.aggs.empty() && P.gkey) {
         generate_agg_grouped(g, o, P, X);
@@ -1326,7 +1331,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -67,6 +67,11 @@ struct Launch {
     // coalesced batches of one tile each (host_batch.cpp small calls): every
     // block copies its batch's finished header to Args::hdr_out and zeroes it
     int hdr_out = 0;
+    // tiles taken from an atomic ticket in the order blocks start instead of
+    // blockIdx: a look-back then only waits on tiles whose blocks are running
+    // (the relaunch after a look-back timeout, e.g. when another process's
+    // kernel holds the CUs the next tiles in dispatch order would need)
+    int ticket = 0;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their
