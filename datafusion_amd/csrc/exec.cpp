@@ -649,6 +649,10 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
                     // waits only on running blocks, whatever else holds the CUs
                     X.ticket = 1;
                     fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
+                    memcpy(A.lits, X.args_lits, sizeof A.lits);  // (that kernel's literal slots)
+                    memcpy(A.str_off, X.str_off, sizeof A.str_off);
+                    memcpy(A.str_len, X.str_len, sizeof A.str_len);
+                    memcpy(A.str, X.str, sizeof A.str);
                     continue;
                 }
                 break;

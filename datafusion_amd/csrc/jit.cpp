@@ -926,6 +926,7 @@ static void emit_batched_prologue(std::ostream& o, const Plan& P, const Launch& 
 }
 
 std::string generate(const Plan& P, Launch& X) {
+    X.n_lits = X.n_str = X.str_bytes = 0;  // (slots are assigned anew by every generation)
     Gen g(P, X);
     std::ostringstream& o = g.o;
     const int K = X.K, BLOCK = X.BLOCK;
