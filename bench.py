@@ -1069,6 +1069,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if BACKEND != "nccl":
         local %= torch.cuda.device_count()
+        if world > torch.cuda.device_count():
+            # ranks sharing a GPU: ticket-ordered tiles from the first launch
+            # (DESIGN.md §4 "Look-back": blockIdx order can stall behind the
+            # other rank's kernel until the 2 s timeout and its relaunch)
+            os.environ["DFMI_DIAG"] = "1"
+            os.environ["DFMI_TICKET"] = "1"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
