@@ -276,6 +276,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
         if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
         if (const char* e = getenv("DFMI_TICKET")) X.ticket = atoi(e) & 1;  // ticket-ordered tiles from the start
+        if (const char* e = getenv("DFMI_UTF8_EARLY")) X.early = atoi(e) & 1;
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         // the numeric sub-tile kernel at any size (parity tests, A/B runs)

@@ -1049,7 +1049,8 @@ std::string generate(const Plan& P, Launch& X) {
                       << (X.gather == 2 ? "" : X.gather == 4 ? (X.pairs ? ", 3" : X.st16 ? ", 4" : ", 1") : X.gather == 5 ? ", 2" : ", 0")
                       << (X.gather == 2 ? "" : (prestaged && j == 0 ? ", pre_" : ", -1"))
                       << (X.gather == 2 ? "" : X.gather_phases ? ", true" : ", false")
-                      << (X.gather == 2 ? "" : X.dbuf ? ", true" : ", false") << ");\n";
+                      << (X.gather == 2 ? "" : X.dbuf ? ", true" : ", false")
+                      << (X.gather == 2 || !X.early ? "" : ", true") << ");\n";
             }
             if (!X.utf8_outs.empty()) o << "  }\n";
         };
@@ -1332,7 +1333,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -72,6 +72,7 @@ struct Launch {
     // (the relaunch after a look-back timeout, e.g. when another process's
     // kernel holds the CUs the next tiles in dispatch order would need)
     int ticket = 0;
+    int early = 0;  // Utf8 gather: stage the next group before the last slice's stores (DFMI_UTF8_EARLY)
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

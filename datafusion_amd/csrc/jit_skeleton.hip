@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
                                             unsigned selm, const u64 (&wm)[K], const unsigned (&dst)[K],
                                             const int (&s)[K], const int (&nx)[K], Utf8Stage<ARENA, DST>& G, int lane,
                                             int wave, int kb = 0, int emit = 0, int pre = -1, bool prof = false,
-                                            bool dbuf = false) {
+                                            bool dbuf = false, bool early = false) {
     constexpr int WAVES = BLOCK / 64;
     const u64 bpre = T.prefix[ch];
     const i64 obase = (i64)T.prefix[0];
@@ -1186,6 +1186,13 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
     u8* out = A.out_data[o];
     const unsigned* gs = (const unsigned*)G.src;
     unsigned* gd = (unsigned*)G.dst;
+    // early (LDS image, one arena): the next group's spans are staged as soon
+    // as the group's last slice is placed -- before that slice's image
+    // stores -- so the staging wait counts those stores out instead of
+    // waiting for them (vmcnt counts loads and stores in issue order)
+    bool e_pend = false;  // a group staged early is in flight: slices (staged_to, e_to]
+    int e_to = -1;
+    unsigned e_since = 0;  // store instructions issued after it (a lower bound)
     int staged_to = pre;  // slices <= staged_to are in the arena (or need no staging)
     int aoff = 0;         // arena chunk of the next staged slice to process
     int cs[K];
@@ -1269,7 +1276,15 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         tick(1);
         if (k > staged_to) {
             if (emit == 3) flush_single();  // the arena is about to be restaged
-            if (!dbuf) {
+            if (e_pend) {
+                if (e_since >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if (e_since >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else if (e_since >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                else wait_vm_loads();
+                staged_to = e_to;
+                e_pend = false;
+                aoff = 0;
+            } else if (!dbuf) {
                 staged_to = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k, G.src, lane);
                 wait_vm_loads();
                 aoff = 0;
@@ -1365,6 +1380,15 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         tick(2);
         if (L) utf8_place(gs + 4 * my_off, gd, (int)(s[k] - c0), sh + (int)rel, (int)L);
         wave_lds_fence();
+        if (early && !dbuf && emit == 1 && k == staged_to && k + 1 < K) {
+            // the arena's last slice is placed: stage the next group now
+            const int nt = utf8_stage_group<K, ARENA>(src, wm, cs, cn, k + 1, G.src, lane);
+            if (nt > k) {
+                e_pend = true;
+                e_to = nt;
+                e_since = 0;
+            }
+        }
         tick(3);
         if (emit == 4) {
             utf8_image_store16(G.dst, w0, sh, (int)Ls, lane);
@@ -1387,6 +1411,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         wave_lds_fence();
         tick(4);
         since += 2;  // this slice's out_offs store and at least one image store
+        if (e_pend) e_since += (unsigned)((nw + 63) >> 6);  // one store instruction per round at least
     }
     if (emit == 3) flush_single();
     if (tp_on && lane == 0)
