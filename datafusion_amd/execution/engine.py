@@ -260,10 +260,14 @@ class DeviceEngine:
                                         progs, len(projections), C.byref(cb), flags, C.byref(res), C.byref(err))
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
-        try:
-            return _host_result_arrays(res)
-        finally:
+        # views into the result's pinned block where it has one (a small call:
+        # no copy), copies of its per-column buffers otherwise; the result is
+        # freed with the last view
+        n = L.dfmi_host_result_num_columns(res)
+        if n == 0:
             L.dfmi_host_result_free(res)
+            return []
+        return HostBatchColumns(HostResultBlock(res, n, n), 0, n).materialize()
 
     def filter_project_host_batches(self, predicate, projections: Optional[Sequence], batches: Sequence[RecordBatch],
                                     flags: int = 0):
@@ -605,35 +609,6 @@ class ShardComm:
             except Exception:
                 pass
             self.handle = C.c_void_p(0)
-
-
-def _host_result_arrays(res) -> List[Array]:
-    """Every column of a dfmi_host_result, copied into host Arrays."""
-    import numpy as np
-    from ..arrow import _bytes_tensor, _offsets_tensor
-    L = _abi.lib()
-    out = []
-    for i in range(L.dfmi_host_result_num_columns(res)):
-        v = _abi.dfmi_column()
-        L.dfmi_host_result_column(res, i, C.byref(v))
-        t = DataType(v.type)
-        n = v.length
-        if t == DataType.Utf8:
-            offs = (np.ctypeslib.as_array(C.cast(v.offsets, C.POINTER(C.c_int32)), shape=(n + 1,)).copy()
-                    if v.offsets else np.zeros(1, np.int32))
-            nb = int(offs[-1])
-        else:
-            offs = None
-            nb = (n + 7) // 8 if t == DataType.Boolean else n * t.width
-        vals = (np.ctypeslib.as_array(C.cast(v.values, C.POINTER(C.c_uint8)), shape=(nb,))
-                if nb else np.zeros(0, np.uint8))
-        valid = None
-        if v.null_count and v.validity:
-            valid = _bytes_tensor(np.ctypeslib.as_array(C.cast(v.validity, C.POINTER(C.c_uint8)),
-                                                    shape=((n + 7) // 8,)).copy())
-        out.append(Array(t, n, _bytes_tensor(vals.copy()), valid,
-                         _offsets_tensor(offs, "cpu") if offs is not None else None, v.null_count))
-    return out
 
 
 # ---- host batches: vectorised ABI structs in, zero-copy result slices out
