@@ -282,13 +282,16 @@ class DeviceEngine:
         return self._host_batches_finish(prep, self._host_batches_call(prep))
 
     def filter_project_host_batches_async(self, predicate, projections: Optional[Sequence],
-                                          batches: Sequence[RecordBatch], flags: int = 0) -> "HostBatchesFuture":
+                                          batches: Sequence[RecordBatch], flags: int = 0,
+                                          schema: Schema = None) -> "HostBatchesFuture":
         """filter_project_host_batches whose C call runs on the engine's worker
         thread (ctypes releases the GIL for it): the caller hands out the
         previous group's batches while this group's staging, PCIe copies and
         launch proceed. The batches' structs are built here, on the calling
-        thread; result() gives what filter_project_host_batches returns. The
-        engine runs one call at a time: every other entry point waits for an
+        thread; result() gives what filter_project_host_batches returns -- or,
+        with `schema`, the output RecordBatches themselves (HostResultBatch:
+        one object per batch, its Arrays built when first read). The engine
+        runs one call at a time: every other entry point waits for an
         in-flight one first (drain)."""
         self.drain()
         prep = self._host_batches_prepare(predicate, projections, batches, flags)
@@ -297,7 +300,7 @@ class DeviceEngine:
             self._worker = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dfmi-engine")
         fut = self._worker.submit(self._host_batches_call, prep)
         self._inflight = fut
-        return HostBatchesFuture(self, prep, fut)
+        return HostBatchesFuture(self, prep, fut, schema)
 
     def drain(self) -> None:
         """Wait for the in-flight asynchronous call (its result stays with its future)."""
@@ -333,7 +336,7 @@ class DeviceEngine:
         return rc, res, failed.value, err
 
     @staticmethod
-    def _host_batches_finish(prep, raw):
+    def _host_batches_finish(prep, raw, schema=None):
         nb, nout = prep[5], prep[6]
         rc, res, failed, err = raw
         if nb == 0:
@@ -346,6 +349,8 @@ class DeviceEngine:
                 raise error
         done = nb if error is None else max(0, failed)
         block = HostResultBlock(res, done * nout, nout)
+        if schema is not None:
+            return [HostResultBatch.make(schema, block, b, nout) for b in range(done)], error
         return [HostBatchColumns(block, b, nout) for b in range(done)], error
 
     # ---- aggregate extension (DFMI_FLAG_EXT_AGGREGATE)
@@ -634,14 +639,14 @@ def host_batch_structs(batches: Sequence[RecordBatch], ncols: int):
 class HostBatchesFuture:
     """An in-flight filter_project_host_batches_async call."""
 
-    def __init__(self, eng: DeviceEngine, prep, fut):
-        self.eng, self.prep, self.fut = eng, prep, fut
+    def __init__(self, eng: DeviceEngine, prep, fut, schema=None):
+        self.eng, self.prep, self.fut, self.schema = eng, prep, fut, schema
 
     def result(self):
         raw = self.fut.result()
         if self.eng._inflight is self.fut:
             self.eng._inflight = None
-        return DeviceEngine._host_batches_finish(self.prep, raw)
+        return DeviceEngine._host_batches_finish(self.prep, raw, self.schema)
 
 
 class _ResultOwner:
@@ -738,3 +743,34 @@ class HostBatchColumns(LazyColumns):
             vals = k.buffer(k.values[i], nb)
             out.append(Array(t, n, vals, valid, None, nulls))
         return out
+
+
+class HostResultBatch(RecordBatch):
+    """Output batch b of a HostResultBlock as the RecordBatch itself (the
+    relations' pull loop over host batches: one Python object per pulled
+    batch). Its Arrays are built when first read (HostBatchColumns)."""
+
+    @classmethod
+    def make(cls, schema, blk: "HostResultBlock", b: int, nout: int) -> "HostResultBatch":
+        r = object.__new__(cls)
+        r.schema, r._blk, r._b, r._n, r._cols = schema, blk, b, nout, None
+        return r
+
+    @property
+    def _columns(self) -> List[Array]:
+        c = self._cols
+        if c is None:
+            c = self._cols = HostBatchColumns(self._blk, self._b, self._n).materialize()
+        return c
+
+    @_columns.setter
+    def _columns(self, cols) -> None:
+        self._cols = list(cols)
+
+    def num_columns(self) -> int:
+        return self._n if self._cols is None else len(self._cols)
+
+    def num_rows(self) -> int:
+        if self._cols is not None:
+            return self._cols[0].length if self._cols else 0
+        return self._blk.length[self._b * self._n] if self._n else 0

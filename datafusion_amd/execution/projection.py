@@ -46,10 +46,15 @@ class ProjectRelation(Relation):
             return RecordBatch.lazy(self._batch_schema, cols)
         return RecordBatch(self._batch_schema, cols)
 
+    def _output_schema(self) -> Schema:
+        if self._batch_schema is None:  # projection.rs:52-57, the same for every batch
+            self._batch_schema = Schema([Field(e.get_name(), e.get_type(), True) for e in self.expr])
+        return self._batch_schema
+
     def _wrap_many(self, results) -> list:
-        if self._batch_schema is None:
-            self._wrap(results[0])
-        sch, lazy = self._batch_schema, RecordBatch.lazy
+        if results and isinstance(results[0], RecordBatch):  # already batches (HostResultBatch)
+            return results
+        sch, lazy = self._output_schema(), RecordBatch.lazy
         return [lazy(sch, c) if isinstance(c, LazyColumns) else RecordBatch(sch, c) for c in results]
 
     def run_batch(self, batch: RecordBatch):
@@ -75,7 +80,8 @@ class ProjectRelation(Relation):
                                      lambda bs: engine(self.device).filter_project_host_batches(pred, self.expr, bs,
                                                                                                 self.flags),
                                      run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
-                                         pred, self.expr, bs, self.flags), wrap_many=self._wrap_many)
+                                         pred, self.expr, bs, self.flags, schema=self._output_schema()),
+                                     wrap_many=self._wrap_many)
             # later pulls go straight to the Coalescer (one Python frame less
             # per batch at the reference's 1024-row batch size)
             self.next = self._co.next

@@ -70,3 +70,41 @@ def test_schema_mismatch_and_non_tensor_buffers_are_refused():
     bad.values = np.zeros(32, np.uint8)  # not a torch tensor
     with pytest.raises(TypeError):
         host_batch_structs([RecordBatch(Schema.empty(), [bad])], 1)
+
+
+def fake_block(nb, nout, n):
+    """A HostResultBlock over a host tensor: batch b, column o holds the
+    float64 values b*100 + o*10 + i (i < n), no nulls."""
+    import torch
+    from datafusion_amd.execution.engine import HostResultBlock
+    blk = HostResultBlock.__new__(HostResultBlock)
+    per = ((n * 8 + 255) // 256) * 256
+    vals = np.zeros(nb * nout * per // 8, np.float64)
+    for b in range(nb):
+        for o in range(nout):
+            k = (b * nout + o) * per // 8
+            vals[k:k + n] = b * 100 + o * 10 + np.arange(n)
+    blk.block = torch.from_numpy(vals.view(np.uint8))
+    blk.base = blk.block.data_ptr()
+    blk.end = blk.base + blk.block.numel()
+    m = nb * nout
+    blk.type, blk.length, blk.nulls = [DataType.Float64] * m, [n] * m, [0] * m
+    blk.validity, blk.offsets = [0] * m, [0] * m
+    blk.values = [blk.base + k * per for k in range(m)]
+    return blk
+
+
+def test_host_result_batch():
+    """The relations' one-object-per-batch result (engine.HostResultBatch):
+    row / column counts without building Arrays, Arrays on first read (views
+    of the block), the columns setter, and the glue reading it as input."""
+    from datafusion_amd.execution.engine import HostResultBatch
+    blk = fake_block(3, 2, 5)
+    rb = HostResultBatch.make(Schema.empty(), blk, 1, 2)
+    assert rb.num_rows() == 5 and rb.num_columns() == 2 and rb._cols is None
+    assert [list(c.numpy_values()) for c in rb.columns] == [[100.0 + i for i in range(5)], [110.0 + i for i in range(5)]]
+    barr, keep = host_batch_structs([rb], 2)
+    cols = C.cast(barr[0].columns, C.POINTER(_abi.dfmi_column))
+    assert [as_tuple(cols[j]) for j in range(2)] == [as_tuple(column_struct(a)) for a in rb.columns]
+    rb.columns = rb.columns[:1]
+    assert rb.num_columns() == 1 and rb.num_rows() == 5
