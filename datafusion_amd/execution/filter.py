@@ -150,6 +150,15 @@ class Coalescer:
         return item
 
 
+def _wrap_many_empty(results) -> list:
+    """FilterRelation's output batches (Schema::empty(), filter.rs:60-61):
+    ready-made HostResultBatches pass through."""
+    if results and isinstance(results[0], RecordBatch):
+        return results
+    sch = Schema.empty()
+    return [RecordBatch.lazy(sch, c) if isinstance(c, LazyColumns) else RecordBatch(sch, c) for c in results]
+
+
 class FilterRelation(Relation):
     """FilterRelation::new(input, expr, schema). next() pulls one batch from
     the input and returns every column filtered by the predicate, in a batch
@@ -186,7 +195,8 @@ class FilterRelation(Relation):
                                      lambda bs: engine(self.device).filter_project_host_batches(self.expr, None, bs,
                                                                                                 self.flags),
                                      run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
-                                         self.expr, None, bs, self.flags))
+                                         self.expr, None, bs, self.flags, schema=Schema.empty()),
+                                     wrap_many=_wrap_many_empty)
             return self._co.next()
         batch = self.input.next()
         if batch is None:
