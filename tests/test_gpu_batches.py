@@ -158,12 +158,12 @@ def test_relation_coalesces_batches():
             assert_same(x, y)
 
 
-def _oracle_stream(schema, batches, pred_e, proj_e):
+def _oracle_stream(schema, batches, pred_e, proj_e, flags=0):
     """The reference pull loop's view, batch by batch: column lists or errors."""
     out = []
     for b in batches:
         try:
-            out.append([r for _, r in oracle_filter_project(schema, b, pred_e, proj_e, 0)])
+            out.append([r for _, r in oracle_filter_project(schema, b, pred_e, proj_e, flags)])
         except ExecutionError as e:
             out.append(e)
     return out
@@ -215,6 +215,27 @@ def test_relation_host_batches_against_oracle(m):
             assert d.values.device.type == "cpu"  # host batches in, host batches out
             assert_same(d, x, "batch %d" % i)
     assert isinstance(got[57], ExecutionError)
+
+
+@pytest.mark.parametrize("m", [1, 64])
+def test_filter_relation_host_batches_against_oracle(m):
+    """FilterRelation alone (filter.rs:46-111: every column filtered, the
+    batch's schema Schema::empty()) over host batches with read-ahead M,
+    including a Utf8 column, ragged and empty batches."""
+    from datafusion_amd.execution.filter import FilterRelation
+    from datafusion_amd.execution.relation import DataSourceRelation
+    s, bs = make_batches([1024] * 40 + [7, 0, 3000] + [1024] * 20, seed=13, utf8=True)
+    pred_e = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.4)))
+    rel = FilterRelation(DataSourceRelation(MemoryDataSource(s, bs)),
+                         compile_scalar_expr(None, pred_e, s, DFMI_FLAG_EXT_GATHER_ALL), s, coalesce=m)
+    got = _pull_all(rel)
+    ref = _oracle_stream(s, bs, pred_e, [], DFMI_FLAG_EXT_GATHER_ALL)
+    assert len(got) == len(ref) == len(bs)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert not isinstance(g, ExecutionError), (i, g)
+        assert g.num_rows() == r[0].length and g.num_columns() == len(r)
+        for d, x in zip(g.columns, r):
+            assert_same(d, x, "batch %d" % i)
 
 
 def test_relation_native_csv_views_coalesced(tmp_path):
