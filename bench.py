@@ -17,6 +17,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
 import sys
 import time
 
@@ -99,7 +100,7 @@ class FusedStep:
         return self.outs[0].length
 
 
-PROFILE_TAG = "profiles/r04"
+PROFILE_TAG = "profiles/r05"
 PROFILE_DIR = os.path.join(ROOT, PROFILE_TAG)
 
 
@@ -121,31 +122,47 @@ def profiled(kernel, run="main"):
 
 
 def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
-    """roofline object of one bench line: ALGORITHMIC bytes per
-    launch over the kernel's average launch time from HIP events on the launch
-    stream, plus -- from the committed profile of the same command -- the
-    rocprofv3 average (its frac must agree) and the PMC HBM bytes."""
+    """roofline object of one bench line. `frac` is the fraction the hardware
+    backs: the lower of the FORMULA fraction (SURVEY §8(d)'s algorithmic bytes
+    per launch over the kernel's average HIP-event time on the launch stream,
+    `formula_frac`) and the PMC fraction (the HBM bytes the committed profile
+    of the same kernel measured, `traffic_frac`, over this run's time) -- where
+    a kernel skips bytes the formula counts (masked loads, head-word compares)
+    only the moved bytes are credited. Without a PMC record, `frac` never
+    exceeds the measured copy ceiling (6.29 of 8 TB/s, MI355X_MICROARCH.md).
+    `rocprof` names the committed profile (its box, its average time and
+    fraction); the line's own box is the bench JSON's `box`."""
     ach = alg_bytes / (kms * 1e-3) / 1e9
+    ffrac = ach / HBM_PEAK_GBS
     r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": kernel, "kernel_ms": round(kms, 4),
+         "frac": None, "formula_frac": round(ffrac, 4), "kernel": kernel, "kernel_ms": round(kms, 4),
          "launches_per_step": launches, "algorithmic_bytes_per_row": round(alg_bytes * launches / rows, 3),
          "traffic": None}
     p = profiled(kernel, run)
+    frac, basis = min(ffrac, COPY_CEILING_GBS / HBM_PEAK_GBS), "formula, capped at the copy ceiling (no PMC record)"
+    if ffrac <= COPY_CEILING_GBS / HBM_PEAK_GBS:
+        basis = "formula (no PMC record)"
     if p:
         per_launch_alg = alg_bytes  # alg_bytes and kms are per launch
         avg_ms = p["avg_ns"] * 1e-6
-        r["rocprof"] = {"source": "%s/%s/traffic.json" % (PROFILE_TAG, run), "avg_ms": round(avg_ms, 4),
-                        "launches": p["launches"], "frac": round(per_launch_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        r["rocprof"] = {"source": "%s/%s/traffic.json" % (PROFILE_TAG, run), "box": p.get("box"),
+                        "avg_ms": round(avg_ms, 4), "launches": p["launches"],
+                        "formula_frac": round(per_launch_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "vgpr": p["vgpr"], "sgpr": p["sgpr"], "scratch": p["scratch"], "lds": p["lds"]}
         if "traffic_bytes" in p:
             r["traffic"] = round(p["traffic_bytes"])
             r["traffic_bytes_per_row"] = round(p["traffic_bytes"] * launches / rows, 3)
-            r["traffic_gbs"] = round(p["traffic_bytes"] / (avg_ms * 1e-3) / 1e9, 1)
-            r["traffic_frac"] = round(r["traffic_gbs"] / HBM_PEAK_GBS, 4)
-    # credit only what the hardware backs: where a kernel skips bytes the
-    # formula counts (masked loads, head-word compares), the PMC rate is the
-    # lower one; a formula rate above the measured copy ceiling is no evidence
-    r["credited_frac"] = round(min(r["frac"], r.get("traffic_frac", r["frac"])), 4)
+            # the profile's bytes per launch over THIS run's kernel time
+            tgbs = p["traffic_bytes"] / (kms * 1e-3) / 1e9
+            r["traffic_gbs"] = round(tgbs, 1)
+            r["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
+            r["rocprof"]["traffic_frac"] = round(p["traffic_bytes"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if r["traffic_frac"] < ffrac:
+                frac, basis = r["traffic_frac"], "PMC HBM bytes (the kernel moves fewer bytes than the formula counts)"
+            else:
+                frac, basis = ffrac, "formula (PMC bytes >= formula bytes)"
+    r["frac"] = round(frac, 4)
+    r["frac_basis"] = basis
     r["formula_exceeds_ceiling"] = ach > COPY_CEILING_GBS
     return r
 
@@ -583,10 +600,15 @@ def relation_host_line(sel, m=1024, nbatches=4096, passes=5, coalesce=256):
                 best = el
         return {"us_per_batch": round(best / nbatches * 1e6, 3), "rows_per_s": n / best, "selected": rows}
 
+    pc = run(True)
     out = {"workload": "ctx.sql(%r) over %d HOST batches of %d rows (MemoryDataSource), read-ahead %d"
                        % (sql, nbatches, m, coalesce),
-           "pull": run(False), "pull_and_columns": run(True),
-           "one_call_per_pull": run(False, co=1) if nbatches <= 4096 else None}
+           # the relation figure: every pulled batch's output Arrays built
+           # (what the reference's next() returns, projection.rs:59-60)
+           "rows_per_s": pc["rows_per_s"], "us_per_batch": pc["us_per_batch"],
+           "pull_and_columns": pc, "pull": run(False),
+           "one_call_per_pull": run(False, co=1) if nbatches <= 4096 else None,
+           "rust_binding_path": rust_binding_path(host, schema, sql, sel, m, nbatches, coalesce)}
     # gate: one pass, every batch against the oracle (outside the timed loops)
     pred_e, proj_e = query(sel)
     bs = batches()
@@ -598,7 +620,62 @@ def relation_host_line(sel, m=1024, nbatches=4096, passes=5, coalesce=256):
             ok = ok and d.length == r.length and np.array_equal(np.asarray(d.numpy_values()).view(np.uint8),
                                                                 np.asarray(r.numpy_values()).view(np.uint8))
     out["parity_gate"] = {"batches_checked": len(range(0, nbatches, 7)), "bit_identical_to_oracle": bool(ok)}
+    out["rust_binding_path"]["selected_matches_relation"] = out["rust_binding_path"]["selected"] == \
+        sum(b.num_rows() for b in got)
     return out
+
+
+def rust_binding_path(host, schema, sql, sel, m, nbatches, group, passes=5):
+    """What INTEGRATION.md's Rust ProjectRelation::run_group does per group of
+    `group` 1024-row host batches, on one thread without read-ahead overlap:
+    the dfmi_batch structs over the batches' (pageable) buffers, the block
+    size (dfmi_host_batches_output_bytes), a FRESH pageable block per group
+    (arrow's allocator: malloc, first-touch page faults included), and
+    dfmi_filter_project_host_batches_into -- whose selected bytes the library
+    copies from its pinned staging into the block. The output arrays are
+    slices of that block (Buffer::slice), so nothing is copied after the call.
+    Checked: the group outputs equal the relation's for the same batches."""
+    from datafusion_amd.arrow import Array, RecordBatch
+    from datafusion_amd.execution.engine import _OUT_DTYPE, host_batch_structs
+    eng = engine()
+    pred_e, proj_e = query(sel)
+    pred = compile_scalar_expr(None, pred_e, schema)
+    projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+    progs = (C.c_void_p * 3)(*[p.handle.value for p in projs])
+    L = _abi.lib()
+    err = _abi.dfmi_error()
+    failed = C.c_int32()
+    size = C.c_size_t()
+
+    def batches():
+        return [RecordBatch(schema, [Array(DataType.Float64, m, t[i * m * 8:(i + 1) * m * 8]) for t in host])
+                for i in range(nbatches)]
+    best, sel_rows = None, 0
+    for p in range(passes + 1):
+        bs = batches()
+        rows = 0
+        t0 = time.perf_counter()
+        for g in range(0, nbatches, group):
+            barr, keep = host_batch_structs(bs[g:g + group], 3)
+            nb = len(barr)
+            rc = L.dfmi_host_batches_output_bytes(pred.handle, progs, 3, C.cast(barr, C.c_void_p), nb, 0,
+                                                  C.byref(size), C.byref(err))
+            block = np.empty(size.value + 64, np.uint8)  # pageable, fresh each group
+            a = (-block.ctypes.data) % 64
+            outs = np.empty(nb * 3, _OUT_DTYPE)
+            rc = rc or L.dfmi_filter_project_host_batches_into(eng.ctx, pred.handle, progs, 3, C.cast(barr, C.c_void_p),
+                                                               nb, 0, block.ctypes.data + a, size.value,
+                                                               outs.ctypes.data, C.byref(failed), C.byref(err))
+            if rc != 0:
+                raise RuntimeError(err.message.decode())
+            rows += int(outs["length"][2::3].sum())
+        el = time.perf_counter() - t0
+        if p and (best is None or el < best):
+            best = el
+        sel_rows = rows
+    return {"us_per_batch": round(best / nbatches * 1e6, 3), "rows_per_s": nbatches * m / best, "selected": sel_rows,
+            "note": "one thread, no read-ahead overlap; pageable caller-owned block per group (one library copy of "
+                    "the selected bytes into it)"}
 
 
 def prefix_gate(eng, schema, dev_cols, m, pred_e, proj_e, flags=0):
@@ -1073,8 +1150,7 @@ def main():
             # ranks sharing a GPU: ticket-ordered tiles from the first launch
             # (DESIGN.md §4 "Look-back": blockIdx order can stall behind the
             # other rank's kernel until the 2 s timeout and its relaunch)
-            os.environ["DFMI_DIAG"] = "1"
-            os.environ["DFMI_TICKET"] = "1"
+            os.environ["DFMI_SHARED"] = "1"  # dfmi_context_create reads it (dfmi_context_set_shared)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -1175,6 +1251,7 @@ def main():
                                  "roofline": r["rl"]}
                   for s, r in results.items()},
         "parity_gate": gate,
+        "box": {"host": socket.gethostname(), "gpu": _gpu_id(dev)},
     }
     if gather is not None:
         out["gather"] = gather
@@ -1189,6 +1266,16 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def _gpu_id(dev):
+    """The GPU this run measured (name + PCI bus id): which box the line's
+    HIP-event times come from, next to the committed profile's box."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        return "%s pci %s:%s" % (p.name, getattr(p, "pci_bus_id", "?"), getattr(p, "pci_device_id", "?"))
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def _cpu_model():

@@ -128,8 +128,15 @@ class dfmi_agg_value(C.Structure):
     _fields_ = [("type", C.c_int32), ("is_null", C.c_int32), ("count", C.c_int64), ("bits", C.c_uint64)]
 
 
+# include/dfmi.h's DFMI_ABI_VERSION: lib() refuses a library built from another header
+DFMI_ABI_VERSION = 2
+
 # Every symbol include/dfmi.h declares (checked by the CPU test suite).
 EXPORTED = [
+    "dfmi_abi_version",
+    "dfmi_context_set_shared",
+    "dfmi_host_batches_output_bytes",
+    "dfmi_filter_project_host_batches_into",
     "dfmi_compile_scalar_expr",
     "dfmi_program_name",
     "dfmi_program_type",
@@ -239,6 +246,20 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libdfmi.so is not built (%s); run __graft_entry__.build()" % LIB_PATH)
     L = C.CDLL(LIB_PATH)
+    L.dfmi_abi_version.argtypes = []
+    L.dfmi_abi_version.restype = C.c_int32
+    v = L.dfmi_abi_version()
+    if v != DFMI_ABI_VERSION:
+        raise RuntimeError("libdfmi.so has ABI version %d, this binding expects %d (rebuild)" % (v, DFMI_ABI_VERSION))
+    L.dfmi_context_set_shared.argtypes = [C.c_void_p, C.c_int32]
+    L.dfmi_context_set_shared.restype = C.c_int32
+    L.dfmi_host_batches_output_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.c_void_p, C.c_int32,
+                                                 C.c_uint32, C.POINTER(C.c_size_t), C.POINTER(dfmi_error)]
+    L.dfmi_host_batches_output_bytes.restype = C.c_int32
+    L.dfmi_filter_project_host_batches_into.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                                        C.c_void_p, C.c_int32, C.c_uint32, C.c_void_p, C.c_size_t,
+                                                        C.c_void_p, C.POINTER(C.c_int32), C.POINTER(dfmi_error)]
+    L.dfmi_filter_project_host_batches_into.restype = C.c_int32
     L.dfmi_compile_scalar_expr.argtypes = [C.POINTER(dfmi_expr_node), C.c_int32, C.POINTER(dfmi_schema),
                                            C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(dfmi_error)]
     L.dfmi_compile_scalar_expr.restype = C.c_int32

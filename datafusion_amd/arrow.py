@@ -234,6 +234,44 @@ class Array:
                                 valid if not valid.all() else None, device)
 
 
+class _BlockBuffer:
+    """Non-data descriptor for one buffer of a BlockArray: the torch view of
+    the block's byte range (dict keys `o` / `n`) is made on first read and
+    stored in the instance dict, which from then on shadows this descriptor."""
+
+    __slots__ = ("name", "o", "n", "dtype")
+
+    def __init__(self, name: str, o: str, n: str, dtype=None):
+        self.name, self.o, self.n, self.dtype = name, o, n, dtype
+
+    def __get__(self, obj, cls=None):
+        if obj is None:
+            return self
+        d = obj.__dict__
+        o = d.get(self.o)
+        t = None
+        if o is not None:
+            t = d["_blk"][o:o + d[self.n]]
+            if self.dtype is not None:
+                t = t.view(self.dtype)
+        d[self.name] = t
+        return t
+
+
+class BlockArray(Array):
+    """An Array whose buffers are byte ranges of one host block -- the output
+    block of a coalesced host call (dfmi_filter_project_host_batches_into),
+    shared by every array of the group, as arrow's Buffer::slice shares one
+    Arc'd allocation. Built by the native glue (_dfmi_glue.make_block_batches)
+    with the ranges recorded (`_blk`, `_vo`/`_vn`, `_bo`/`_bn`, `_oo`/`_on`);
+    each torch view is made when first read, and the glue reads the pointers
+    of views not made yet straight from the block."""
+
+    values = _BlockBuffer("values", "_vo", "_vn")
+    validity = _BlockBuffer("validity", "_bo", "_bn")
+    offsets = _BlockBuffer("offsets", "_oo", "_on", torch.int32)
+
+
 def _offsets_tensor(offs: np.ndarray, device) -> torch.Tensor:
     n = len(offs)
     t = torch.zeros(max(16, (n + 15) // 16 * 16), dtype=torch.int32)

@@ -350,6 +350,7 @@ extern "C" int32_t dfmi_context_create(int32_t device, void* stream, dfmi_contex
         HIP_TRY(hipSetDevice(device));
         c->device = device;
         c->stream = (hipStream_t)stream;
+        if (const char* e = getenv("DFMI_SHARED")) c->shared = atoi(e) != 0;
         HIP_TRY(hipHostMalloc((void**)&c->host_hdr, kHdrAlloc, hipHostMallocDefault));
 
         HIP_TRY(hipEventCreate(&c->ev0));
@@ -394,6 +395,14 @@ extern "C" void dfmi_context_destroy(dfmi_context* c) {
 extern "C" int32_t dfmi_context_set_stream(dfmi_context* c, void* stream) {
     if (!c) return DFMI_ERR_INVALID_ARGUMENT;
     c->stream = (hipStream_t)stream;
+    return DFMI_OK;
+}
+
+extern "C" int32_t dfmi_abi_version(void) { return DFMI_ABI_VERSION; }
+
+extern "C" int32_t dfmi_context_set_shared(dfmi_context* c, int32_t shared) {
+    if (!c) return DFMI_ERR_INVALID_ARGUMENT;
+    c->shared = shared != 0;
     return DFMI_OK;
 }
 
@@ -468,6 +477,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             B.low_sel = it != ctx->sel_hint.end() && it->second < kLowSel;
         }
         build_plan(pred, projs, np, in, outs, flags, B);
+        if (ctx->shared) B.X.ticket = 1;  // shared GPU: ticket-ordered tiles from the start
         auto t_b = tnow();
         if (prof) ph[0] += tms(t_a, t_b);
         Err& se = B.se;
@@ -789,6 +799,7 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
         const dfmi_batch shape_batch{ncols, 0, maxn, shape.data()};
         Built B;
         build_plan(pred, projs, np, &shape_batch, outs, flags, B);
+        if (ctx->shared) B.X.ticket = 1;  // shared GPU: ticket-ordered tiles from the start
         jit::Plan& plan = B.plan;
         jit::Launch& X = B.X;
         bool one_by_one = B.se.set || X.gather == 3 || !(pred || B.any_kernel_out);
@@ -826,14 +837,7 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
             max_tiles = std::max(max_tiles, tiles[b]);
         }
         if (T > 0x7fffffff) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "batch too large"};
-        // one tile per batch and a caller that can take the headers in place
-        X.hdr_out = stage && stage->hdr_out && max_tiles <= 1;
-        prof.mark(0);
-        hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
-        ctx->last_kernel = X.kname;
-        prof.mark(1);
-
-        // ---- batch table
+        // ---- batch table (its layout does not depend on hdr_out)
         const int NPW = jit::batch_words(X, nout);
         const size_t table_bytes = (size_t)nb * NPW * 8, meta_bytes = table_bytes + (size_t)T * 4;
         // the table and the per-batch headers: in the caller's staging (one
@@ -842,6 +846,14 @@ int32_t dfmi::filter_project_batches_staged(dfmi_context* ctx, const dfmi_progra
         const uint8_t* host_hdr = nullptr;
         const bool staged = stage && stage->locate &&
                             stage->locate(meta_bytes, (size_t)nb * kBHdr, &host_meta, &dev_meta, &dev_hdr, &host_hdr);
+        // one tile per batch and a staged caller that takes the headers in
+        // place (decided after locate: an unstaged call reads its headers
+        // from ctx->bhdr, which a hdr_out kernel would zero before the D2H)
+        X.hdr_out = staged && stage->hdr_out && max_tiles <= 1;
+        prof.mark(0);
+        hipFunction_t fn = jit::get_kernel(ctx->device, plan, X, &ctx->last_compile_ms);
+        ctx->last_kernel = X.kname;
+        prof.mark(1);
         if (!staged) {
             ensure_host(&ctx->host_bmeta, &ctx->host_bmeta_bytes, meta_bytes);
             ensure(ctx, &ctx->bmeta, &ctx->bmeta_bytes, meta_bytes);

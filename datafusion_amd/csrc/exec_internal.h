@@ -43,6 +43,10 @@ struct dfmi_context {
     size_t utf8_src_bytes = 0;
     uint8_t* host_hdr = nullptr; // pinned copy of the header
     bool timing = true;  // record HIP events around launches (dfmi_context_set_timing)
+    // the GPU is shared with other processes (dfmi_context_set_shared, or
+    // DFMI_SHARED=1 at creation): look-back kernels take their tiles in
+    // ticket order from the first launch instead of after a 2 s timeout
+    bool shared = false;
     void* host_arena = nullptr;  // host_batch.cpp's staging arena (per context: no shared state)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double last_total_ms = 0, last_main_ms = 0, last_compile_ms = 0;

@@ -481,8 +481,22 @@ struct Arena {
         pin_cap = need;
         HIP_TRY(hipHostGetDevicePointer((void**)&pin_dev, pin, 0));
     }
+    // headers of the caller-owned form (dfmi_filter_project_host_batches_into)
+    uint8_t *hdr_pin = nullptr, *hdr_pin_dev = nullptr;
+    size_t hdr_pin_cap = 0;
+    void reserve_hdr_pin(size_t need) {
+        if (need <= hdr_pin_cap) return;
+        if (hdr_pin) (void)hipHostFree(hdr_pin);
+        hdr_pin = nullptr;
+        hdr_pin_cap = 0;
+        const size_t cap = std::max<size_t>(need, (size_t)64 << 10);
+        HIP_TRY(hipHostMalloc((void**)&hdr_pin, cap, hipHostMallocDefault));
+        hdr_pin_cap = cap;
+        HIP_TRY(hipHostGetDevicePointer((void**)&hdr_pin_dev, hdr_pin, 0));
+    }
     void release() {
         if (h2d) (void)hipStreamSynchronize(h2d);
+        if (hdr_pin) (void)hipHostFree(hdr_pin);
         if (d2h) (void)hipStreamSynchronize(d2h);
         if (dev) (void)hipFree(dev);
         if (hb) (void)hipFree(hb);
@@ -1192,8 +1206,263 @@ extern "C" void dfmi_host_result_free(dfmi_host_result* r) { delete r; }
 // batches from csv::Reader, in host memory): every batch's buffers are packed
 // into one pinned staging region (host threads), moved with ONE H2D copy,
 // run as ONE coalesced launch (dfmi_filter_project_batches), and the outputs
-// come back with ONE D2H copy into one pinned block the result owns; the
-// result holds num_batches x n columns, batch-major, as views into it.
+// come back with ONE D2H copy -- into one pinned block the result owns
+// (dfmi_filter_project_host_batches: num_batches x n columns, batch-major, as
+// views into it), or into the caller's own block
+// (dfmi_filter_project_host_batches_into).
+namespace {
+
+// Input and worst-case output layout of one host-batches call.
+struct HBLayout {
+    struct In {
+        size_t val = 0, off = 0, vld = 0, nval = 0, noff = 0, nvld = 0;
+    };
+    struct Out {
+        size_t val = 0, vld = 0, off = 0, dat = 0, ndat = 0;
+    };
+    int ncols = 0, nout = 0;
+    std::vector<int> otype;
+    std::vector<In> lay;    // [batch][column]
+    std::vector<Out> olay;  // [batch][output], offsets in the output region
+    size_t in_bytes = 0, out_bytes = 0;
+    size_t OB = 0, H = 0, IB = 0, MB = 0;  // outputs, headers, inputs, batch table (aligned)
+};
+
+void hb_layout(const dfmi_program* pred, const dfmi_program* const* projs, int32_t np, const dfmi_batch* ins,
+               int32_t nb, HBLayout& Lo) {
+    if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+    const int ncols = ins[0].num_columns;
+    const int nout = np > 0 ? np : ncols;
+    Lo.ncols = ncols;
+    Lo.nout = nout;
+    for (int32_t b = 0; b < nb; ++b) {
+        if (ins[b].num_columns != ncols || (ncols > 0 && !ins[b].columns))
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
+        for (int i = 0; i < ncols; ++i) {
+            const dfmi_column& c = ins[b].columns[i];
+            if (c.type != ins[0].columns[i].type) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
+            if (c.length != ins[b].num_rows) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
+            if (c.type == DFMI_TYPE_UTF8 && !c.offsets) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 offsets are NULL"};
+            if (!c.values && values_bytes(c)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
+        }
+    }
+    // ---- input layout: per batch and column, values / offsets / validity
+    Lo.lay.assign((size_t)nb * ncols, HBLayout::In{});
+    size_t in_bytes = 0;
+    for (int32_t b = 0; b < nb; ++b)
+        for (int i = 0; i < ncols; ++i) {
+            const dfmi_column& c = ins[b].columns[i];
+            HBLayout::In& L = Lo.lay[(size_t)b * ncols + i];
+            L.nval = values_bytes(c);
+            L.val = in_bytes;
+            in_bytes += align256(L.nval);
+            if (c.type == DFMI_TYPE_UTF8) {
+                L.noff = (size_t)(c.length + 1) * 4;
+                L.off = in_bytes;
+                in_bytes += align256(L.noff);
+            }
+            if (c.validity && c.null_count > 0) {
+                L.nvld = (size_t)((c.length + 7) / 8);
+                L.vld = in_bytes;
+                in_bytes += align256(L.nvld);
+            }
+        }
+    // ---- output layout (worst case per batch: every row selected)
+    Lo.otype.assign(nout, 0);
+    for (int o = 0; o < nout; ++o) {
+        if (np > 0 && !projs[o]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL projection"};
+        Lo.otype[o] = np > 0 ? projs[o]->type : ins[0].columns[o].type;
+    }
+    auto osrc = [&](int o) -> int {  // the input column a Utf8 output gathers
+        if (np == 0) return o;
+        const dfmi::IrNode& root = projs[o]->ir[projs[o]->root];
+        return root.kind == dfmi::IR_COL ? root.col : -1;
+    };
+    Lo.olay.assign((size_t)nb * nout, HBLayout::Out{});
+    size_t out_bytes = 0;
+    for (int32_t b = 0; b < nb; ++b)
+        for (int o = 0; o < nout; ++o) {
+            const int64_t n = ins[b].num_rows;
+            HBLayout::Out& L = Lo.olay[(size_t)b * nout + o];
+            const int t = Lo.otype[o];
+            L.val = out_bytes;
+            out_bytes += align256(t == DFMI_TYPE_BOOLEAN ? (size_t)bitmap_bytes(n)
+                                                         : (t == DFMI_TYPE_UTF8 ? 0 : (size_t)n * width_of(t)));
+            L.vld = out_bytes;
+            out_bytes += align256(bitmap_bytes(n));
+            if (t == DFMI_TYPE_UTF8) {
+                L.off = out_bytes;
+                out_bytes += align256((size_t)(n + 1) * 4);
+                const int c = osrc(o);
+                L.ndat = c >= 0 ? values_bytes(ins[b].columns[c]) : 0;
+                L.dat = out_bytes;
+                out_bytes += align256(std::max<size_t>(L.ndat, 1));
+            }
+        }
+    Lo.in_bytes = in_bytes;
+    Lo.out_bytes = out_bytes;
+    Lo.OB = align256(std::max<size_t>(out_bytes, 256));
+    Lo.H = align256((size_t)nb * 256);
+    Lo.IB = align256(std::max<size_t>(in_bytes, 256));
+    size_t MB = 256;  // bound on the launch's batch table + tile map (exec.cpp)
+    for (int32_t b = 0; b < nb; ++b)
+        MB += (size_t)(4 + 3 * ncols + 5 * nout) * 8 + (size_t)((ins[b].num_rows + 63) / 64 + 1) * 4;
+    Lo.MB = align256(MB);
+}
+
+// Where a host-batches call's headers and outputs land (pinned host memory,
+// with the device-visible addresses the kernel writes through when the call
+// is zero-copy). `contiguous`: outputs right after the headers (one D2H).
+struct HBTarget {
+    uint8_t *hdr_host = nullptr, *hdr_dev = nullptr;
+    uint8_t *out_host = nullptr, *out_dev = nullptr;
+    bool contiguous = false;
+};
+
+uint8_t* device_address(uint8_t* host) {
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, host, 0));
+    return (uint8_t*)d;
+}
+
+// The common body: layout, packing, the staged coalesced launch. `target`
+// is asked once (H, OB, zero-copy) for the output placement. Returns the
+// launch's status; *nok = batches completed.
+int32_t host_batches_run(dfmi_context* ctx, const dfmi_program* pred, const dfmi_program* const* projs, int32_t np,
+                         const dfmi_batch* ins, int32_t nb, uint32_t flags, const HBLayout& Lo,
+                         const std::function<HBTarget(size_t H, size_t OB, bool zc)>& target,
+                         std::vector<dfmi_out_column>& douts, int32_t* failed, dfmi_error* err, dfmi::CallProf& prof) {
+    HIP_TRY(hipSetDevice(dfmi::ctx_device(ctx)));
+    hipStream_t st = dfmi::ctx_stream(ctx);
+    Arena& A = arena_of(ctx);
+    A.init(dfmi::ctx_device(ctx));
+    const int ncols = Lo.ncols, nout = Lo.nout;
+    const size_t OB = Lo.OB, H = Lo.H, IB = Lo.IB, MB = Lo.MB;
+    // ---- regions. Device (Arena::hb): this call's half [headers |
+    // outputs], the other half's headers zeroed by this call's kernel, and
+    // [inputs | batch table]; pinned staging: [inputs | table] (ONE H2D, or
+    // none: small calls read it in place); the target: headers + outputs
+    // (ONE D2H, or none: a small call's kernel writes them in place).
+    A.reserve_pin(IB + MB);
+    A.reserve_hb(H, OB, IB + MB, st);
+    uint8_t* const pin_in = A.pin;
+    prof.mark(0);
+    {
+        std::vector<std::function<void()>> tasks;
+        const int ways = std::max(1, std::min(A.pool->ways(), (int)(Lo.in_bytes >> 20) + 1));
+        for (int w = 0; w < ways; ++w)
+            tasks.push_back([&, w] {
+                for (int32_t b = w; b < nb; b += ways)
+                    for (int i = 0; i < ncols; ++i) {
+                        const dfmi_column& c = ins[b].columns[i];
+                        const HBLayout::In& L = Lo.lay[(size_t)b * ncols + i];
+                        if (L.nval) memcpy(pin_in + L.val, c.values, L.nval);
+                        if (L.noff) memcpy(pin_in + L.off, c.offsets, L.noff);
+                        if (L.nvld) memcpy(pin_in + L.vld, c.validity, L.nvld);
+                    }
+            });
+        A.pool->run(tasks);
+    }
+    // zero-copy inputs (small calls): the kernel reads the inputs and the
+    // batch table straight from the pinned staging region over PCIe -- no
+    // copy in at all on the call's critical path
+    static const int zc_env = [] {
+        const char* e = getenv("DFMI_HOST_ZC");
+        return e ? atoi(e) : -1;
+    }();
+    const bool zc = zc_env > 0 || (zc_env < 0 && Lo.in_bytes + MB <= kZeroCopyBytes);
+    prof.mark(1);
+    const int half = A.hb_half, other = 1 - half;
+    const HBTarget T = target(H, OB, zc);
+    uint8_t* const dhdr = A.hb_half_base(half) + A.hb_hcap - H;  // the kernel's header atomics
+    uint8_t* const dout = zc ? T.out_dev : A.hb_half_base(half) + A.hb_hcap;
+    uint8_t* const dev = zc ? A.pin_dev : A.hb + 2 * (A.hb_hcap + A.hb_ocap);  // inputs
+    std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
+    std::vector<dfmi_batch> dins(nb);
+    for (int32_t b = 0; b < nb; ++b) {
+        for (int i = 0; i < ncols; ++i) {
+            const dfmi_column& c = ins[b].columns[i];
+            const HBLayout::In& L = Lo.lay[(size_t)b * ncols + i];
+            dfmi_column& d = dcols[(size_t)b * ncols + i];
+            d = c;
+            d.values = dev + L.val;
+            d.offsets = c.type == DFMI_TYPE_UTF8 ? (const int32_t*)(dev + L.off) : nullptr;
+            d.validity = L.nvld ? dev + L.vld : nullptr;
+            if (!L.nvld) d.null_count = 0;
+        }
+        dins[b] = dfmi_batch{ncols, 0, ins[b].num_rows, dcols.data() + (size_t)b * ncols};
+    }
+    douts.assign((size_t)nb * nout, dfmi_out_column{});
+    for (size_t k = 0; k < douts.size(); ++k) {
+        const HBLayout::Out& L = Lo.olay[k];
+        dfmi_out_column& d = douts[k];
+        memset(&d, 0, sizeof d);
+        d.values = dout + L.val;
+        d.validity = dout + L.vld;
+        if (Lo.otype[k % nout] == DFMI_TYPE_UTF8) {
+            d.offsets = (int32_t*)(dout + L.off);
+            d.data = dout + L.dat;
+            d.data_capacity = (int64_t)L.ndat;
+        }
+    }
+    // ---- (one H2D), the coalesced launch, (one D2H), one synchronisation
+    size_t meta_used = 0;
+    hipError_t copy_err = hipSuccess;
+    bool cleared = false, hdr_written = false;
+    dfmi::BatchStage stage;
+    stage.locate = [&](size_t meta_bytes, size_t hdr_bytes, uint8_t** host_meta, uint8_t** dev_meta,
+                       uint8_t** dev_hdr, const uint8_t** host_hdr) {
+        if (meta_bytes > MB || hdr_bytes > H) return false;
+        meta_used = meta_bytes;
+        *host_meta = pin_in + IB;
+        *dev_meta = dev + IB;
+        *dev_hdr = dhdr;
+        *host_hdr = T.hdr_host;
+        return true;
+    };
+    stage.copy_in = [&](hipStream_t s) {
+        hipError_t e = hipSuccess;
+        if (A.hb_dirty[half])  // headers the other half's last kernel did not zero (an earlier failed call)
+            e = hipMemsetAsync(A.hb_half_base(half) + A.hb_hcap - A.hb_dirty[half], 0, A.hb_dirty[half], s);
+        if (e == hipSuccess && !zc)
+            e = hipMemcpyAsync(dev, pin_in, meta_used ? IB + meta_used : Lo.in_bytes, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) copy_err = e;
+        else A.hb_dirty[half] = 0;
+    };
+    stage.copy_out = [&](hipStream_t s) {
+        if (zc && hdr_written) return;  // outputs and headers are in place
+        hipError_t e;
+        if (T.contiguous && !zc) {  // [headers | outputs] in one copy
+            e = hipMemcpyAsync(T.hdr_host, dhdr, H + OB, hipMemcpyDeviceToHost, s);
+        } else {
+            e = hipMemcpyAsync(T.hdr_host, dhdr, H, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess && !zc) e = hipMemcpyAsync(T.out_host, dout, OB, hipMemcpyDeviceToHost, s);
+        }
+        if (e != hipSuccess) copy_err = e;
+    };
+    if (zc) {
+        stage.hdr_out = (uint64_t*)T.hdr_dev;
+        stage.hdr_written = &hdr_written;
+    }
+    stage.clear_bhdr = (uint64_t*)(A.hb_half_base(other) + A.hb_hcap - A.hb_dirty[other]);
+    stage.clear_bhdr_words = (int64_t)(A.hb_dirty[other] / 8);
+    stage.cleared = &cleared;
+    prof.mark(2);
+    const int32_t rc = dfmi::filter_project_batches_staged(ctx, pred, projs, np, dins.data(), nb, douts.data(), flags,
+                                                           failed, err, &stage);
+    if (rc != DFMI_OK) (void)hipStreamSynchronize(st);  // (a call that failed after copy_in: drain it)
+    prof.mark(3);
+    if (cleared) {  // this kernel zeroed the other half's headers; this half's are dirty now
+        A.hb_dirty[other] = 0;
+        A.hb_dirty[half] = std::max(A.hb_dirty[half], H);
+        A.hb_half = other;
+    }
+    HIP_TRY(copy_err);
+    return rc;
+}
+
+}  // namespace
+
 extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfmi_program* pred,
                                                     const dfmi_program* const* projs, int32_t np,
                                                     const dfmi_batch* ins, int32_t nb, uint32_t flags,
@@ -1214,8 +1483,6 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
         dfmi::Unsliced us_;  // sliced arrays (slice.cpp)
         if (nb > 0 && dfmi::any_offset(ins, nb)) ins = dfmi::unslice(ins, nb, us_, false, nullptr);
-        HIP_TRY(hipSetDevice(dfmi::ctx_device(ctx)));
-        hipStream_t st = dfmi::ctx_stream(ctx);
         Arena& A = arena_of(ctx);
         A.init(dfmi::ctx_device(ctx));
         R = new dfmi_host_result();
@@ -1224,217 +1491,40 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
             *out = R;
             return DFMI_OK;
         }
-        const int ncols = ins[0].num_columns;
-        const int nout = np > 0 ? np : ncols;
-        for (int32_t b = 0; b < nb; ++b) {
-            if (ins[b].num_columns != ncols || (ncols > 0 && !ins[b].columns))
-                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
-            for (int i = 0; i < ncols; ++i) {
-                const dfmi_column& c = ins[b].columns[i];
-                if (c.type != ins[0].columns[i].type) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "batches do not share a schema"};
-                if (c.length != ins[b].num_rows) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "ragged batch"};
-                if (c.type == DFMI_TYPE_UTF8 && !c.offsets) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "Utf8 offsets are NULL"};
-                if (!c.values && values_bytes(c)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "column values pointer is NULL"};
-            }
-        }
-        // ---- input layout: per batch and column, values / offsets / validity
-        struct In {
-            size_t val = 0, off = 0, vld = 0, nval = 0, noff = 0, nvld = 0;
-        };
-        std::vector<In> lay((size_t)nb * ncols);
-        size_t in_bytes = 0;
-        for (int32_t b = 0; b < nb; ++b)
-            for (int i = 0; i < ncols; ++i) {
-                const dfmi_column& c = ins[b].columns[i];
-                In& L = lay[(size_t)b * ncols + i];
-                L.nval = values_bytes(c);
-                L.val = in_bytes;
-                in_bytes += align256(L.nval);
-                if (c.type == DFMI_TYPE_UTF8) {
-                    L.noff = (size_t)(c.length + 1) * 4;
-                    L.off = in_bytes;
-                    in_bytes += align256(L.noff);
-                }
-                if (c.validity && c.null_count > 0) {
-                    L.nvld = (size_t)((c.length + 7) / 8);
-                    L.vld = in_bytes;
-                    in_bytes += align256(L.nvld);
-                }
-            }
-        // ---- output layout (worst case per batch: every row selected)
-        std::vector<int> otype(nout);
-        for (int o = 0; o < nout; ++o) {
-            if (np > 0 && !projs[o]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL projection"};
-            otype[o] = np > 0 ? projs[o]->type : ins[0].columns[o].type;
-        }
-        auto osrc = [&](int o) -> int {  // the input column a Utf8 output gathers
-            if (np == 0) return o;
-            const dfmi::IrNode& root = projs[o]->ir[projs[o]->root];
-            return root.kind == dfmi::IR_COL ? root.col : -1;
-        };
-        struct Out {
-            size_t val = 0, vld = 0, off = 0, dat = 0, ndat = 0;
-        };
-        std::vector<Out> olay((size_t)nb * nout);
-        size_t out_bytes = 0;
-        for (int32_t b = 0; b < nb; ++b)
-            for (int o = 0; o < nout; ++o) {
-                const int64_t n = ins[b].num_rows;
-                Out& L = olay[(size_t)b * nout + o];
-                const int t = otype[o];
-                L.val = out_bytes;
-                out_bytes += align256(t == DFMI_TYPE_BOOLEAN ? (size_t)bitmap_bytes(n)
-                                                             : (t == DFMI_TYPE_UTF8 ? 0 : (size_t)n * width_of(t)));
-                L.vld = out_bytes;
-                out_bytes += align256(bitmap_bytes(n));
-                if (t == DFMI_TYPE_UTF8) {
-                    L.off = out_bytes;
-                    out_bytes += align256((size_t)(n + 1) * 4);
-                    const int c = osrc(o);
-                    L.ndat = c >= 0 ? values_bytes(ins[b].columns[c]) : 0;
-                    L.dat = out_bytes;
-                    out_bytes += align256(std::max<size_t>(L.ndat, 1));
-                }
-            }
-        // ---- regions. Device (Arena::hb): this call's half [headers |
-        // outputs], the other half's headers zeroed by this call's kernel,
-        // and [inputs | batch table]; pinned staging: [inputs | table] (ONE
-        // H2D, or none: small calls read it in place); the result's block:
-        // [headers | outputs] (ONE D2H).
-        const size_t OB = align256(std::max<size_t>(out_bytes, 256)), H = align256((size_t)nb * 256),
-                     IB = align256(std::max<size_t>(in_bytes, 256));
-        size_t MB = 256;  // bound on the launch's batch table + tile map (exec.cpp)
-        for (int32_t b = 0; b < nb; ++b)
-            MB += (size_t)(4 + 3 * ncols + 5 * nout) * 8 + (size_t)((ins[b].num_rows + 63) / 64 + 1) * 4;
-        MB = align256(MB);
-        A.reserve_pin(IB + MB);
-        A.reserve_hb(H, OB, IB + MB, st);
-        uint8_t* const pin_in = A.pin;
-        prof.mark(0);
-        {
-            std::vector<std::function<void()>> tasks;
-            const int ways = std::max(1, std::min(A.pool->ways(), (int)(in_bytes >> 20) + 1));
-            for (int w = 0; w < ways; ++w)
-                tasks.push_back([&, w] {
-                    for (int32_t b = w; b < nb; b += ways)
-                        for (int i = 0; i < ncols; ++i) {
-                            const dfmi_column& c = ins[b].columns[i];
-                            const In& L = lay[(size_t)b * ncols + i];
-                            if (L.nval) memcpy(pin_in + L.val, c.values, L.nval);
-                            if (L.noff) memcpy(pin_in + L.off, c.offsets, L.noff);
-                            if (L.nvld) memcpy(pin_in + L.vld, c.validity, L.nvld);
-                        }
-                });
-            A.pool->run(tasks);
-        }
-        // zero-copy inputs (small calls): the kernel reads the inputs and the
-        // batch table straight from the pinned staging region over PCIe -- no
-        // copy in at all on the call's critical path
-        static const int zc_env = [] {
-            const char* e = getenv("DFMI_HOST_ZC");
-            return e ? atoi(e) : -1;
-        }();
-        const bool zc = zc_env > 0 || (zc_env < 0 && in_bytes + MB <= kZeroCopyBytes);
-        prof.mark(1);
-        const int half = A.hb_half, other = 1 - half;
+        HBLayout Lo;
+        hb_layout(pred, projs, np, ins, nb, Lo);
+        const int ncols = Lo.ncols, nout = Lo.nout;
+        std::vector<dfmi_out_column> douts;
+        dfmi_error e2{};
         // the result's pinned block [headers | outputs]; a small call's kernel
         // writes its outputs there directly (and, one tile per batch, the
         // finished headers too: Launch::hdr_out) -- no copy back at all
-        R->arena = R->pool->get(H + OB);
-        uint8_t* res_dev = nullptr;
-        if (zc) HIP_TRY(hipHostGetDevicePointer((void**)&res_dev, R->arena.p, 0));
-        uint8_t* const dhdr = A.hb_half_base(half) + A.hb_hcap - H;  // the kernel's header atomics
-        uint8_t* const dout = zc ? res_dev + H : A.hb_half_base(half) + A.hb_hcap;
-        uint8_t* const dev = zc ? A.pin_dev : A.hb + 2 * (A.hb_hcap + A.hb_ocap);  // inputs
-        std::vector<dfmi_column> dcols((size_t)nb * std::max(1, ncols));
-        std::vector<dfmi_batch> dins(nb);
-        for (int32_t b = 0; b < nb; ++b) {
-            for (int i = 0; i < ncols; ++i) {
-                const dfmi_column& c = ins[b].columns[i];
-                const In& L = lay[(size_t)b * ncols + i];
-                dfmi_column& d = dcols[(size_t)b * ncols + i];
-                d = c;
-                d.values = dev + L.val;
-                d.offsets = c.type == DFMI_TYPE_UTF8 ? (const int32_t*)(dev + L.off) : nullptr;
-                d.validity = L.nvld ? dev + L.vld : nullptr;
-                if (!L.nvld) d.null_count = 0;
+        auto target = [&](size_t H, size_t OB, bool zc) {
+            R->arena = R->pool->get(H + OB);
+            HBTarget T;
+            T.hdr_host = R->arena.p;
+            T.out_host = R->arena.p + H;
+            T.contiguous = true;
+            if (zc) {
+                T.hdr_dev = device_address(R->arena.p);
+                T.out_dev = T.hdr_dev + H;
             }
-            dins[b] = dfmi_batch{ncols, 0, ins[b].num_rows, dcols.data() + (size_t)b * ncols};
-        }
-        std::vector<dfmi_out_column> douts((size_t)nb * nout);
-        for (size_t k = 0; k < douts.size(); ++k) {
-            const Out& L = olay[k];
-            dfmi_out_column& d = douts[k];
-            memset(&d, 0, sizeof d);
-            d.values = dout + L.val;
-            d.validity = dout + L.vld;
-            if (otype[k % nout] == DFMI_TYPE_UTF8) {
-                d.offsets = (int32_t*)(dout + L.off);
-                d.data = dout + L.dat;
-                d.data_capacity = (int64_t)L.ndat;
-            }
-        }
-        // ---- (one H2D), the coalesced launch, (one D2H), one synchronisation
-        size_t meta_used = 0;
-        hipError_t copy_err = hipSuccess;
-        bool cleared = false, hdr_written = false;
-        dfmi::BatchStage stage;
-        stage.locate = [&](size_t meta_bytes, size_t hdr_bytes, uint8_t** host_meta, uint8_t** dev_meta,
-                           uint8_t** dev_hdr, const uint8_t** host_hdr) {
-            if (meta_bytes > MB || hdr_bytes > H) return false;
-            meta_used = meta_bytes;
-            *host_meta = pin_in + IB;
-            *dev_meta = dev + IB;
-            *dev_hdr = dhdr;
-            *host_hdr = R->arena.p;
-            return true;
+            return T;
         };
-        stage.copy_in = [&](hipStream_t s) {
-            hipError_t e = hipSuccess;
-            if (A.hb_dirty[half])  // headers the other half's last kernel did not zero (an earlier failed call)
-                e = hipMemsetAsync(A.hb_half_base(half) + A.hb_hcap - A.hb_dirty[half], 0, A.hb_dirty[half], s);
-            if (e == hipSuccess && !zc)
-                e = hipMemcpyAsync(dev, pin_in, meta_used ? IB + meta_used : in_bytes, hipMemcpyHostToDevice, s);
-            if (e != hipSuccess) copy_err = e;
-            else A.hb_dirty[half] = 0;
-        };
-        stage.copy_out = [&](hipStream_t s) {
-            if (zc && hdr_written) return;  // outputs and headers are in place
-            const hipError_t e = hipMemcpyAsync(R->arena.p, dhdr, zc ? H : H + OB, hipMemcpyDeviceToHost, s);
-            if (e != hipSuccess) copy_err = e;
-        };
-        if (zc) {
-            stage.hdr_out = (uint64_t*)res_dev;
-            stage.hdr_written = &hdr_written;
-        }
-        stage.clear_bhdr = (uint64_t*)(A.hb_half_base(other) + A.hb_hcap - A.hb_dirty[other]);
-        stage.clear_bhdr_words = (int64_t)(A.hb_dirty[other] / 8);
-        stage.cleared = &cleared;
-        dfmi_error e2{};
-        prof.mark(2);
-        const int32_t rc = dfmi::filter_project_batches_staged(ctx, pred, projs, np, dins.data(), nb, douts.data(),
-                                                               flags, failed, &e2, &stage);
-        if (rc != DFMI_OK) (void)hipStreamSynchronize(st);  // (a call that failed after copy_in: drain it)
-        prof.mark(3);
-        if (cleared) {  // this kernel zeroed the other half's headers; this half's are dirty now
-            A.hb_dirty[other] = 0;
-            A.hb_dirty[half] = std::max(A.hb_dirty[half], H);
-            A.hb_half = other;
-        }
-        HIP_TRY(copy_err);
+        const int32_t rc = host_batches_run(ctx, pred, projs, np, ins, nb, flags, Lo, target, douts, failed, &e2, prof);
         const int32_t nok = rc == DFMI_OK ? nb : std::max(0, *failed);
         R->cols.resize((size_t)nb * nout);
         for (int32_t b = 0; b < nb; ++b)
             for (int o = 0; o < nout; ++o) {
                 const size_t k = (size_t)b * nout + o;
                 dfmi_host_result::Col& c = R->cols[k];
-                c.type = otype[o];
+                c.type = Lo.otype[o];
                 if (b >= nok) continue;  // a failed call: batches from the failing one are empty
                 const dfmi_out_column& d = douts[k];
-                const Out& L = olay[k];
+                const HBLayout::Out& L = Lo.olay[k];
                 if (d.passthrough_column >= 0) {  // Arc clone: the caller's own column, copied
                     const dfmi_column& src = ins[b].columns[d.passthrough_column];
-                    const In& I = lay[(size_t)b * ncols + d.passthrough_column];
+                    const HBLayout::In& I = Lo.lay[(size_t)b * ncols + d.passthrough_column];
                     c.length = src.length;
                     c.null_count = I.nvld ? src.null_count : 0;
                     c.values = R->pool->get(std::max<size_t>(I.nval, 1));
@@ -1456,9 +1546,9 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
                 c.length = d.length;
                 c.null_count = d.null_count;
                 c.data_length = d.data_length;
-                uint8_t* const ob = R->arena.p + H;  // the outputs, after the headers
-                c.v_values = ob + (otype[o] == DFMI_TYPE_UTF8 ? L.dat : L.val);
-                c.v_offsets = otype[o] == DFMI_TYPE_UTF8 ? (const int32_t*)(ob + L.off) : nullptr;
+                uint8_t* const ob = R->arena.p + Lo.H;  // the outputs, after the headers
+                c.v_values = ob + (Lo.otype[o] == DFMI_TYPE_UTF8 ? L.dat : L.val);
+                c.v_offsets = Lo.otype[o] == DFMI_TYPE_UTF8 ? (const int32_t*)(ob + L.off) : nullptr;
                 c.v_validity = ob + L.vld;
             }
         *out = R;
@@ -1472,6 +1562,164 @@ extern "C" int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfm
         return DFMI_OK;
     } catch (const Fail& f) {
         delete R;
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_host_batches_output_bytes(const dfmi_program* pred, const dfmi_program* const* projs,
+                                                  int32_t np, const dfmi_batch* ins, int32_t nb, uint32_t flags,
+                                                  size_t* bytes, dfmi_error* err) {
+    (void)flags;
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!bytes || nb < 0 || (nb > 0 && !ins) || (np > 0 && !projs))
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        *bytes = 0;
+        if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        if (nb == 0) return DFMI_OK;
+        dfmi::Unsliced us_;
+        if (dfmi::any_offset(ins, nb)) ins = dfmi::unslice(ins, nb, us_, false, nullptr);
+        HBLayout Lo;
+        hb_layout(pred, projs, np, ins, nb, Lo);
+        *bytes = Lo.OB;
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_filter_project_host_batches_into(dfmi_context* ctx, const dfmi_program* pred,
+                                                         const dfmi_program* const* projs, int32_t np,
+                                                         const dfmi_batch* ins, int32_t nb, uint32_t flags,
+                                                         void* out_block, size_t out_capacity,
+                                                         dfmi_out_column* outputs, int32_t* failed, dfmi_error* err) {
+    static thread_local dfmi::CallProf prof("host_batches_into");
+    prof.start();
+    set_err(err, DFMI_OK, "");
+    int32_t dummy_failed;
+    if (!failed) failed = &dummy_failed;
+    *failed = -1;
+    Arena* Ap = nullptr;
+    dfmi_host::PinnedPool::Blk stage_blk;
+    try {
+        if (!ctx || nb < 0 || (nb > 0 && (!ins || !outputs || !out_block)) || (np > 0 && !projs))
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        dfmi::ctx_last_err_key(ctx) = ~0ull;
+        if (!pred && np == 0) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "neither a predicate nor projections"};
+        if (nb == 0) return DFMI_OK;
+        if ((uintptr_t)out_block & 63) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "out_block must be 64-byte aligned"};
+        dfmi::Unsliced us_;
+        const dfmi_batch* const caller_ins = ins;
+        if (dfmi::any_offset(ins, nb)) ins = dfmi::unslice(ins, nb, us_, false, nullptr);
+        HBLayout Lo;
+        hb_layout(pred, projs, np, ins, nb, Lo);
+        const int nout = Lo.nout;
+        if (out_capacity < Lo.OB)
+            throw Fail{DFMI_ERR_CAPACITY, "out_block holds " + std::to_string(out_capacity) + " bytes, the outputs need " +
+                                              std::to_string(Lo.OB) + " (dfmi_host_batches_output_bytes)"};
+        Arena& A = arena_of(ctx);
+        A.init(dfmi::ctx_device(ctx));
+        Ap = &A;
+        uint8_t* const blk = (uint8_t*)out_block;
+        // a pinned caller block is the kernel's (or the D2H's) target itself
+        uint8_t* blk_dev = nullptr;
+        if (is_pinned(blk, 1) && is_pinned(blk, Lo.OB)) {
+            blk_dev = device_address(blk);
+        } else {
+            hipPointerAttribute_t pa;
+            if (hipPointerGetAttributes(&pa, blk) == hipSuccess && pa.type == hipMemoryTypeHost &&
+                hipPointerGetAttributes(&pa, blk + Lo.OB - 1) == hipSuccess && pa.type == hipMemoryTypeHost)
+                blk_dev = device_address(blk);
+            else
+                (void)hipGetLastError();
+        }
+        std::vector<dfmi_out_column> douts;
+        dfmi_error e2{};
+        auto target = [&](size_t H, size_t OB, bool zc) {
+            HBTarget T;
+            A.reserve_hdr_pin(H);
+            T.hdr_host = A.hdr_pin;
+            T.hdr_dev = A.hdr_pin_dev;
+            if (blk_dev) {
+                T.out_host = blk;
+                T.out_dev = blk_dev;
+            } else {  // pageable: the library's pinned staging, copied below
+                stage_blk = A.results->get(OB);
+                T.out_host = stage_blk.p;
+                if (zc) T.out_dev = device_address(stage_blk.p);
+            }
+            (void)H;
+            return T;
+        };
+        const int32_t rc = host_batches_run(ctx, pred, projs, np, ins, nb, flags, Lo, target, douts, failed, &e2, prof);
+        const int32_t nok = rc == DFMI_OK ? nb : std::max(0, *failed);
+        // ---- the outputs as views into the caller's block; a pageable block
+        // gets the selected bytes (only those) from the staging block
+        std::vector<std::function<void()>> tasks;
+        const uint8_t* const src = stage_blk.p;
+        for (int32_t b = 0; b < nb; ++b)
+            for (int o = 0; o < nout; ++o) {
+                const size_t k = (size_t)b * nout + o;
+                const HBLayout::Out& L = Lo.olay[k];
+                dfmi_out_column& u = outputs[k];
+                const dfmi_out_column d = douts[k];
+                memset(&u, 0, sizeof u);
+                u.type = Lo.otype[o];
+                u.passthrough_column = -1;
+                if (b >= nok) continue;  // a failed call: batches from the failing one are empty
+                if (d.passthrough_column >= 0) {  // the caller's own input column (expression.rs:272-276)
+                    const dfmi_column& c = caller_ins[b].columns[d.passthrough_column];
+                    u.passthrough_column = d.passthrough_column;
+                    u.length = c.length;
+                    u.null_count = c.validity ? c.null_count : 0;
+                    continue;
+                }
+                u.length = d.length;
+                u.null_count = d.null_count;
+                u.data_length = d.data_length;
+                u.validity = blk + L.vld;
+                const int t = Lo.otype[o];
+                size_t nv = 0;
+                if (t == DFMI_TYPE_UTF8) {
+                    u.offsets = (int32_t*)(blk + L.off);
+                    u.data = blk + L.dat;
+                    u.data_capacity = (int64_t)L.ndat;
+                } else {
+                    u.values = blk + L.val;
+                    nv = t == DFMI_TYPE_BOOLEAN ? (size_t)(d.length + 7) / 8 : (size_t)d.length * width_of(t);
+                }
+                if (!src) continue;
+                const size_t nb_ = (size_t)(d.length + 7) / 8;
+                tasks.emplace_back([=] {
+                    if (nv) memcpy(blk + L.val, src + L.val, nv);
+                    if (d.null_count > 0) memcpy(blk + L.vld, src + L.vld, nb_);
+                    if (t == DFMI_TYPE_UTF8) {
+                        memcpy(blk + L.off, src + L.off, (size_t)(d.length + 1) * 4);
+                        if (d.data_length) memcpy(blk + L.dat, src + L.dat, (size_t)d.data_length);
+                    }
+                });
+            }
+        if (!tasks.empty()) {  // batch-sized pieces, spread over the host threads
+            const int ways = A.pool->ways();
+            std::vector<std::function<void()>> parts((size_t)std::min<size_t>(ways, tasks.size()));
+            for (size_t w = 0; w < parts.size(); ++w)
+                parts[w] = [&, w] {
+                    for (size_t i = w; i < tasks.size(); i += parts.size()) tasks[i]();
+                };
+            A.pool->run(parts);
+        }
+        if (stage_blk.p) A.results->put(stage_blk);
+        if (rc != DFMI_OK) {
+            if (err) *err = e2;
+            return rc;
+        }
+        prof.mark(4);
+        prof.done();
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        if (Ap && stage_blk.p) Ap->results->put(stage_blk);
         set_err(err, f.code, f.msg);
         return f.code;
     }

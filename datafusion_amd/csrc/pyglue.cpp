@@ -33,8 +33,15 @@ typedef struct {
     uint64_t columns;
 } batch_rec; /* dfmi_batch */
 
+typedef struct {
+    uint64_t values, validity, offsets, data;
+    int64_t data_capacity;
+    int32_t type, passthrough_column;
+    int64_t length, null_count, data_length;
+} out_rec; /* dfmi_out_column */
+
 static PyObject *s_columns, *s__columns, *s_data_type, *s_length, *s_null_count, *s_validity, *s_values,
-    *s_offsets, *s_offset;
+    *s_offsets, *s_offset, *s_schema, *s__blk, *s__vo, *s__vn, *s__bo, *s__bn, *s__oo, *s__on;
 
 /* Integer attribute `name` of `o`: from the instance dict when it is there
  * (a borrowed lookup), else by attribute lookup. */
@@ -54,10 +61,27 @@ static int get_i64(PyObject* o, PyObject* name, int64_t* out) {
 }
 
 /* Data pointer of tensor attribute `name` of array `a` (0 for None); fails
- * unless the tensor is in host memory. */
-static int get_ptr(PyObject* a, PyObject* name, uint64_t* out) {
+ * unless the tensor is in host memory. A BlockArray (arrow.py) whose buffer
+ * view was not made yet is read from its block and byte offset (`lazy_off`,
+ * e.g. "_vo") without making the view. */
+static int get_ptr(PyObject* a, PyObject* name, uint64_t* out, PyObject* lazy_off) {
     PyObject** dp = _PyObject_GetDictPtr(a);
     PyObject* t = dp && *dp ? PyDict_GetItemWithError(*dp, name) : NULL;
+    if (!t && !PyErr_Occurred() && dp && *dp) {
+        PyObject* blk = PyDict_GetItemWithError(*dp, s__blk);
+        PyObject* off = blk ? PyDict_GetItemWithError(*dp, lazy_off) : NULL;
+        if (off && THPVariable_Check(blk)) {
+            const at::Tensor& x = THPVariable_Unpack(blk);
+            if (!x.is_cpu()) {
+                PyErr_SetString(PyExc_ValueError, "filter_project_host_batches takes host batches");
+                return -1;
+            }
+            const long long o = PyLong_AsLongLong(off);
+            if (o == -1 && PyErr_Occurred()) return -1;
+            *out = (uint64_t)(uintptr_t)x.data_ptr() + (uint64_t)o;
+            return 0;
+        }
+    }
     if (t) {
         Py_INCREF(t);
     } else {
@@ -120,8 +144,8 @@ static int pack(PyObject* seq, Py_ssize_t ncols, const Py_buffer& cb, const Py_b
             int64_t t;
             memset(&r[i], 0, sizeof r[i]);
             if (get_i64(a, s_data_type, &t) || get_i64(a, s_length, &r[i].length) ||
-                get_i64(a, s_null_count, &r[i].null_count) || get_ptr(a, s_validity, &r[i].validity) ||
-                get_ptr(a, s_values, &r[i].values) || get_ptr(a, s_offsets, &r[i].offsets) ||
+                get_i64(a, s_null_count, &r[i].null_count) || get_ptr(a, s_validity, &r[i].validity, s__bo) ||
+                get_ptr(a, s_values, &r[i].values, s__vo) || get_ptr(a, s_offsets, &r[i].offsets, s__oo) ||
                 get_i64(a, s_offset, &r[i].offset)) {
                 Py_DECREF(cseq);
                 return -1;
@@ -155,7 +179,178 @@ static PyObject* pack_host_batches(PyObject* self, PyObject* args) {
     Py_RETURN_NONE;
 }
 
+static int width_of(int t) {
+    switch (t) {
+        case 2: case 6: return 1;            /* Int8, UInt8 */
+        case 3: case 7: return 2;            /* Int16, UInt16 */
+        case 4: case 8: case 10: return 4;   /* Int32, UInt32, Float32 */
+        case 5: case 9: case 11: return 8;   /* Int64, UInt64, Float64 */
+        default: return 0;
+    }
+}
+
+static inline int set_ll(PyObject* d, PyObject* k, long long v) {
+    PyObject* x = PyLong_FromLongLong(v);
+    if (!x) return -1;
+    const int rc = PyDict_SetItem(d, k, x);
+    Py_DECREF(x);
+    return rc;
+}
+
+/* A new instance of heap type `cls` with a fresh instance dict (no __init__). */
+static PyObject* bare_instance(PyTypeObject* cls, PyObject** dict) {
+    PyObject* o = cls->tp_alloc(cls, 0);
+    if (!o) return NULL;
+    PyObject** dp = _PyObject_GetDictPtr(o);
+    if (!dp) {
+        Py_DECREF(o);
+        PyErr_SetString(PyExc_TypeError, "class without an instance dict");
+        return NULL;
+    }
+    *dp = PyDict_New();
+    if (!*dp) {
+        Py_DECREF(o);
+        return NULL;
+    }
+    *dict = *dp;
+    return o;
+}
+
+/* One BlockArray (arrow.py) for an output record: its buffers are byte
+ * ranges of `block` (64-byte padded, clamped to the block), each torch view
+ * made when first read. */
+static PyObject* block_array(PyTypeObject* cls, PyObject* block, uint64_t base, uint64_t size, const out_rec& r,
+                             PyObject* dtypes) {
+    if (r.type < 0 || r.type >= PyList_GET_SIZE(dtypes)) {
+        PyErr_SetString(PyExc_ValueError, "bad output type");
+        return NULL;
+    }
+    PyObject* d;
+    PyObject* a = bare_instance(cls, &d);
+    if (!a) return NULL;
+    const int64_t n = r.length;
+    auto range = [&](uint64_t ptr, uint64_t nbytes, PyObject* ko, PyObject* kn) -> int {
+        if (ptr < base || ptr > base + size) {
+            PyErr_SetString(PyExc_ValueError, "output buffer outside the block");
+            return -1;
+        }
+        const uint64_t o = ptr - base;
+        uint64_t len = nbytes < 64 ? 64 : (nbytes + 63) & ~(uint64_t)63;
+        if (o + len > size) len = size - o;
+        return set_ll(d, ko, (long long)o) || set_ll(d, kn, (long long)len) ? -1 : 0;
+    };
+    int bad = PyDict_SetItem(d, s_data_type, PyList_GET_ITEM(dtypes, r.type)) || set_ll(d, s_length, n) ||
+              set_ll(d, s_null_count, r.null_count) || set_ll(d, s_offset, 0) || PyDict_SetItem(d, s__blk, block);
+    if (!bad) {
+        if (r.type == 12) { /* Utf8: offsets + data */
+            bad = range(r.offsets, (uint64_t)(n + 1) * 4, s__oo, s__on) ||
+                  range(r.data, (uint64_t)r.data_length, s__vo, s__vn);
+        } else {
+            const uint64_t nb = r.type == 1 ? (uint64_t)(n + 7) / 8 : (uint64_t)n * width_of(r.type);
+            bad = PyDict_SetItem(d, s_offsets, Py_None) || range(r.values, nb, s__vo, s__vn);
+        }
+    }
+    if (!bad)
+        bad = r.null_count > 0 ? range(r.validity, (uint64_t)(n + 7) / 8, s__bo, s__bn)
+                               : PyDict_SetItem(d, s_validity, Py_None);
+    if (bad) {
+        Py_DECREF(a);
+        return NULL;
+    }
+    return a;
+}
+
+/* make_block_batches(batch_cls, array_cls, schema, block, outs, nb, nout, inputs, dtypes) -> list
+ * The output RecordBatches of a caller-owned host-batches call
+ * (dfmi_filter_project_host_batches_into): `outs` holds nb * nout
+ * dfmi_out_column records filled by the library (pointers into `block`, a
+ * host uint8 tensor); batch b's column o is a BlockArray over the block, or --
+ * passthrough_column >= 0 -- input batch b's own Array (the Arc clone of
+ * expression.rs:272-276). One call per group: no per-batch Python. */
+static PyObject* make_block_batches(PyObject* self, PyObject* args) {
+    PyObject *bcls, *acls, *schema, *block, *inputs, *dtypes;
+    Py_buffer ob;
+    Py_ssize_t nb, nout;
+    if (!PyArg_ParseTuple(args, "O!O!OOy*nnOO!", &PyType_Type, &bcls, &PyType_Type, &acls, &schema, &block, &ob, &nb,
+                          &nout, &inputs, &PyList_Type, &dtypes))
+        return NULL;
+    PyObject* result = NULL;
+    PyObject* inseq = NULL;
+    do {
+        if (!THPVariable_Check(block)) {
+            PyErr_SetString(PyExc_TypeError, "block must be a torch.Tensor");
+            break;
+        }
+        const at::Tensor& bt = THPVariable_Unpack(block);
+        if (!bt.is_cpu() || !bt.is_contiguous()) {
+            PyErr_SetString(PyExc_ValueError, "block must be a contiguous host tensor");
+            break;
+        }
+        const uint64_t base = (uint64_t)(uintptr_t)bt.data_ptr(), size = (uint64_t)bt.nbytes();
+        if (nb < 0 || nout < 0 || ob.len < (Py_ssize_t)(nb * nout * sizeof(out_rec))) {
+            PyErr_SetString(PyExc_ValueError, "outs too small");
+            break;
+        }
+        inseq = PySequence_Fast(inputs, "inputs must be a sequence");
+        if (!inseq) break;
+        if (PySequence_Fast_GET_SIZE(inseq) < nb) {
+            PyErr_SetString(PyExc_ValueError, "fewer input batches than outputs");
+            break;
+        }
+        const out_rec* R = (const out_rec*)ob.buf;
+        result = PyList_New(nb);
+        if (!result) break;
+        bool fail = false;
+        for (Py_ssize_t b = 0; b < nb && !fail; ++b) {
+            PyObject* cols = PyList_New(nout);
+            if (!cols) {
+                fail = true;
+                break;
+            }
+            PyObject* in_cols = NULL;
+            for (Py_ssize_t o = 0; o < nout; ++o) {
+                const out_rec& r = R[b * nout + o];
+                PyObject* a;
+                if (r.passthrough_column >= 0) {
+                    if (!in_cols) {
+                        in_cols = PyObject_GetAttr(PySequence_Fast_GET_ITEM(inseq, b), s_columns);
+                        if (!in_cols) {
+                            fail = true;
+                            break;
+                        }
+                    }
+                    a = PySequence_GetItem(in_cols, r.passthrough_column);
+                } else {
+                    a = block_array((PyTypeObject*)acls, block, base, size, r, dtypes);
+                }
+                if (!a) {
+                    fail = true;
+                    break;
+                }
+                PyList_SET_ITEM(cols, o, a);
+            }
+            Py_XDECREF(in_cols);
+            PyObject* d;
+            PyObject* rb = fail ? NULL : bare_instance((PyTypeObject*)bcls, &d);
+            if (!rb || PyDict_SetItem(d, s_schema, schema) || PyDict_SetItem(d, s__columns, cols)) {
+                Py_XDECREF(rb);
+                Py_DECREF(cols);
+                fail = true;
+                break;
+            }
+            Py_DECREF(cols);
+            PyList_SET_ITEM(result, b, rb);
+        }
+        if (fail) Py_CLEAR(result);
+    } while (0);
+    Py_XDECREF(inseq);
+    PyBuffer_Release(&ob);
+    return result;
+}
+
 static PyMethodDef methods[] = {
+    {"make_block_batches", make_block_batches, METH_VARARGS,
+     "RecordBatches of BlockArrays over a caller-owned output block (dfmi_filter_project_host_batches_into)."},
     {"pack_host_batches", pack_host_batches, METH_VARARGS,
      "Fill dfmi_column / dfmi_batch records for host batches (include/dfmi.h)."},
     {NULL, NULL, 0, NULL}};
@@ -174,5 +369,13 @@ PyMODINIT_FUNC PyInit__dfmi_glue(void) {
     INTERN(s_values, "values");
     INTERN(s_offsets, "offsets");
     INTERN(s_offset, "offset");
+    INTERN(s_schema, "schema");
+    INTERN(s__blk, "_blk");
+    INTERN(s__vo, "_vo");
+    INTERN(s__vn, "_vn");
+    INTERN(s__bo, "_bo");
+    INTERN(s__bn, "_bn");
+    INTERN(s__oo, "_oo");
+    INTERN(s__on, "_on");
     return PyModule_Create(&module);
 }

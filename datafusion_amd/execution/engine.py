@@ -68,6 +68,7 @@ class DeviceEngine:
             pass
 
     def last_timing(self):
+        self.drain()
         t, m = C.c_double(), C.c_double()
         if _abi.lib().dfmi_last_timing(self.ctx, C.byref(t), C.byref(m)) != _abi.DFMI_OK:
             return None
@@ -283,24 +284,27 @@ class DeviceEngine:
 
     def filter_project_host_batches_async(self, predicate, projections: Optional[Sequence],
                                           batches: Sequence[RecordBatch], flags: int = 0,
-                                          schema: Schema = None) -> "HostBatchesFuture":
+                                          schema: Schema = None, start: bool = True) -> "HostBatchesCall":
         """filter_project_host_batches whose C call runs on the engine's worker
         thread (ctypes releases the GIL for it): the caller hands out the
         previous group's batches while this group's staging, PCIe copies and
         launch proceed. The batches' structs are built here, on the calling
         thread; result() gives what filter_project_host_batches returns -- or,
-        with `schema`, the output RecordBatches themselves (HostResultBatch:
-        one object per batch, its Arrays built when first read). The engine
-        runs one call at a time: every other entry point waits for an
-        in-flight one first (drain)."""
-        self.drain()
+        with `schema`, the output RecordBatches themselves. With `schema` the
+        outputs land in ONE block this binding owns
+        (dfmi_filter_project_host_batches_into) -- pinned, so the kernel writes
+        it in place -- and the glue builds the group's RecordBatches of
+        BlockArrays over it in one native call. start=False prepares the call
+        (structs, block) without running it: submit() starts it, so a relation
+        can prepare group g+2 while g+1 runs and start it the moment g+1 ends.
+        The engine runs one call at a time: submit() and every other entry
+        point wait for an in-flight one first (drain)."""
+        if start:
+            self.drain()
         prep = self._host_batches_prepare(predicate, projections, batches, flags)
-        if self._worker is None:
-            from concurrent.futures import ThreadPoolExecutor
-            self._worker = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dfmi-engine")
-        fut = self._worker.submit(self._host_batches_call, prep)
-        self._inflight = fut
-        return HostBatchesFuture(self, prep, fut, schema)
+        into = self._host_batches_block(prep) if schema is not None and prep[5] else None
+        call = HostBatchesCall(self, prep, schema, into)
+        return call.submit() if start else call
 
     def drain(self) -> None:
         """Wait for the in-flight asynchronous call (its result stays with its future)."""
@@ -313,17 +317,64 @@ class DeviceEngine:
     def _host_batches_prepare(self, predicate, projections, batches, flags):
         projections = list(projections or [])
         nb = len(batches)
-        ncols = len(batches[0].columns) if nb else 0
+        ncols = batches[0].num_columns() if nb else 0
         nout = len(projections) if projections else ncols
         barr, keep = host_batch_structs(batches, ncols) if nb else (None, None)
         progs = (C.c_void_p * max(1, len(projections)))(*[p.handle.value for p in projections])
         stream = torch.cuda.current_stream(self.device).cuda_stream  # the caller's stream (thread-local in torch)
+        # `batches` rides along: the structs hold raw pointers into their
+        # buffers, so the call in flight keeps the batches alive itself
         return (predicate.handle if predicate is not None else None, progs, len(projections), barr, keep, nb, nout,
-                flags, stream)
+                flags, stream, list(batches))
+
+    def _host_batches_block(self, prep):
+        """(block, outs) of a caller-owned call: a pinned host block of the
+        worst-case output size (dfmi_host_batches_output_bytes) from torch's
+        caching host allocator, and the dfmi_out_column records to fill."""
+        pred, progs, np_, barr, keep, nb, nout, flags = prep[:8]
+        L = _abi.lib()
+        size = C.c_size_t()
+        err = _abi.dfmi_error()
+        rc = L.dfmi_host_batches_output_bytes(pred, progs, np_, C.cast(barr, C.c_void_p), nb, flags, C.byref(size),
+                                              C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        block = torch.empty(max(size.value, 64), dtype=torch.uint8, pin_memory=True)
+        return block, np.zeros(max(1, nb * nout), dtype=_OUT_DTYPE)
+
+    def _host_batches_into_call(self, prep, into):
+        """dfmi_filter_project_host_batches_into (any thread): (rc, failed batch, dfmi_error)."""
+        pred, progs, np_, barr, keep, nb, nout, flags, stream = prep[:9]
+        block, outs = into
+        L = _abi.lib()
+        err = _abi.dfmi_error()
+        failed = C.c_int32(-1)
+        L.dfmi_context_set_stream(self.ctx, C.c_void_p(stream))
+        rc = L.dfmi_filter_project_host_batches_into(self.ctx, pred, progs, np_, C.cast(barr, C.c_void_p), nb, flags,
+                                                     block.data_ptr(), block.numel(), outs.ctypes.data,
+                                                     C.byref(failed), C.byref(err))
+        return rc, failed.value, err
+
+    @staticmethod
+    def _host_batches_into_finish(prep, raw, schema, into):
+        nb, nout, batches = prep[5], prep[6], prep[9]
+        rc, failed, err = raw
+        error = None
+        if rc != _abi.DFMI_OK:
+            error = ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+            error.failed_batch = failed
+            if failed < 0:  # nothing ran (arguments, capacity)
+                raise error
+        done = nb if error is None else max(0, failed)
+        from .. import _dfmi_glue
+        from ..arrow import BlockArray
+        block, outs = into
+        return _dfmi_glue.make_block_batches(RecordBatch, BlockArray, schema, block, outs, done, nout, batches,
+                                             _DTYPES), error
 
     def _host_batches_call(self, prep):
         """The C call (any thread): (rc, result handle, failed batch, dfmi_error)."""
-        pred, progs, np_, barr, keep, nb, nout, flags, stream = prep
+        pred, progs, np_, barr, keep, nb, nout, flags, stream = prep[:9]
         if nb == 0:
             return _abi.DFMI_OK, None, -1, None
         L = _abi.lib()
@@ -409,12 +460,14 @@ class AggState:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
 
     def reset(self) -> None:
+        self.eng.drain()
         err = _abi.dfmi_error()
         rc = _abi.lib().dfmi_agg_state_reset(self.eng.ctx, self.handle, C.byref(err))
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
 
     def finish(self) -> List[_abi.dfmi_agg_value]:
+        self.eng.drain()
         out = (_abi.dfmi_agg_value * len(self.aggs))()
         err = _abi.dfmi_error()
         rc = _abi.lib().dfmi_agg_state_finish(self.eng.ctx, self.handle, out, C.byref(err))
@@ -424,6 +477,7 @@ class AggState:
 
     def partial(self) -> bytes:
         """The exact partial state (for merging shards: dfmi_agg_merge_partials)."""
+        self.eng.drain()
         L = _abi.lib()
         nb = L.dfmi_agg_partial_bytes(self.handle)
         buf = C.create_string_buffer(nb)
@@ -452,11 +506,13 @@ class GroupedAggState(AggState):
         super().__init__(eng, aggs, key)
 
     def finish(self):
+        self.eng.drain()
         return _grouped_call(len(self.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_state_finish_grouped(
             self.eng.ctx, self.handle, cap, keys, vals, ng, err))
 
     def partial(self) -> bytes:
         """The exact per-group partial state (dfmi_agg_state_grouped_partial)."""
+        self.eng.drain()
         L = _abi.lib()
         err = _abi.dfmi_error()
         nb = L.dfmi_agg_state_grouped_partial_bytes(self.eng.ctx, self.handle, C.byref(err))
@@ -525,6 +581,7 @@ class ShardComm:
         return buf.raw
 
     def __init__(self, eng: DeviceEngine, world: int, rank: int, uid: bytes):
+        eng.drain()
         self.eng = eng
         self.world, self.rank = world, rank
         out = C.c_void_p()
@@ -547,6 +604,7 @@ class ShardComm:
         fn = L.dfmi_internal_shard_comm_loopback
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(_abi.dfmi_error)]
         fn.restype = C.c_int32
+        eng.drain()
         self = cls.__new__(cls)
         self.eng = eng
         self.world, self.rank = None, rank
@@ -563,6 +621,7 @@ class ShardComm:
 
     def gather_to_root(self, cols: List[Array], root: int = 0) -> Optional[List[Array]]:
         """The last shard pass's outputs concatenated on `root` (collective)."""
+        self.eng.drain()
         place = self.placement
         n = place.total_rows
         L = _abi.lib()
@@ -591,6 +650,7 @@ class ShardComm:
 
     def agg_finish(self, state: "AggState") -> List[_abi.dfmi_agg_value]:
         """Every rank's exact aggregate partial merged (collective)."""
+        self.eng.drain()
         arr = (C.c_void_p * len(state.aggs))(*[a.handle.value for a in state.aggs])
         out = (_abi.dfmi_agg_value * len(state.aggs))()
         err = _abi.dfmi_error()
@@ -602,6 +662,7 @@ class ShardComm:
 
     def agg_finish_grouped(self, state: "GroupedAggState"):
         """Every rank's per-group partials merged (collective): (keys, values)."""
+        self.eng.drain()
         arr = (C.c_void_p * len(state.aggs))(*[a.handle.value for a in state.aggs])
         return _grouped_call(len(state.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_shard_agg_finish_grouped(
             self.eng.ctx, self.handle, state.handle, arr, len(state.aggs), cap, keys, vals, ng, err))
@@ -621,7 +682,12 @@ class ShardComm:
 _COL_DTYPE = np.dtype([("type", "<i4"), ("reserved", "<i4"), ("length", "<i8"), ("null_count", "<i8"),
                        ("validity", "<u8"), ("values", "<u8"), ("offsets", "<u8"), ("offset", "<i8")])
 _BATCH_DTYPE = np.dtype([("num_columns", "<i4"), ("reserved", "<i4"), ("num_rows", "<i8"), ("columns", "<u8")])
+_OUT_DTYPE = np.dtype([("values", "<u8"), ("validity", "<u8"), ("offsets", "<u8"), ("data", "<u8"),
+                       ("data_capacity", "<i8"), ("type", "<i4"), ("passthrough_column", "<i4"), ("length", "<i8"),
+                       ("null_count", "<i8"), ("data_length", "<i8")])
 assert _COL_DTYPE.itemsize == C.sizeof(_abi.dfmi_column) and _BATCH_DTYPE.itemsize == C.sizeof(_abi.dfmi_batch)
+assert _OUT_DTYPE.itemsize == C.sizeof(_abi.dfmi_out_column)
+_DTYPES = [DataType(i) for i in range(13)]  # dfmi_type -> DataType (the glue's output types)
 
 
 def host_batch_structs(batches: Sequence[RecordBatch], ncols: int):
@@ -636,17 +702,47 @@ def host_batch_structs(batches: Sequence[RecordBatch], ncols: int):
     return (_abi.dfmi_batch * nb).from_buffer(ba), (cols, ba)
 
 
-class HostBatchesFuture:
-    """An in-flight filter_project_host_batches_async call."""
+class HostBatchesCall:
+    """One filter_project_host_batches_async call: prepared, then submitted
+    to the engine's worker thread, then finished on the caller's thread."""
 
-    def __init__(self, eng: DeviceEngine, prep, fut, schema=None):
-        self.eng, self.prep, self.fut, self.schema = eng, prep, fut, schema
+    __slots__ = ("eng", "prep", "schema", "into", "fut", "raw")
+
+    def __init__(self, eng: DeviceEngine, prep, schema=None, into=None):
+        self.eng, self.prep, self.schema, self.into = eng, prep, schema, into
+        self.fut = self.raw = None
+
+    def submit(self) -> "HostBatchesCall":
+        eng = self.eng
+        eng.drain()
+        if eng._worker is None:
+            from concurrent.futures import ThreadPoolExecutor
+            eng._worker = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dfmi-engine")
+        if self.into is not None:
+            self.fut = eng._worker.submit(eng._host_batches_into_call, self.prep, self.into)
+        else:
+            self.fut = eng._worker.submit(eng._host_batches_call, self.prep)
+        eng._inflight = self.fut
+        return self
+
+    def wait(self) -> bool:
+        """Wait for the call; True when every batch ran without an error."""
+        if self.raw is None:
+            if self.fut is None:
+                self.submit()
+            self.raw = self.fut.result()
+            if self.eng._inflight is self.fut:
+                self.eng._inflight = None
+        return self.raw[0] == _abi.DFMI_OK
 
     def result(self):
-        raw = self.fut.result()
-        if self.eng._inflight is self.fut:
-            self.eng._inflight = None
-        return DeviceEngine._host_batches_finish(self.prep, raw, self.schema)
+        self.wait()
+        if self.into is not None:
+            return DeviceEngine._host_batches_into_finish(self.prep, self.raw, self.schema, self.into)
+        return DeviceEngine._host_batches_finish(self.prep, self.raw, self.schema)
+
+
+HostBatchesFuture = HostBatchesCall  # (the name of round 4)
 
 
 class _ResultOwner:

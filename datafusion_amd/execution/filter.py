@@ -17,10 +17,23 @@ def is_host_batch(b: RecordBatch) -> bool:
 def detach(b: RecordBatch) -> RecordBatch:
     """A batch that owns its buffers: a source's zero-copy views (e.g.
     NativeCsvDataSource(copy=False)) are valid only until its next pull."""
+    return RecordBatch(b.schema, [_own(a) for a in b.columns])
+
+
+def _own(a):
+    """A copy of Array `a` that owns its buffers, rebased to offset 0 (a
+    sliced array keeps only its rows: values, bitmaps and Utf8 offsets)."""
     from ..arrow import Array
+    from ..logicalplan import DataType
     cl = lambda t: None if t is None else t.clone()
-    return RecordBatch(b.schema, [Array(a.data_type, a.length, cl(a.values), cl(a.validity), cl(a.offsets),
-                                        a.null_count) for a in b.columns])
+    if not a.offset:
+        return Array(a.data_type, a.length, cl(a.values), cl(a.validity), cl(a.offsets), a.null_count)
+    valid = a.valid_mask() if a.validity is not None else None
+    if a.data_type == DataType.Utf8:
+        vals = a.numpy_values()
+        return Array.from_strings([None if (valid is not None and not valid[i]) else vals[i]
+                                   for i in range(a.length)]) if valid is not None else Array.from_strings(vals)
+    return Array.from_numpy(a.data_type, a.numpy_values().copy(), valid)
 
 
 class Coalescer:
@@ -38,7 +51,12 @@ class Coalescer:
     With `run_many_host_async`, while one group's results are handed out the
     next group of host batches is already read and its call runs on the
     engine's worker thread (staging, PCIe and the launch overlap the pull
-    loop); the stream is the same."""
+    loop); the stream is the same. When that call object can be prepared
+    without running (it has submit()), the Coalescer keeps the worker busy:
+    group g+2 is read and prepared while g+1 runs, and is submitted the
+    moment g+1's call returns -- before g+1's output batches are built and
+    handed out -- so the pull loop's own work overlaps the device call
+    instead of adding to it."""
 
     def __init__(self, m: int, source: Relation, run_one: Callable, run_many: Callable, wrap: Callable,
                  run_many_host: Callable = None, max_rows: int = 1 << 20, run_many_host_async: Callable = None,
@@ -49,7 +67,8 @@ class Coalescer:
         self.run_many_host_async = run_many_host_async
         self.ready = deque()       # RecordBatches / exceptions, in stream order
         self.pending = deque()     # pulled input batches (or a source error) still to run one by one
-        self.ahead = None          # the next group read ahead: (future or None, batches, source error)
+        self.ahead = None          # the next group read ahead: (call in flight or None, batches, source error)
+        self.staged = None         # the group after it: (prepared call, not started, batches, source error)
 
     def _read_ahead(self):
         many = getattr(self.source, "next_many", None)
@@ -73,8 +92,9 @@ class Coalescer:
             rows += b.num_rows()
         return pulled, None
 
-    def _fetch(self):
-        """Read the next group; start its call now when it can run on the worker."""
+    def _fetch(self, start: bool = True):
+        """Read the next group and prepare its call when it can run on the
+        worker; start it now unless start=False (a call with submit())."""
         pulled, src_err = self._read_ahead()
         fut = None
         if self.run_many_host_async is not None and len(pulled) > 1 and is_host_batch(pulled[0]):
@@ -82,7 +102,22 @@ class Coalescer:
                 fut = self.run_many_host_async(pulled)
             except ValueError:  # not every batch is in host memory: the synchronous runs
                 fut = None
+            if fut is not None and start and hasattr(fut, "submit"):
+                fut.submit()
         return fut, pulled, src_err
+
+    def _take_ahead(self):
+        """The next group: the one in flight, else the prepared one (started
+        now), else a freshly read one."""
+        if self.ahead is not None:
+            a, self.ahead = self.ahead, None
+            return a
+        if self.staged is not None:
+            (fut, pulled, src_err), self.staged = self.staged, None
+            if fut is not None:
+                fut.submit()
+            return fut, pulled, src_err
+        return self._fetch()
 
     def _accept(self, pulled, results, err) -> bool:
         """Results of one coalesced call into ready; after a failing batch the
@@ -129,13 +164,20 @@ class Coalescer:
                 if isinstance(item, Exception):
                     raise item
                 return self.wrap(self.run_one(item))
-            fut, pulled, src_err = self.ahead if self.ahead is not None else self._fetch()
-            self.ahead = None
+            fut, pulled, src_err = self._take_ahead()
             if not pulled:
                 if src_err is not None:
                     raise src_err
                 return None
             if fut is not None:
+                ok = fut.wait() if hasattr(fut, "wait") else True
+                if ok and src_err is None and self.staged is not None:
+                    # the worker goes on with the next group while this one's
+                    # batches are built and handed out
+                    (nf, npulled, nerr), self.staged = self.staged, None
+                    if nf is not None:
+                        nf.submit()
+                    self.ahead = (nf, npulled, nerr)
                 results, err = fut.result()
                 self._accept(pulled, results, err)
             else:
@@ -143,7 +185,11 @@ class Coalescer:
             if src_err is not None:
                 self.pending.append(src_err)
             elif not self.pending and self.run_many_host_async is not None:
-                self.ahead = self._fetch()  # the next group runs while this one is handed out
+                if self.ahead is None and self.staged is None:
+                    self.ahead = self._fetch()  # the next group runs while this one is handed out
+                if self.ahead is not None and self.ahead[0] is not None and hasattr(self.ahead[0], "submit") \
+                        and self.ahead[2] is None and self.ahead[1] and self.staged is None:
+                    self.staged = self._fetch(start=False)  # and the one after it is prepared
         item = self.ready.popleft()
         if isinstance(item, Exception):
             raise item
@@ -195,7 +241,7 @@ class FilterRelation(Relation):
                                      lambda bs: engine(self.device).filter_project_host_batches(self.expr, None, bs,
                                                                                                 self.flags),
                                      run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
-                                         self.expr, None, bs, self.flags, schema=Schema.empty()),
+                                         self.expr, None, bs, self.flags, schema=Schema.empty(), start=False),
                                      wrap_many=_wrap_many_empty)
             return self._co.next()
         batch = self.input.next()

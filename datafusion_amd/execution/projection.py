@@ -80,7 +80,7 @@ class ProjectRelation(Relation):
                                      lambda bs: engine(self.device).filter_project_host_batches(pred, self.expr, bs,
                                                                                                 self.flags),
                                      run_many_host_async=lambda bs: engine(self.device).filter_project_host_batches_async(
-                                         pred, self.expr, bs, self.flags, schema=self._output_schema()),
+                                         pred, self.expr, bs, self.flags, schema=self._output_schema(), start=False),
                                      wrap_many=self._wrap_many)
             # later pulls go straight to the Coalescer (one Python frame less
             # per batch at the reference's 1024-row batch size)

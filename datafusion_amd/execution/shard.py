@@ -217,15 +217,29 @@ def gather_to_root(res: ShardResult, types: Sequence[DataType], root: int = 0, g
                 out.append(("validity", o, (n + 7) // 8))
         return out
 
+    def bits(buf: torch.Tensor, off: int, n: int, nb: int) -> torch.Tensor:
+        """Bits [off, off + n) of an LSB-first bitmap as nb bytes from bit 0."""
+        if off % 8 == 0:
+            return buf[off // 8: off // 8 + nb]
+        return _bool_to_bits(_bits_to_bool(buf, off + n)[off:])[:nb]
+
     def local(kind: str, o: int, nb: int) -> torch.Tensor:
+        # a passthrough output is the input Array itself, which may be sliced
+        # (arrow ArrayData::offset): read its rows from physical slot `off`
         a = res.columns[o]
+        off = a.offset
         if kind == "values":
-            start = int(a.offsets[0]) if a.data_type == DataType.Utf8 and a.length else 0
-            return a.values[start: start + nb]
-        if kind == "offsets":
-            return a.offsets[: a.length + 1].contiguous().view(torch.uint8)
+            if a.data_type == DataType.Utf8:
+                start = int(a.offsets[off]) if a.length else 0
+                return a.values[start: start + nb]
+            if a.data_type == DataType.Boolean:
+                return bits(a.values, off, a.length, nb)
+            w = a.data_type.width
+            return a.values[off * w: off * w + nb]
+        if kind == "offsets":  # (the root rebases each part from its first offset)
+            return a.offsets[off: off + a.length + 1].contiguous().view(torch.uint8)
         if a.validity is not None:
-            return a.validity[:nb]
+            return bits(a.validity, off, a.length, nb)
         return _bool_to_bits(torch.ones(a.length, dtype=torch.bool, device=a.values.device))[:nb]
 
     for o, t in enumerate(types):  # i32 offsets address < 2^31 bytes (arrow BinaryArray)

@@ -27,7 +27,14 @@
 extern "C" {
 #endif
 
-#define DFMI_ABI_VERSION 1
+/* Version of this header's structs and entry points. 2: dfmi_column.offset
+ * (arrow ArrayData::offset), dfmi_abi_version(), the caller-owned output form
+ * dfmi_filter_project_host_batches_into. A binding compares the library's
+ * dfmi_abi_version() with the constant it was built against. */
+#define DFMI_ABI_VERSION 2
+
+/* DFMI_ABI_VERSION of the loaded library. */
+int32_t dfmi_abi_version(void);
 
 /* ---------------------------------------------------------------------------
  * Types. Subset of arrow::datatypes::DataType that logicalplan.rs can name
@@ -319,6 +326,33 @@ int32_t dfmi_filter_project_host_batches(dfmi_context* ctx, const dfmi_program* 
                                          const dfmi_batch* inputs, int32_t num_batches, uint32_t flags,
                                          dfmi_host_result** out, int32_t* failed_batch, dfmi_error* err);
 
+/* Caller-owned form of dfmi_filter_project_host_batches: the outputs are
+ * written into ONE host block the caller allocated (e.g. an arrow 0.12
+ * MutableBuffer, which freezes into the Buffer every output array slices --
+ * projection.rs:59-60 / filter.rs:60-61 return freshly built arrays per pull),
+ * instead of a library-owned result. dfmi_host_batches_output_bytes gives the
+ * block's worst-case size for these batches (every row selected); the block
+ * must be 64-byte aligned. Each output buffer starts at a 256-byte multiple
+ * of the block. `outputs` (num_batches x n, batch-major, n = num_projections
+ * or num_columns without a projection) is filled by the library: values /
+ * validity (null_count > 0) / Utf8 offsets + data point into the block;
+ * passthrough_column >= 0 marks an output that IS that input column (the Arc
+ * clone of expression.rs:272-276: the caller reuses its own input array).
+ * A block in pinned memory (dfmi_host_alloc, dfmi_host_register, any
+ * hipHostMalloc'd allocation) is written by the kernel in place; a pageable
+ * block receives the selected bytes with one host copy from the library's
+ * pinned staging. Errors and *failed_batch as dfmi_filter_project_host_batches
+ * (the batches before the failing one are complete);
+ * out_capacity < the size needed -> DFMI_ERR_CAPACITY, nothing run. */
+int32_t dfmi_host_batches_output_bytes(const dfmi_program* predicate, const dfmi_program* const* projections,
+                                       int32_t num_projections, const dfmi_batch* inputs, int32_t num_batches,
+                                       uint32_t flags, size_t* bytes, dfmi_error* err);
+int32_t dfmi_filter_project_host_batches_into(dfmi_context* ctx, const dfmi_program* predicate,
+                                              const dfmi_program* const* projections, int32_t num_projections,
+                                              const dfmi_batch* inputs, int32_t num_batches, uint32_t flags,
+                                              void* out_block, size_t out_capacity, dfmi_out_column* outputs,
+                                              int32_t* failed_batch, dfmi_error* err);
+
 /* Pinned host memory for batch buffers (e.g. a CSV reader parsing straight
  * into them; csv_sql.rs:49's DataSource side). Columns whose buffers lie in
  * such memory -- or in any hipHostMalloc'd allocation of at least 1 MiB --
@@ -329,6 +363,15 @@ int32_t dfmi_host_alloc(size_t bytes, void** out, dfmi_error* err);
 int32_t dfmi_host_free(void* ptr);
 int32_t dfmi_host_register(void* ptr, size_t bytes, dfmi_error* err);
 int32_t dfmi_host_unregister(void* ptr);
+
+/* The context's GPU is shared with other processes (several ranks on one
+ * device, a time-sliced GPU): kernels with a decoupled look-back take their
+ * tiles from an atomic ticket counter from the first launch, so a tile never
+ * waits on a predecessor another process keeps off the CUs.
+ * Default: off, or DFMI_SHARED=1 in the environment at dfmi_context_create.
+ * Without it a shared launch still completes, after a 2 s look-back timeout
+ * and a ticket-ordered relaunch. */
+int32_t dfmi_context_set_shared(dfmi_context* ctx, int32_t shared);
 
 /* HIP events around each launch (default on): dfmi_last_timing needs them;
  * off saves two event records per call on the small-batch path. */
@@ -377,10 +420,11 @@ int32_t dfmi_last_error_order(const dfmi_context* ctx, uint64_t* key);
  * GROUP BY (dfmi_agg_state_create_grouped): one key, Boolean or integer;
  * per group the aggregates above. Groups come out in key order (false <
  * true, integers numerically) with the null key last -- the order of the
- * reference's expected/csv_aggregate_by_c_bool.csv. Low-cardinality keys:
- * the selected rows of one batch may hold at most 16 consecutive integer key
- * values (any number of batches, any number of groups overall); a wider batch
- * is NotImplemented.
+ * reference's expected/csv_aggregate_by_c_bool.csv. A batch whose selected
+ * keys lie within 16 consecutive integer values runs the grouped kernel; a
+ * wider batch runs the key and the arguments through the fused Selection +
+ * Projection pass and is merged into the groups on the host with the same
+ * per-row rules (any number of keys per batch and overall).
  * ------------------------------------------------------------------------- */
 typedef enum dfmi_agg_fn {       /* AggregateType (expression.rs:33-40) */
     DFMI_AGG_MIN = 0,

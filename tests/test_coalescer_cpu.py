@@ -97,13 +97,60 @@ def run_many_async(bs):
     return Done(run_many(bs))
 
 
+log = []
+
+
+class Staged:
+    """A prepared call (the engine's HostBatchesCall with start=False): runs
+    on submit(), wait() says whether every batch ran, result() hands over."""
+
+    def __init__(self, bs):
+        self.bs, self.v = bs, None
+        log.append(("prepare", tag_of(bs[0])))
+
+    def submit(self):
+        log.append(("submit", tag_of(self.bs[0])))
+        self.v = run_many(self.bs)
+        return self
+
+    def wait(self):
+        assert self.v is not None, "waited on a call that was never submitted"
+        return self.v[1] is None
+
+    def result(self):
+        log.append(("result", tag_of(self.bs[0])))
+        return self.v
+
+
 def co(src, m=8, max_rows=1 << 20, asynchronous=False):
     calls.clear()
+    log.clear()
+    fn = None
+    if asynchronous == "staged":
+        fn = Staged
+    elif asynchronous:
+        fn = run_many_async
     return Coalescer(m, src, run_one, None, lambda cols: RecordBatch(Schema.empty(), cols), run_many,
-                     max_rows=max_rows, run_many_host_async=run_many_async if asynchronous else None)
+                     max_rows=max_rows, run_many_host_async=fn)
 
 
-@pytest.mark.parametrize("asynchronous", [False, True])
+def test_staged_calls_keep_the_worker_busy():
+    """With prepared calls, group g+1 is submitted as soon as group g's call
+    returns -- before g's results are taken -- and group g+2 is read and
+    prepared (not started) while g+1 runs; the stream is unchanged."""
+    c = co(Source(40), asynchronous="staged")
+    assert tag_of(c.next()) == 0.0
+    assert log == [("prepare", 0.0), ("submit", 0.0), ("result", 0.0), ("prepare", 8.0), ("submit", 8.0),
+                   ("prepare", 16.0)]
+    for _ in range(7):
+        c.next()
+    log.clear()
+    assert tag_of(c.next()) == 8.0
+    assert log == [("submit", 16.0), ("result", 8.0), ("prepare", 24.0)]
+    assert stream(c) == [float(i) for i in range(9, 40)]
+
+
+@pytest.mark.parametrize("asynchronous", [False, True, "staged"])
 def test_order_and_one_call_per_group(asynchronous):
     assert stream(co(Source(20), asynchronous=asynchronous)) == [float(i) for i in range(20)]
     assert calls == [8, 8, 4]
@@ -123,7 +170,7 @@ def test_row_bound_ends_read_ahead():
     assert calls == [3, 3, 3]  # 4-row batches: three reach 12 rows; the last one runs alone
 
 
-@pytest.mark.parametrize("asynchronous", [False, True])
+@pytest.mark.parametrize("asynchronous", [False, True, "staged"])
 @pytest.mark.parametrize("m", [8, 16])
 def test_error_in_a_middle_batch_then_the_rest(m, asynchronous):
     """Batch 13 fails: 0..12 come first, then the error, then 14.. (the
@@ -138,7 +185,7 @@ def test_error_in_a_middle_batch_then_the_rest(m, asynchronous):
     assert got[14:] == [float(i) for i in range(14, 20)]
 
 
-@pytest.mark.parametrize("asynchronous", [False, True])
+@pytest.mark.parametrize("asynchronous", [False, True, "staged"])
 @pytest.mark.parametrize("fail_at", [5, 8, 9, 12])
 def test_source_error_while_reading_ahead(fail_at, asynchronous):
     """The source fails on the pull of batch `fail_at`: the batches before it
@@ -163,7 +210,7 @@ def test_source_error_on_first_pull():
     assert got == ["bad row in batch 0", 0.0, 1.0, 2.0]
 
 
-@pytest.mark.parametrize("asynchronous", [False, True])
+@pytest.mark.parametrize("asynchronous", [False, True, "staged"])
 def test_transient_batches_are_copied_before_the_next_pull(asynchronous):
     """A source that overwrites its batch buffers on every pull (e.g.
     NativeCsvDataSource(copy=False)): the read-ahead keeps its own copies."""

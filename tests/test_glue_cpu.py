@@ -108,3 +108,48 @@ def test_host_result_batch():
     assert [as_tuple(cols[j]) for j in range(2)] == [as_tuple(column_struct(a)) for a in rb.columns]
     rb.columns = rb.columns[:1]
     assert rb.num_columns() == 1 and rb.num_rows() == 5
+
+
+def test_make_block_batches():
+    """_dfmi_glue.make_block_batches (the relations' caller-owned output path):
+    BlockArrays over one host block from dfmi_out_column records -- Float64,
+    Boolean, nullable, Utf8 and a passthrough column (the input batch's own
+    Array) -- each buffer a 64-byte padded range of the block, viewed on first
+    read; the struct packing reads a BlockArray's pointers without viewing."""
+    import torch
+    from datafusion_amd import _dfmi_glue
+    from datafusion_amd.arrow import BlockArray
+    from datafusion_amd.execution.engine import _DTYPES, _OUT_DTYPE
+    blk = torch.zeros(4096, dtype=torch.uint8)
+    base = blk.data_ptr()
+    f = np.array([1.5, -2.0, 3.25], np.float64)
+    blk[0:24] = torch.from_numpy(f.view(np.uint8))
+    blk[256] = 0b101  # Boolean values: t f t
+    blk[512] = 0b011  # validity: v v n
+    offs = np.array([0, 2, 2, 5], np.int32)
+    blk[768:784] = torch.from_numpy(offs.view(np.uint8))
+    blk[1024:1029] = torch.tensor(list(b"abxyz"), dtype=torch.uint8)
+    outs = np.zeros(4, _OUT_DTYPE)
+    outs[0] = (base, base + 512, 0, 0, 0, int(DataType.Float64), -1, 3, 1, 0)
+    outs[1] = (base + 256, 0, 0, 0, 0, int(DataType.Boolean), -1, 3, 0, 0)
+    outs[2] = (0, 0, base + 768, base + 1024, 5, int(DataType.Utf8), -1, 3, 0, 5)
+    outs[3] = (0, 0, 0, 0, 0, int(DataType.Int32), 1, 3, 0, 0)
+    src = RecordBatch(Schema.empty(), [Array.from_numpy(DataType.Float64, np.zeros(3)),
+                                       Array.from_numpy(DataType.Int32, np.array([7, 8, 9], np.int32))])
+    (rb,) = _dfmi_glue.make_block_batches(RecordBatch, BlockArray, Schema.empty(), blk, outs, 1, 4, [src], _DTYPES)
+    a, b, u, p = rb.columns
+    assert type(a) is BlockArray and a.data_type == DataType.Float64 and a.length == 3 and a.null_count == 1
+    assert "values" not in a.__dict__
+    # the packing reads pointers without making the views
+    barr, keep = host_batch_structs([rb], 4)
+    cols = C.cast(barr[0].columns, C.POINTER(_abi.dfmi_column))
+    assert (cols[0].values, cols[0].validity, cols[2].offsets, cols[2].values) == (base, base + 512, base + 768,
+                                                                                    base + 1024)
+    assert cols[3].values == src.columns[1].values.data_ptr()
+    assert "values" not in a.__dict__
+    assert a.to_pylist() == [1.5, -2.0, None]
+    assert a.values.numel() == 64 and a.values.data_ptr() == base
+    assert b.to_pylist() == [True, False, True] and b.validity is None
+    assert u.to_pylist() == ["ab", "", "xyz"] and u.offsets.dtype == torch.int32
+    assert p is src.columns[1]
+    assert as_tuple(cols[0]) == as_tuple(column_struct(a))

@@ -44,13 +44,36 @@ def make_batches(sizes, seed=1, nullable_every=3, utf8=True):
     return s, out
 
 
+def host_into(p, cp, batches, flags, pinned, shift=64):
+    """dfmi_filter_project_host_batches_into over host batches, the outputs in
+    a caller-owned block -- pinned (torch's pinned allocator: the kernel writes
+    it in place) or pageable (staged + copied by the library) -- at a 64-byte
+    (not 256-byte) aligned address; the glue builds the RecordBatches."""
+    import torch
+    eng = engine()
+    prep = eng._host_batches_prepare(p, cp, batches, flags)
+    block, outs = eng._host_batches_block(prep)
+    n = block.numel()
+    raw = torch.empty(n + shift + 256, dtype=torch.uint8, pin_memory=pinned)
+    a = (-raw.data_ptr()) % 256 + shift
+    block = raw[a:a + n]
+    assert block.data_ptr() % 64 == 0
+    block.fill_(0xCD)  # stale bytes must not leak into the results
+    res = eng._host_batches_into_call(prep, (block, outs))
+    rbs, err = eng._host_batches_into_finish(prep, res, Schema.empty(), (block, outs))
+    return [rb.columns for rb in rbs], err
+
+
 def check(schema, batches, pred_e, proj_e, flags=0, host=False):
     """Device batched results == the oracle batch by batch, or the first
     failing batch with the oracle's error (batches before it complete).
-    host: the batches stay in host memory (dfmi_filter_project_host_batches)."""
+    host: the batches stay in host memory (dfmi_filter_project_host_batches);
+    "pinned" / "pageable": ..._into with a caller-owned output block."""
     p = compile_scalar_expr(None, pred_e, schema, flags) if pred_e is not None else None
     cp = [compile_scalar_expr(None, e, schema, flags) for e in proj_e]
-    if host:
+    if host in ("pinned", "pageable"):
+        got, err = host_into(p, cp, [b.to("cpu") for b in batches], flags, host == "pinned")
+    elif host:
         got, err = engine().filter_project_host_batches(p, cp, [b.to("cpu") for b in batches], flags)
     else:
         dbs = [b.to(engine().device) for b in batches]
@@ -71,7 +94,7 @@ def check(schema, batches, pred_e, proj_e, flags=0, host=False):
     return None
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "pinned", "pageable"])
 def test_c2_query_many_batches(host):
     s, bs = make_batches(SIZES)
     pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.3))), Operator.And,
@@ -83,7 +106,7 @@ def test_c2_query_many_batches(host):
     assert check(s, bs, pred, [], host=host) is None
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "pinned", "pageable"])
 def test_utf8_equality_and_gather_many_batches(host):
     s, bs = make_batches(SIZES, seed=2)
     pred = BinaryExpr(Column(3), Operator.Eq, Literal(Utf8("w17")))
@@ -92,7 +115,7 @@ def test_utf8_equality_and_gather_many_batches(host):
     assert check(s, bs, pred, [Column(3), Column(2)], host=host) is None
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "pinned", "pageable"])
 def test_projection_only_many_batches(host):
     """No predicate: dense kernel per batch, null propagation, passthrough."""
     s, bs = make_batches(SIZES, seed=3)
@@ -101,7 +124,7 @@ def test_projection_only_many_batches(host):
     assert check(s, bs, None, projs, host=host) is None
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "pinned", "pageable"])
 def test_error_in_a_middle_batch(host):
     """DivideByZero in batch 57 only: batches 0..56 are returned, batch 57
     raises the oracle's error."""
@@ -120,7 +143,7 @@ def test_error_in_a_middle_batch(host):
     assert check(s, bs, pred, projs, host=host) is None
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "pinned", "pageable"])
 def test_static_error_fails_batch_zero(host):
     """A plan error the reference raises on every pull ("filter not supported
     for Int64", filter.rs:106-110) fails the first batch."""
@@ -133,7 +156,7 @@ def test_static_error_fails_batch_zero(host):
     assert check(s, bs, pred, [], DFMI_FLAG_EXT_GATHER_ALL, host=host) is None  # the extension gathers Int64
 
 
-@pytest.mark.parametrize("host", [False, True])
+@pytest.mark.parametrize("host", [False, True, "pinned", "pageable"])
 def test_boolean_outputs_fall_back_to_per_batch(host):
     s, bs = make_batches([1024] * 10 + [77, 0, 3000], seed=6)
     pred = BinaryExpr(Column(0), Operator.Lt, Literal(Float64(0.8)))
@@ -263,3 +286,53 @@ def test_relation_native_csv_views_coalesced(tmp_path):
         for x, y in zip(streams[0], other):
             for p, q in zip(x, y):
                 assert_same(p, q)
+
+
+def test_into_capacity_and_alignment_errors():
+    """A block smaller than dfmi_host_batches_output_bytes is refused before
+    anything runs (Capacity), as is a block that is not 64-byte aligned."""
+    import ctypes as C
+    import torch
+    from datafusion_amd import _abi
+    s, bs = make_batches([1024] * 4, seed=21, utf8=False)
+    p = compile_scalar_expr(None, BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.5))), s)
+    cp = [compile_scalar_expr(None, Column(1), s)]
+    eng = engine()
+    prep = eng._host_batches_prepare(p, cp, bs, 0)
+    block, outs = eng._host_batches_block(prep)
+    L = _abi.lib()
+    for blk, code in ((block[:block.numel() - 256], _abi.DFMI_ERR_CAPACITY), (block[8:], _abi.DFMI_ERR_INVALID_ARGUMENT)):
+        err = _abi.dfmi_error()
+        failed = C.c_int32(-1)
+        rc = L.dfmi_filter_project_host_batches_into(eng.ctx, prep[0], prep[1], prep[2], C.cast(prep[3], C.c_void_p),
+                                                     prep[5], 0, blk.data_ptr(), blk.numel(), outs.ctypes.data,
+                                                     C.byref(failed), C.byref(err))
+        assert rc == code and failed.value == -1, (rc, err.message)
+
+
+def test_relation_results_are_block_arrays_and_keep_inputs_alive():
+    """The relations' host path: output arrays are BlockArrays over one
+    caller-owned pinned block per group (views made on first read), and the
+    call in flight holds its input batches itself (dropping the
+    relation mid-stream must not free what the worker thread still reads)."""
+    import gc
+    from datafusion_amd.arrow import BlockArray
+    s, bs = make_batches([1024] * 600, seed=22, utf8=False)
+    ctx = ExecutionContext(coalesce=256)
+    ctx.register_datasource("t", MemoryDataSource(s, bs))
+    rel = ctx.sql("SELECT a, b, a * b + c FROM t WHERE a > 0.25 AND b < 0.75")
+    first = rel.next()
+    assert all(type(c) is BlockArray for c in first.columns)
+    assert "values" not in first.columns[0].__dict__  # not viewed yet
+    co = rel._co
+    assert co.ahead is not None and co.ahead[0] is not None  # the next group's call is in flight
+    assert co.ahead[0].prep[9] == co.ahead[1]  # ... and owns its input batches
+    del rel, co, ctx
+    gc.collect()
+    engine().drain()
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Float64(0.25))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.75))))
+    projs = [Column(0), Column(1), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus,
+                                              Column(2))]
+    for d, (_, r) in zip(first.columns, oracle_filter_project(s, bs[0], pred, projs)):
+        assert_same(d, r)

@@ -81,13 +81,20 @@ print(json.dumps({"expect": expect, "counts": sorted(counts),
 """
 
 
-def test_two_processes_share_one_gpu_subtiles(tmp_path):
+@pytest.mark.parametrize("shared", [False, True])
+def test_two_processes_share_one_gpu_subtiles(tmp_path, shared):
     """The low-selectivity sub-tile kernel (1% of rows selected: chosen from
-    the second launch on) in two processes at once."""
+    the second launch on) in two processes at once. With DFMI_SHARED=1 the
+    contexts know they share the GPU and start in ticket order: no launch
+    waits out the look-back timeout, so nothing is relaunched."""
     script = tmp_path / "worker.py"
     script.write_text(WORKER)
+    env = dict(os.environ)
+    env.pop("DFMI_SHARED", None)
+    if shared:
+        env["DFMI_SHARED"] = "1"
     procs = [subprocess.Popen([sys.executable, str(script), ROOT, str(11 + i), str(30_000_000), "80"],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=dict(os.environ))
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for i in range(2)]
     outs = []
     for p in procs:
@@ -101,3 +108,5 @@ def test_two_processes_share_one_gpu_subtiles(tmp_path):
         outs.append(json.loads(o.strip().splitlines()[-1]))
     for r in outs:
         assert r["counts"] == [r["expect"]], r
+        if shared:
+            assert r["relaunches"] == 0, r

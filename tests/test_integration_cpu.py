@@ -1,0 +1,181 @@
+"""INTEGRATION.md's Rust binding against the C ABI (no Rust toolchain in the
+image, so the binding is text -- this test keeps it from drifting away from
+include/dfmi.h, as round 4's 48-byte dfmi_column did):
+
+* every `#[repr(C)]` struct in INTEGRATION.md: field names, order, the C width
+  and alignment of each Rust field type, offsets and total size, against the
+  ctypes layout in datafusion_amd/_abi.py (which test_abi_cpu.py pins to the
+  header's sizes);
+* every function of its `extern "C"` block: exported by libdfmi.so, declared
+  in include/*.h with the same arity, the same kind per parameter (pointer,
+  i32, u32, i64, u64, usize, f64) and the same return kind;
+* every function the headers declare is in the block;
+* the binding's DFMI_ABI_VERSION is the header's and the library's.
+"""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from datafusion_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DOC = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+HEADERS = "\n".join(open(os.path.join(ROOT, "include", h)).read() for h in sorted(os.listdir(os.path.join(ROOT, "include"))))
+
+# Rust type -> (size, alignment) on x86-64
+RUST = {"i32": (4, 4), "u32": (4, 4), "i64": (8, 8), "u64": (8, 8), "f64": (8, 8), "usize": (8, 8), "u8": (1, 1),
+        "c_char": (1, 1)}
+
+
+def rust_blocks():
+    return re.findall(r"```rust\n(.*?)```", DOC, re.S)
+
+
+def repr_c_structs():
+    """name -> [(field, rust type)] for every #[repr(C)] struct in the doc."""
+    out = {}
+    for blk in rust_blocks():
+        for m in re.finditer(r"#\[repr\(C\)\]\s*(?:#\[derive\([^)]*\)\]\s*)?pub struct (\w+)\s*\{(.*?)\}", blk, re.S):
+            fields = []
+            for f in m.group(2).split(","):
+                f = f.strip()
+                if not f:
+                    continue
+                fm = re.match(r"pub (r#)?(\w+)\s*:\s*(.+)$", f, re.S)
+                assert fm, "unparsed field %r in %s" % (f, m.group(1))
+                fields.append((fm.group(2), " ".join(fm.group(3).split())))
+            assert m.group(1) not in out, "struct %s declared twice" % m.group(1)
+            out[m.group(1)] = fields
+    return out
+
+
+def rust_layout(t):
+    """(size, alignment) of a Rust field type."""
+    if t.startswith("*"):
+        return 8, 8
+    am = re.match(r"\[(\w+);\s*(\d+)\]$", t)
+    if am:
+        s, a = rust_layout(am.group(1))
+        return s * int(am.group(2)), a
+    assert t in RUST, "unknown Rust field type %r" % t
+    return RUST[t]
+
+
+CTYPES = {"dfmi_error": _abi.dfmi_error, "dfmi_column": _abi.dfmi_column, "dfmi_batch": _abi.dfmi_batch,
+          "dfmi_field": _abi.dfmi_field, "dfmi_schema": _abi.dfmi_schema, "dfmi_expr_node": _abi.dfmi_expr_node,
+          "dfmi_out_column": _abi.dfmi_out_column, "dfmi_agg_value": _abi.dfmi_agg_value,
+          "dfmi_shard_placement": _abi.dfmi_shard_placement}
+
+
+def test_every_header_struct_is_mirrored():
+    header_structs = set(re.findall(r"typedef struct (\w+) \{", HEADERS))
+    assert header_structs == set(CTYPES), header_structs ^ set(CTYPES)
+    assert set(repr_c_structs()) == header_structs
+
+
+@pytest.mark.parametrize("name", sorted(CTYPES))
+def test_repr_c_struct_matches_abi(name):
+    fields = repr_c_structs()[name]
+    ct = CTYPES[name]
+    assert [f for f, _ in fields] == [f for f, _ in ct._fields_], name
+    off, align = 0, 1
+    for (f, t), (cf, ctype) in zip(fields, ct._fields_):
+        size, a = rust_layout(t)
+        off = (off + a - 1) // a * a
+        assert off == getattr(ct, cf).offset, (name, f, off)
+        assert size == C.sizeof(ctype), (name, f, t, size, C.sizeof(ctype))
+        off += size
+        align = max(align, a)
+    assert (off + align - 1) // align * align == C.sizeof(ct), name
+
+
+def test_struct_fields_match_header_declarations():
+    """Field order of the header's typedefs (names only), for every mirrored struct."""
+    for name, fields in repr_c_structs().items():
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), HEADERS, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        names = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            for part in decl.split(","):  # int32_t world, rank;
+                nm = re.findall(r"(\w+)\s*(?:\[\d+\])?\s*$", part.strip())
+                names.append(nm[0])
+        assert names == [f for f, _ in fields], (name, names)
+
+
+def c_kind(t):
+    t = " ".join(t.replace("const", "").split())
+    if "*" in t:
+        return "ptr"
+    return {"int32_t": "i32", "uint32_t": "u32", "int64_t": "i64", "uint64_t": "u64", "size_t": "usize",
+            "double": "f64", "void": "void"}[t.strip()]
+
+
+def r_kind(t):
+    t = t.strip()
+    if t.startswith("*"):
+        return "ptr"
+    return t
+
+
+def header_functions():
+    """name -> (return kind, [param kinds]) of every declaration in include/*.h."""
+    text = re.sub(r"/\*.*?\*/", "", HEADERS, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*((?:const\s+)?[\w]+\s*\**)\s*(dfmi_\w+)\s*\(([^)]*)\)\s*;", text, re.M):
+        ret, name, params = m.group(1), m.group(2), m.group(3)
+        ps = [] if params.strip() in ("", "void") else params.split(",")
+        kinds = []
+        for p in ps:
+            p = re.sub(r"\[\s*\d*\s*\]", "*", p)  # arrays decay to pointers
+            p = re.sub(r"\w+\s*$", "", p.strip()) if re.search(r"[\w*]\s+\**\w+\s*$", p.strip()) else p
+            kinds.append(c_kind(p))
+        out[name] = (c_kind(ret), kinds)
+    return out
+
+
+def binding_functions():
+    """name -> (return kind, [param kinds]) of the doc's extern "C" block(s)."""
+    out = {}
+    for blk in rust_blocks():
+        for em in re.finditer(r'extern "C" \{(.*?)\n\}', blk, re.S):
+            body = re.sub(r"//[^\n]*", "", em.group(1))
+            for m in re.finditer(r"pub fn (\w+)\s*\((.*?)\)\s*(->\s*([^;]+))?;", body, re.S):
+                params = [p for p in m.group(2).split(",") if p.strip()]
+                kinds = [r_kind(p.split(":", 1)[1]) for p in params]
+                ret = r_kind(m.group(4)) if m.group(4) else "void"
+                assert m.group(1) not in out, "declared twice: " + m.group(1)
+                out[m.group(1)] = (ret, kinds)
+    return out
+
+
+def test_extern_block_matches_header_and_library():
+    hdr = header_functions()
+    rs = binding_functions()
+    assert set(hdr) == set(_abi.EXPORTED)  # the header parse sees what test_abi_cpu sees
+    assert set(rs) == set(hdr), sorted(set(rs) ^ set(hdr))
+    L = _abi.lib()
+    for name, (ret, kinds) in rs.items():
+        assert hasattr(L, name), name
+        assert (ret, kinds) == hdr[name], (name, (ret, kinds), hdr[name])
+
+
+def test_abi_version_constant():
+    m = re.search(r"pub const DFMI_ABI_VERSION: i32 = (\d+);", DOC)
+    h = re.search(r"#define DFMI_ABI_VERSION (\d+)", HEADERS)
+    assert m and h and int(m.group(1)) == int(h.group(1)) == _abi.DFMI_ABI_VERSION
+    assert _abi.lib().dfmi_abi_version() == _abi.DFMI_ABI_VERSION
+    assert "dfmi_abi_version()" in DOC and "DfmiContext::new" in DOC
+
+
+def test_fusion_is_planned_in_context_not_over_a_trait_object():
+    """the fused pass is built where the plan is visible
+    (context.rs Projection arm matching Projection{Selection}), and the
+    relations call the programs carried by RuntimeExpr (get_prog)."""
+    assert "LogicalPlan::Selection { expr: ref p, input: ref sel_input }" in DOC
+    assert ".prog()" not in DOC and "get_prog()" in DOC
+    assert "prog: Rc<DfmiProgram>" in DOC

@@ -138,6 +138,51 @@ def test_sharded_projection_with_nulls_matches_oracle():
     assert out[0][6] == [r.null_count]
 
 
+def _slice_worker(rank, world, port, q):
+    """Projection-only shards whose outputs are passthrough columns (the input
+    Arrays themselves, expression.rs:272-276) over SLICED inputs (arrow
+    ArrayData::offset 3 / 5: bitmaps not byte-aligned): the root gather reads
+    each rank's rows from its physical slots."""
+    try:
+        import torch.distributed as dist
+
+        from datafusion_amd.execution.shard import ShardedFilterProject, gather_to_root
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = shard_range(N, rank, world)
+        batch, _ = table(lo, hi, nullable=True)
+        off = 3 + 2 * rank
+        cols = [c.slice(off, c.length - off - 1) for c in batch.columns]
+        bools = Array.from_numpy(DataType.Boolean, np.arange(hi - lo) % 3 == 0).slice(off, hi - lo - off - 1)
+        outs = [cols[3], cols[0], bools]
+        step = ShardedFilterProject(None, [Column(3), Column(0), Column(4)], run_shard=lambda p, e, bt, f: outs)
+        res = step(RecordBatch(SCHEMA, cols))
+        full = gather_to_root(res, [c.data_type for c in res.columns], root=0)
+        q.put((rank, [c.to_pylist() for c in outs], None if full is None else [c.to_pylist() for c in full]))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put(("error", traceback.format_exc(), str(e)))
+
+
+def test_gather_of_sliced_passthrough_columns():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slice_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+    errs = [o for o in out if o[0] == "error"]
+    assert not errs, errs[0][1]
+    out = sorted(out, key=lambda o: o[0])
+    want = [out[0][1][c] + out[1][1][c] for c in range(3)]
+    assert out[0][2] == want
+    assert any(v is None for v in want[1])  # the nullable column kept its nulls
+
+
 def _fail_worker(rank, world, port, plan, q):
     """plan[rank] = None (healthy) or (status code, message, evaluation position)."""
     try:
