@@ -1273,7 +1273,8 @@ def _gpu_id(dev):
     HIP-event times come from, next to the committed profile's box."""
     try:
         p = torch.cuda.get_device_properties(dev)
-        return "%s pci %s:%s" % (p.name, getattr(p, "pci_bus_id", "?"), getattr(p, "pci_device_id", "?"))
+        return "%s %s uuid %s pci %s" % (p.name, getattr(p, "gcnArchName", ""), getattr(p, "uuid", "?"),
+                                          getattr(p, "pci_bus_id", "?"))
     except Exception:  # noqa: BLE001
         return None
 

@@ -51,7 +51,18 @@ struct Built {
     bool any_kernel_out = false;
     int64_t n_tiles = 0;
     bool low_sel = false;  // in: this query shape selected few rows last time (dfmi_context::sel_hint)
+    bool ring_ok = false;  // in: ... selected many rows with short Utf8 strings (the ring-staged gather)
 };
+
+// The ring-staged Utf8 gather stages every byte of a 256-row step (not only
+// the selected strings), into slots of kRingSlot 16-byte chunks: chosen when
+// the same query shape's previous large batch selected at least kRingSel of
+// its rows and its selected strings averaged at most kRingLen bytes (a step
+// then fits a slot with ~10% to spare; a longer step copies per lane).
+constexpr int kRingSlot = 256;
+constexpr double kRingSel = 0.15;
+constexpr double kRingLen = 14.5;
+constexpr bool kRingDefault = false;
 
 // A numeric predicate over a large batch that selects few rows runs the
 // sub-tile kernel: M sub-tiles of BLOCK * K rows share one scan + look-back
@@ -245,6 +256,11 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             X.BLOCK = 256;
             X.waves_per_eu = 7;
             X.waves_soft = true;
+            // ... at high selectivity, the ring-staged gather (one loader wave)
+            // when kRingDefault: same-box A/B (profiles/r05/c3_ring_ab.log) put it
+            // within the box's spread of the per-wave gather (1.135-1.153 vs
+            // 1.138-1.143 ms per C3 batch), so it stays a diagnostic variant
+            if (kRingDefault && B.ring_ok && X.utf8_outs.size() == 1 && !X.pred_slots.empty()) X.ring = kRingSlot;
         } else if (pred && B.low_sel && !X.pred_slots.empty() && X.utf8_cols.empty() && n >= kSubtileMinRows) {
             // a numeric predicate that selected < 4% last time: M sub-tiles
             // share one look-back, a sparse output pass re-reads only the
@@ -277,6 +293,9 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
         if (const char* e = getenv("DFMI_TICKET")) X.ticket = atoi(e) & 1;  // ticket-ordered tiles from the start
         if (const char* e = getenv("DFMI_UTF8_EARLY")) X.early = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_UTF8_RING"))  // 0: off; > 0: on (slot chunks) where it applies
+            if (pred && X.utf8_outs.size() == 1 && !X.pred_slots.empty() && X.BLOCK == 256 && X.M == 1)
+                X.ring = atoi(e) > 1 ? atoi(e) : (atoi(e) == 1 ? kRingSlot : 0);
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         // the numeric sub-tile kernel at any size (parity tests, A/B runs)
@@ -475,6 +494,9 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             hint_key = sel_hint_key(pred, projs, np, in, flags);
             auto it = ctx->sel_hint.find(hint_key);
             B.low_sel = it != ctx->sel_hint.end() && it->second < kLowSel;
+            const auto lt = ctx->utf8_len_hint.find(hint_key);
+            B.ring_ok = it != ctx->sel_hint.end() && it->second >= kRingSel && lt != ctx->utf8_len_hint.end() &&
+                        lt->second <= kRingLen;
         }
         build_plan(pred, projs, np, in, outs, flags, B);
         if (ctx->shared) B.X.ticket = 1;  // shared GPU: ticket-ordered tiles from the start
@@ -691,6 +713,10 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
         if (hint_key && launch) {  // what this shape selected, for its next large batch
             if (ctx->sel_hint.size() >= 4096) ctx->sel_hint.clear();
             ctx->sel_hint[hint_key] = (double)out_rows / (double)n;
+            if (!X.utf8_outs.empty() && out_rows > 0) {
+                if (ctx->utf8_len_hint.size() >= 4096) ctx->utf8_len_hint.clear();
+                ctx->utf8_len_hint[hint_key] = (double)totals[1] / (double)out_rows;
+            }
         }
         for (int o = 0; o < nout; ++o) {
             dfmi_out_column& oc = outs[o];

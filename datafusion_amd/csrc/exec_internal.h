@@ -72,6 +72,9 @@ struct dfmi_context {
     // selectivity of each query shape's last large batch (exec.cpp
     // kSubtileMinRows): picks the sub-tile kernel for low selectivity
     std::unordered_map<uint64_t, double> sel_hint;
+    // ... and the mean bytes of its first Utf8 output's selected strings
+    // (picks the ring-staged gather, which stages whole 256-row steps)
+    std::unordered_map<uint64_t, double> utf8_len_hint;
 };
 
 namespace dfmi {

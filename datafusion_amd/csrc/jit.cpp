@@ -1039,6 +1039,9 @@ std::string generate(const Plan& P, Launch& X) {
                 if (X.gather == 3)
                     o << "  dfmi::utf8_offsets_src<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << X.utf8_outs[j].first
                       << ", selm, wm, dst" << tail << "lane, wave, " << kb << ");\n";
+                else if (X.ring && j == 0)
+                    o << "  dfmi::utf8_gather_ring<BLOCK, K, NCH, " << X.ring << ">(A, T, 1, " << u << ", "
+                      << X.utf8_outs[j].first << ", selm, dst" << tail << "RG, lane, wave, tid);\n";
                 else if (X.gather == 0)
                     o << "  dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << u << ", "
                       << X.utf8_outs[j].first << ", selm, dst" << tail << "lane, wave, " << kb << ");\n";
@@ -1065,7 +1068,9 @@ std::string generate(const Plan& P, Launch& X) {
         };
         // one tile per block in dispatch order (in order per XCD, so every
         // tile a block waits on in the look-back is running or done)
-        if (!X.utf8_outs.empty() && X.gather && X.gather != 3)
+        if (X.ring)
+            o << "  __shared__ dfmi::Utf8Ring<" << X.ring << "> RG;\n";
+        if (!X.utf8_outs.empty() && X.gather && X.gather != 3 && !(X.ring && X.utf8_outs.size() == 1))
             o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA, "
               << (X.gather == 1 ? 32 : X.gather == 5 ? 72 : X.gather == 2 ? 129 : X.image) << "> G[WAVES];\n";
         o << "  const unsigned t = tile_;\n";
@@ -1078,6 +1083,9 @@ std::string generate(const Plan& P, Launch& X) {
             emit_loads(o, X.pred_slots, X, "", "(i64)t * (BLOCK * K)", nullptr, true);
             o << "  {\n  const i64 base = (i64)t * (BLOCK * K);\n";
             emit_select();
+            if (X.ring)  // the loader wave issues the first steps' source bytes now
+                o << "  dfmi::ring_prologue<BLOCK, K, " << X.ring << ">(A, RG, " << X.utf8_outs[0].second
+                  << ", base, us" << offs_name(X.utf8_outs[0].second) << ", lane, wave);\n";
             // the first Utf8 output's first staging round goes out before the
             // look-back, whose wait then hides it
             const bool pre = !X.utf8_outs.empty() && (X.gather == 1 || X.gather >= 4) && X.prestage;
@@ -1333,7 +1341,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

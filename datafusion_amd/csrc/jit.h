@@ -73,6 +73,11 @@ struct Launch {
     // kernel holds the CUs the next tiles in dispatch order would need)
     int ticket = 0;
     int early = 0;  // Utf8 gather: stage the next group before the last slice's stores (DFMI_UTF8_EARLY)
+    // Utf8 gather of a numeric predicate at high selectivity: one loader wave
+    // streams the tile's source bytes into an LDS ring ahead of use, the block
+    // assembles and stores each 256-row step's output together
+    // (jit_skeleton.hip "ring-staged Utf8 gather"); ring = chunks per slot
+    int ring = 0;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

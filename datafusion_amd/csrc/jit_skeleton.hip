@@ -1419,6 +1419,223 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         for (int i = 0; i < 5; ++i) atomicAdd(A.stats + 8 + i, tacc[i]);
 }
 
+// ------------------------------------------------ ring-staged Utf8 gather
+// Launch::ring (numeric predicate, one Utf8 output, high selectivity): the
+// tile's source bytes are streamed into LDS by ONE wave of the block ahead of
+// use, and the block assembles and stores each step's output together.
+// A step is the 256 rows base + k*BLOCK .. (one 64-row slice per wave); its
+// source bytes [offs[base + k*BLOCK], offs[base + (k+1)*BLOCK]) are one
+// contiguous span, and its selected strings one contiguous output range.
+//   - Wave 0 (the loader) knows every step's span from its own offsets (lane
+//     0 of its slice k starts step k) plus one load of the tile's end offset,
+//     and issues direct global->LDS loads (global_load_lds_dwordx4, no VGPRs)
+//     of steps 0..R-1 before the predicate, scan and look-back -- which then
+//     hide them -- and of step k+R-1 as soon as step k-1's slot is free.
+//   - Per step the block meets once (lds_sync): step k's bytes are in LDS
+//     (the loader waited for them with a counted vmcnt, leaving the later
+//     steps' loads in flight), every wave placed step k-1, so the block
+//     stores step k-1's image -- 16-byte chunks, one or two store
+//     instructions per thread -- and zeroes it while every lane places its
+//     step-k string into the other image (utf8_place: interior words whole,
+//     the two edge words OR-merged).
+// No wave waits on its own staging round trips (round 4: 51% of the gather's
+// cycles); a step whose span exceeds a slot or whose output exceeds an image
+// copies per lane from global memory (utf8_copy).
+template <int SLOT>  // 16-byte chunks per ring slot and per image
+struct Utf8Ring {
+    static constexpr int R = 3;  // ring slots: steps k .. k+2 staged or in flight
+    uint4 src[R][SLOT];
+    uint4 img[2][SLOT];   // step images, double-buffered; zero between uses
+    int c0[16];           // per step: first source chunk (bytes from A.bytes[u], >= -15)
+    int nch[16];          // per step: chunks of the span (0: no bytes)
+};
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (the largest immediate <= n:
+// waiting for more completions than needed is conservative).
+__device__ __forceinline__ void wait_vm_at_most(int n) {
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Load instructions of one staged step (64 chunks each); 0 when not staged.
+template <int SLOT>
+__device__ __forceinline__ int ring_loads(int nch) { return nch > 0 && nch <= SLOT ? (nch + 63) >> 6 : 0; }
+
+// The loader's prologue (wave 0; call after utf8_offs_tile of the gathered
+// column u): every step's span into G.c0 / G.nch, the first R steps issued.
+// The values reach the other waves through the tile barrier (tile_offsets).
+template <int BLOCK, int K, int SLOT>
+__device__ __forceinline__ void ring_prologue(const Args& A, Utf8Ring<SLOT>& G, int u, i64 base, const int (&s)[K],
+                                              int lane, int wave) {
+    static_assert(K <= 16, "step table");
+    for (int c = lane + 64 * wave; c < 2 * SLOT; c += BLOCK) lds_zero128(&G.img[0][0] + c);  // images start zero
+    if (wave != 0) return;
+    const u8* src = A.bytes[u];
+    const int sm = (int)((u64)src & 15u);
+    const i64 rend = base + BLOCK * K < A.n_rows ? base + BLOCK * K : A.n_rows;
+    int b[K + 1];
+#pragma unroll
+    for (int k = 0; k < K; ++k) b[k] = __builtin_amdgcn_readlane(s[k], 0);  // offs[min(base + k*BLOCK, n)]
+    b[K] = __builtin_amdgcn_readfirstlane(A.offs[u][rend]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int c0 = (int)((((i64)b[k] + sm) & ~15ll) - sm);
+        const int nc = b[k + 1] > b[k] ? (int)((((i64)b[k + 1] - 1 - c0) >> 4)) + 1 : 0;
+        if (lane == 0) {
+            G.c0[k] = c0;
+            G.nch[k] = nc;
+        }
+        if (k < Utf8Ring<SLOT>::R && nc > 0 && nc <= SLOT) stage_span(at<uint4>(src, c0), G.src[k], nc, lane);
+    }
+}
+
+// Bytes [lo, hi) of LDS chunk v (0 <= lo < hi <= 16) to the global chunk w
+// (an edge chunk shared with another writer's bytes): whole words where the
+// range covers them, single bytes at the ends; all stores back to back.
+__device__ __forceinline__ void store_chunk_bytes(u8* w, uint4 v, int lo, int hi) {
+    const unsigned x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int a = 4 * q > lo ? 4 * q : lo, b = 4 * q + 4 < hi ? 4 * q + 4 : hi;
+        if (b - a == 4) {
+            *at<unsigned>(w, 4 * q) = x[q];
+        } else if (b > a) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (4 * q + t >= a && 4 * q + t < b) w[4 * q + t] = (u8)(x[q] >> (8 * t));
+        }
+    }
+}
+
+// Store a step image with the whole block (image byte 0 at the 16-byte
+// aligned output address w0; valid bytes [lo, e): lo > 0 only inside chunk 0,
+// the head of a range another writer's bytes precede), zeroing what it reads:
+// whole chunks as 16-byte stores, a partial head chunk bytewise. A partial
+// tail chunk -- its last bytes belong to the next step's output -- is carried
+// into chunk 0 of the next step's image `nx` (OR-merged: the next step's
+// strings only OR into the words it shares), or, without a next image (the
+// tile's end, or a step that does not stage), stored bytewise.
+template <int BLOCK>
+__device__ __forceinline__ void ring_store(uint4* im, u8* w0, int lo, int e, uint4* nx, int tid) {
+    const int full = e >> 4;  // chunks [0, full) end inside the range
+    for (int c = tid; c < full; c += BLOCK) {
+        const uint4 v = im[c];
+        lds_zero128(im + c);
+        if (c == 0 && lo > 0) store_chunk_bytes(w0, v, lo, 16);
+        else *at<uint4>(w0, 16 * c) = v;
+    }
+    if ((e & 15) && tid == BLOCK - 1) {  // the partial tail chunk (another thread than chunk 0's, mostly)
+        const uint4 v = im[full];
+        lds_zero128(im + full);
+        if (nx) {
+            unsigned* d = (unsigned*)nx;
+            lds_or(d, v.x);
+            lds_or(d + 1, v.y);
+            lds_or(d + 2, v.z);
+            lds_or(d + 3, v.w);
+        } else {
+            store_chunk_bytes(w0 + 16 * full, v, full == 0 ? lo : 0, e & 15);
+        }
+    }
+}
+
+// The gather (all waves; after tile_offsets and the numeric outputs).
+template <int BLOCK, int K, int NCH, int SLOT>
+__device__ __forceinline__ void utf8_gather_ring(const Args& A, const Tile<BLOCK, K, NCH>& T, int ch, int u, int o,
+                                                 unsigned selm, const unsigned (&dst)[K], const int (&s)[K],
+                                                 const int (&nx)[K], Utf8Ring<SLOT>& G, int lane, int wave, int tid) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int RR = Utf8Ring<SLOT>::R;
+    constexpr int NW = K * WAVES;
+    const u64 bpre = T.prefix[ch];
+    const i64 obase = (i64)T.prefix[0];
+    const u8* src = A.bytes[u];
+    u8* out = A.out_data[o];
+    // the image placed last (stored at the start of the next step): its
+    // valid bytes [p_lo, p_e), image byte 0 at p_w0
+    int p_img = -1, p_lo = 0, p_e = 0;
+    u8* p_w0 = nullptr;
+    int st_last = 0;  // loader: store instructions issued after the last refill (a lower bound)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int nc = __builtin_amdgcn_readfirstlane(G.nch[k]);
+        const int c0 = __builtin_amdgcn_readfirstlane(G.c0[k]);
+        if (wave == 0) {
+            // step k's loads are complete once at most the instructions issued
+            // after them are outstanding: steps k+1's loads (and, at k = 0,
+            // k+2's), then -- k >= 2: k+1 was the refill of iteration k-1 --
+            // that iteration's stores (vmcnt counts loads and stores in order;
+            // fewer than issued is conservative)
+            int after = 0;
+            if (k + 1 < K) after += ring_loads<SLOT>(__builtin_amdgcn_readfirstlane(G.nch[k + 1]));
+            if (k == 0 && k + 2 < K) after += ring_loads<SLOT>(__builtin_amdgcn_readfirstlane(G.nch[k + 2]));
+            if (k >= 2 && k + 1 < K) after += st_last;
+            // (diagnostics, A.mode: bit 8 waits for everything, bit 9 not at all -- wrong bytes)
+            if (A.mode & 256) after = 0;
+            if (!(A.mode & 512)) wait_vm_at_most(after);
+        }
+        lds_sync();  // step k staged; every wave placed step k-1
+        // the loader refills the slot step k-1 used (its placements are done)
+        if (wave == 0 && k >= 1 && k + RR - 1 < K) {
+            const int j = k + RR - 1;
+            const int cj = __builtin_amdgcn_readfirstlane(G.c0[j]), nj = __builtin_amdgcn_readfirstlane(G.nch[j]);
+            if (nj > 0 && nj <= SLOT) stage_span(at<uint4>(src, cj), G.src[j % RR], nj, lane);
+        }
+        // ---- this step's output range (uniform)
+        const u64 st0 = T.excl[ch][k * WAVES];  // the step's first output byte (in the tile)
+        const u64 st1 = k * WAVES + WAVES < NW ? T.excl[ch][(k + 1) * WAVES] : T.agg[ch];
+        const int Ls = (int)(st1 - st0);
+        const u64 O = bpre + st0;
+        const bool cap_ok = (i64)(O + (u64)Ls) <= A.out_cap[o];
+        const int sh = (int)(((u64)out + O) & 15u);
+        const bool imaged = cap_ok && nc <= SLOT && sh + Ls <= 16 * SLOT;
+        uint4* const im = G.img[k & 1];
+        // ---- store the previous step's image; its partial tail chunk goes on
+        // in this step's image (the output continues there) when this one has one
+        int lo = sh;  // valid start of this image's chunk 0 (sh: nothing before it is ours)
+        st_last = 0;
+        if (p_img >= 0 && !(A.mode & 128)) {  // (mode bit 7: no image stores, diagnostics)
+            ring_store<BLOCK>(G.img[p_img], p_w0, p_lo, p_e, imaged ? im : nullptr, tid);
+            st_last += (p_e >> 4) > 0 ? ((p_e >> 4) - 1) / BLOCK + 1 : 0;  // chunk-loop rounds of wave 0
+            if (imaged && (p_e & 15)) lo = (p_e >> 4) == 0 ? p_lo : 0;  // carried bytes start the chunk
+        }
+        p_img = -1;
+        // ---- this step: offsets, then the strings into its image
+        const bool sel = (selm >> k) & 1;
+        const int e = utf8_end(s[k], nx[k], lane);
+        const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
+        const unsigned incl = wave_incl_scan32(L, lane);
+        const unsigned rel = incl - L;
+        const u64 ob = bpre + T.excl[ch][k * WAVES + wave] + rel;
+        if (sel) A.out_offs[o][obase + dst[k]] = (int)ob;
+        if (__ballot(sel)) ++st_last;
+        if (!cap_ok) {
+            if (tid == 0 && Ls) report_err(A.err, 0, 0, ERRK_CAPACITY);
+            continue;
+        }
+        if (imaged) {
+            if (L && !(A.mode & 64)) utf8_place((const unsigned*)G.src[k % RR], (unsigned*)im, s[k] - c0, sh + (int)(ob - O), (int)L);
+            p_img = k & 1;
+            p_lo = lo;
+            p_e = sh + Ls;
+            p_w0 = out + ((i64)O - sh);
+        } else if (L) {  // not staged / over the image: each lane copies its string
+            // (bytewise, register-light: the ring is chosen for short strings, so this is rare)
+            const u8* sp = src + s[k];
+            u8* dp = out + ob;
+#pragma unroll 1
+            for (unsigned i = 0; i < L; ++i) dp[i] = sp[i];
+        }
+    }
+    lds_sync();
+    if (p_img >= 0) ring_store<BLOCK>(G.img[p_img], p_w0, p_lo, p_e, nullptr, tid);
+}
+
 // Two-pass Utf8 gather, first pass (Launch::gather == 3): the rebased output
 // offset and the source start of each selected row of Utf8 input u; the
 // library's k_utf8_copy_rows (kernels.hip) then copies the bytes as a dense

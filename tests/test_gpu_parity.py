@@ -375,6 +375,49 @@ def test_utf8_multi_channel_many_tiles():
         run_both(s, b, BinaryExpr(Column(c), Operator.NotEq, Literal(Utf8(w))), [Column(c)], DFMI_FLAG_EXT_UTF8_COMPARE)
 
 
+def test_utf8_ring_gather(monkeypatch):
+    """The ring-staged gather (Launch::ring, forced by DFMI_UTF8_RING=1; by
+    default chosen after a large batch of the same query selected >= 15% with
+    short strings): one loader wave streams 256-row steps of source bytes into
+    an LDS ring, the block stores each step's output image. Short strings
+    (every step staged), longer ones (steps over a slot: per-lane copies),
+    a string longer than a whole slot, empty strings and nulls, selectivities
+    from 1% to 97%, and a source buffer at an odd address -- all against the
+    oracle; plus the Utf8 cases above."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_UTF8_RING", "1")
+    n = 300_001
+    rng = np.random.default_rng(41)
+    short = [bytes(rng.integers(97, 123, int(rng.integers(0, 25))).astype(np.uint8)) for _ in range(500)]
+    strs = [short[i] for i in rng.integers(0, len(short), n)]
+    for i in range(0, n, 7919):  # a few long strings: their steps exceed a slot
+        strs[i] = bytes(rng.integers(32, 127, int(rng.integers(100, 400))).astype(np.uint8))
+    strs[150_000] = b"L" * 6000  # longer than a slot by itself
+    sv = [None if rng.random() < 0.05 else x for x in strs]
+    s = Schema([Field("s", DataType.Utf8, True), Field("v", DataType.Float64, True)])
+    v = gen_unit_f64(6, 0, 0, n)
+    b = RecordBatch(s, [Array.from_strings(sv), Array.from_numpy(DataType.Float64, v, rng.random(n) >= 0.1)])
+    for k in (0.01, 0.3, 0.6, 0.97):
+        run_both(s, b, BinaryExpr(Column(1), Operator.Lt, Literal(Float64(k))), [Column(0), Column(1)])
+        run_both(s, b, BinaryExpr(Column(1), Operator.Lt, Literal(Float64(k))), [Column(1), Column(0)])
+    # the source bytes at an odd address (16-byte chunk staging from a misaligned base)
+    import torch
+    dev = engine().device
+    a = b.columns[0]
+    raw = torch.zeros(a.values.numel() + 64, dtype=torch.uint8, device=dev)
+    raw[5:5 + a.values.numel()] = a.values.to(dev)
+    moved = Array(DataType.Utf8, n, raw[5:], a.validity.to(dev), a.offsets.to(dev), a.null_count)
+    db = RecordBatch(s, [moved, b.columns[1].to(dev)])
+    pred = BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5)))
+    p = compile_scalar_expr(None, pred, s)
+    cp = [compile_scalar_expr(None, e, s) for e in (Column(0), Column(1))]
+    got = engine().filter_project(p, cp, db)
+    for d, (_, r) in zip(got, oracle_filter_project(s, b, pred, [Column(0), Column(1)])):
+        assert_same(d.cpu(), r, "misaligned source")
+    test_utf8_gather_and_equality()
+    test_utf8_many_tiles()
+
+
 @pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q", "4w", "4wd"])
 def test_utf8_gather_variants(monkeypatch, variant):
     """The Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG: 3 = two
