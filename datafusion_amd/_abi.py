@@ -175,6 +175,7 @@ EXPORTED = [
     "dfmi_agg_state_reset",
     "dfmi_agg_state_create_grouped",
     "dfmi_agg_state_finish_grouped",
+    "dfmi_agg_state_group_keys_utf8",
     "dfmi_agg_state_grouped_partial_bytes",
     "dfmi_agg_state_grouped_partial",
     "dfmi_agg_merge_grouped_partials",
@@ -352,6 +353,9 @@ def lib() -> C.CDLL:
     L.dfmi_agg_state_finish_grouped.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, P(dfmi_agg_value), P(dfmi_agg_value),
                                                 P(C.c_int64), P(dfmi_error)]
     L.dfmi_agg_state_finish_grouped.restype = C.c_int32
+    L.dfmi_agg_state_group_keys_utf8.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, P(C.c_int64),
+                                                 P(dfmi_error)]
+    L.dfmi_agg_state_group_keys_utf8.restype = C.c_int32
     L.dfmi_agg_partial_bytes.argtypes = [C.c_void_p]
     L.dfmi_agg_partial_bytes.restype = C.c_int64
     L.dfmi_agg_state_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(dfmi_error)]

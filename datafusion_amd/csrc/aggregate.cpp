@@ -60,7 +60,12 @@ struct dfmi_agg_state {
     struct HKey {
         bool null;
         __int128 ord;
-        bool operator<(const HKey& o) const { return null != o.null ? !null : (!null && ord < o.ord); }
+        std::string s;  // Utf8 keys: the bytes (ordered bytewise)
+        bool operator<(const HKey& o) const {
+            if (null != o.null) return !null;
+            if (null) return false;
+            return ord != o.ord ? ord < o.ord : s < o.s;
+        }
     };
     std::map<HKey, std::pair<uint64_t, std::vector<Partial_>>> groups;  // key -> (bits, partials + row count)
     // integer keys: the per-batch key window comes from MIN / MAX of the key
@@ -82,6 +87,26 @@ int agg_fn_of(const std::string& name) {
 }
 
 bool is_float_type(int t) { return t == DFMI_TYPE_FLOAT32 || t == DFMI_TYPE_FLOAT64; }
+
+// GROUP BY keys merged on the host for every batch (no device key window):
+// floating-point keys -- one group per bit pattern, ordered by IEEE 754
+// totalOrder (Rust's f64::total_cmp: -NaN < -inf < ... < -0.0 < +0.0 < ... <
+// +inf < +NaN) -- and Utf8 keys, ordered bytewise (shorter prefix first).
+// Build-defined (the reference executes no Aggregate): parity unpinned.
+bool host_keyed(int t) { return is_float_type(t) || t == DFMI_TYPE_UTF8; }
+
+// Order value of a non-null Boolean / integer / float key from its bits
+// (integers sign/zero-extended, Float32 bits in the low 32).
+bool is_signed_type(int t);
+__int128 key_ord(int t, uint64_t bits) {
+    if (t == DFMI_TYPE_FLOAT64) return (__int128)((bits >> 63) ? ~bits : (bits | (1ull << 63)));
+    if (t == DFMI_TYPE_FLOAT32) {
+        const uint32_t b = (uint32_t)bits;
+        return (__int128)((b >> 31) ? (uint32_t)~b : (b | 0x80000000u));
+    }
+    if (t == DFMI_TYPE_BOOLEAN) return (__int128)bits;
+    return is_signed_type(t) ? (__int128)(int64_t)bits : (__int128)bits;
+}
 
 // ---- exact merge of accumulator copies (host)
 using Partial = Partial_;
@@ -393,12 +418,11 @@ void flush_groups(dfmi_context* ctx, dfmi_agg_state* st) {
             normalize(parts[j]);
         }
         if (parts[n].count == 0) continue;  // no row of this key in the window
-        dfmi_agg_state::HKey hk{g == st->win_width, 0};
+        dfmi_agg_state::HKey hk{g == st->win_width, 0, {}};
         uint64_t bits = 0;
         if (!hk.null) {
             bits = st->win_base + (uint64_t)g;
-            hk.ord = kt == DFMI_TYPE_BOOLEAN ? (__int128)bits
-                                             : (is_signed_type(kt) ? (__int128)(int64_t)bits : (__int128)bits);
+            hk.ord = key_ord(kt, bits);
         }
         auto it = st->groups.find(hk);
         if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(na))).first;
@@ -571,11 +595,28 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
     }
     auto valid = [&](int o, int64_t i) { return hb[o].empty() || ((hb[o][i >> 3] >> (i & 7)) & 1); };
     const int kt = st->key.type;
+    // a Utf8 key: its offsets and bytes (the compacted output, or -- no
+    // predicate, a Column key -- the input column itself)
+    std::vector<int32_t> koff;
+    std::vector<uint8_t> kbytes;
+    if (kt == DFMI_TYPE_UTF8 && m > 0) {
+        const dfmi_out_column& c = outs[0];
+        const dfmi_column* src = c.passthrough_column >= 0 ? &in->columns[c.passthrough_column] : nullptr;
+        koff.resize((size_t)m + 1);
+        HIP_TRY(hipMemcpy(koff.data(), src ? src->offsets : c.offsets, koff.size() * 4, hipMemcpyDeviceToHost));
+        const size_t nbytes = (size_t)std::max(0, koff[m] - koff[0]);
+        kbytes.resize(std::max<size_t>(nbytes, 1));
+        if (nbytes)
+            HIP_TRY(hipMemcpy(kbytes.data(), (src ? (const uint8_t*)src->values : c.data) + koff[0], nbytes,
+                              hipMemcpyDeviceToHost));
+    }
     for (int64_t i = 0; i < m; ++i) {
-        dfmi_agg_state::HKey hk{!valid(0, i), 0};
+        dfmi_agg_state::HKey hk{!valid(0, i), 0, {}};
         uint64_t bits = 0;
         if (!hk.null) {
-            if (kt == DFMI_TYPE_BOOLEAN) {
+            if (kt == DFMI_TYPE_UTF8) {
+                hk.s.assign((const char*)kbytes.data() + (koff[i] - koff[0]), (size_t)(koff[i + 1] - koff[i]));
+            } else if (kt == DFMI_TYPE_BOOLEAN) {
                 bits = (hv[0][i >> 3] >> (i & 7)) & 1;
                 hk.ord = (__int128)bits;
             } else {
@@ -583,7 +624,7 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
                 uint64_t raw = 0;
                 memcpy(&raw, hv[0].data() + (size_t)i * w, w);
                 bits = is_signed_type(kt) ? (uint64_t)(int64_t)narrow_int(raw, kt) : narrow_int(raw, kt);
-                hk.ord = is_signed_type(kt) ? (__int128)(int64_t)bits : (__int128)bits;
+                hk.ord = key_ord(kt, bits);
             }
         }
         auto it = st->groups.find(hk);
@@ -701,7 +742,7 @@ extern "C" int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_p
     try {
         if (!ctx || !out || !key || n <= 0 || !aggs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
         const int kt = key->type;
-        if (kt != DFMI_TYPE_BOOLEAN && !(is_numeric_type(kt) && !is_float_type(kt)))
+        if (kt != DFMI_TYPE_BOOLEAN && !is_numeric_type(kt) && kt != DFMI_TYPE_UTF8)
             throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_debug(kt)};
         if (n > 15) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 15 grouped aggregates"};
         st = new dfmi_agg_state();
@@ -724,7 +765,7 @@ extern "C" int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_p
         HIP_TRY(hipMemcpyAsync(st->acc, init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         st->init = std::move(init);
-        if (kt != DFMI_TYPE_BOOLEAN) {
+        if (kt != DFMI_TYPE_BOOLEAN && !host_keyed(kt)) {
             dfmi_error e2{};
             for (int i = 0; i < 2; ++i)
                 if (dfmi_compile_aggregate(i ? "MAX" : "MIN", key, kt, DFMI_FLAG_EXT_AGGREGATE, &st->mm[i], &e2) != DFMI_OK)
@@ -755,6 +796,34 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
         HIP_TRY(hipSetDevice(ctx->device));
         flush_groups(ctx, st);
         emit_groups(st->groups, st->key.type, st->aggs.data(), st->aggs.size(), cap, keys, values, num_groups);
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_state_group_keys_utf8(const dfmi_agg_state* st, int32_t* offsets, int64_t num_offsets,
+                                                  uint8_t* data, int64_t data_capacity, int64_t* data_length,
+                                                  dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!st || !data_length) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (!st->grouped || st->key.type != DFMI_TYPE_UTF8)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state over a Utf8 key"};
+        int64_t total = 0;
+        for (const auto& kv : st->groups) total += (int64_t)kv.first.s.size();
+        *data_length = total;
+        if (num_offsets < (int64_t)st->groups.size() + 1 || data_capacity < total)
+            throw Fail{DFMI_ERR_CAPACITY, "key offsets / bytes capacity too small"};
+        if (!offsets || (total && !data)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        int64_t g = 0, pos = 0;
+        offsets[0] = 0;
+        for (const auto& kv : st->groups) {
+            if (!kv.first.s.empty()) memcpy(data + pos, kv.first.s.data(), kv.first.s.size());
+            pos += (int64_t)kv.first.s.size();
+            offsets[++g] = (int32_t)pos;
+        }
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -810,6 +879,13 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
         if (any_offset(in, 1)) {
             HIP_TRY(hipSetDevice(ctx->device));
             in = unslice(in, 1, us_, true, ctx->stream);
+        }
+        if (st->grouped && host_keyed(st->key.type)) {
+            // float / Utf8 keys: the key and the arguments through one fused
+            // Selection + Projection pass, each row merged on the host
+            HIP_TRY(hipSetDevice(ctx->device));
+            if (in->num_rows > 0) group_batch_on_host(ctx, st, pred, in, flags);
+            return DFMI_OK;
         }
         // the query's selectivity last time (this state, this predicate)
         const uint64_t hint_key = (uint64_t)(uintptr_t)st * 1099511628211ull ^ (uint64_t)(uintptr_t)pred;
@@ -1017,6 +1093,8 @@ extern "C" int64_t dfmi_agg_state_grouped_partial_bytes(dfmi_context* ctx, dfmi_
             if (err) *err = st->failure;
             return -(int64_t)st->failure.code;
         }
+        if (st->key.type == DFMI_TYPE_UTF8)
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "multi-GPU GROUP BY over Utf8"};
         HIP_TRY(hipSetDevice(ctx->device));
         flush_groups(ctx, st);
         return (int64_t)grouped_bytes(st->groups.size(), st->aggs.size());
@@ -1036,6 +1114,8 @@ extern "C" int32_t dfmi_agg_state_grouped_partial(dfmi_context* ctx, dfmi_agg_st
             if (err) *err = st->failure;
             return st->failure.code;
         }
+        if (st->key.type == DFMI_TYPE_UTF8)
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "multi-GPU GROUP BY over Utf8"};
         HIP_TRY(hipSetDevice(ctx->device));
         flush_groups(ctx, st);
         const size_t n = st->aggs.size();
@@ -1082,10 +1162,8 @@ extern "C" int32_t dfmi_agg_merge_grouped_partials(const dfmi_aggregate* const* 
                 uint64_t rec[2];
                 memcpy(rec, p, 16);
                 p += 16;
-                dfmi_agg_state::HKey hk{rec[0] != 0, 0};
-                if (!hk.null)
-                    hk.ord = kt == DFMI_TYPE_BOOLEAN ? (__int128)rec[1]
-                                                     : (is_signed_type((int)kt) ? (__int128)(int64_t)rec[1] : (__int128)rec[1]);
+                dfmi_agg_state::HKey hk{rec[0] != 0, 0, {}};
+                if (!hk.null) hk.ord = key_ord((int)kt, rec[1]);
                 auto it = groups.find(hk);
                 if (it == groups.end()) it = groups.emplace(hk, std::make_pair(rec[1], std::vector<Partial>(n + 1))).first;
                 for (int j = 0; j <= n; ++j) {

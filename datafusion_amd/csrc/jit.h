@@ -78,6 +78,9 @@ struct Launch {
     // assembles and stores each 256-row step's output together
     // (jit_skeleton.hip "ring-staged Utf8 gather"); ring = chunks per slot
     int ring = 0;
+    // Utf8 `col = literal` predicates: stage the wave's whole source spans into
+    // an LDS arena of eq_dense 16-byte chunks and compare from there (diagnostic A/B)
+    int eq_dense = 0;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

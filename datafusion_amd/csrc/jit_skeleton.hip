@@ -774,6 +774,64 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
+// Dense form of utf8_eq_lit_tile (Launch::eq_dense, diagnostic A/B): the
+// wave's K slices' whole source spans are staged into its LDS arena with
+// direct global->LDS loads (coalesced 16-byte chunks, ~14 B/row at C3's
+// strings) instead of fetching only the equal-length candidates' head words
+// (scattered, ~6 B/row of 64-byte sectors); candidates then compare from LDS.
+// A slice whose span does not fit the arena compares from global memory.
+template <int BLOCK, int K, int CAP>
+__device__ __forceinline__ void utf8_eq_lit_tile_dense(const Args& A, int u, int lit, const char* q, const int (&s)[K],
+                                                       const int (&nx)[K], int lane, bool (&res)[K], uint4* arena) {
+    const int len = A.str_len[lit];
+    const u8* by = A.bytes[u];
+    const int sm = (int)((u64)by & 15u);
+    int cs[K], off[K];
+    int used = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int s0 = __builtin_amdgcn_readlane(s[k], 0), s1 = __builtin_amdgcn_readfirstlane(nx[k]);
+        const int c0 = (int)((((i64)s0 + sm) & ~15ll) - sm);
+        const int n = s1 > s0 ? (int)((((i64)s1 - 1 - c0) >> 4)) + 1 : 0;
+        cs[k] = c0;
+        off[k] = -1;
+        if (n > 0 && used + n <= CAP) {
+            stage_span(at<uint4>(by, c0), arena + used, n, lane);
+            off[k] = 16 * used;
+            used += n;
+        }
+    }
+    wait_vm_loads();
+    wave_lds_fence();
+    const u8* lb = (const u8*)arena;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int e = utf8_end(s[k], nx[k], lane);
+        bool eq = e - s[k] == len;
+        if (eq) {
+            if (off[k] >= 0) {
+                const u8* p = lb + off[k] + (s[k] - cs[k]);
+#pragma unroll 1
+                for (int i = 0; i < len; ++i)
+                    if (p[i] != (u8)q[i]) {
+                        eq = false;
+                        break;
+                    }
+            } else {
+                const u8* p = by + s[k];
+#pragma unroll 1
+                for (int i = 0; i < len; ++i)
+                    if (p[i] != (u8)q[i]) {
+                        eq = false;
+                        break;
+                    }
+            }
+        }
+        res[k] = eq;
+    }
+    wave_lds_fence();  // the arena is reused by the next sub-tile
+}
+
 // OR v into the LDS word p (no return value). Through inline asm: the
 // compiler's wait-count pass, which does not see the explicit vmcnt wait
 // after each staging round, otherwise puts an s_waitcnt vmcnt(0) before

@@ -84,7 +84,9 @@ class AggregateRelation(Relation):
         keys, vals = state.finish()
         if not keys:
             return None
-        cols = [agg_values_array(keys)] + [agg_values_array([g[j] for g in vals]) for j in range(len(self.aggs))]
+        kcol = Array.from_strings(state.key_strings()) if DataType(keys[0].type) == DataType.Utf8 \
+            else agg_values_array(keys)
+        cols = [kcol] + [agg_values_array([g[j] for g in vals]) for j in range(len(self.aggs))]
         return RecordBatch(self._schema, cols)
 
     def schema(self) -> Schema:

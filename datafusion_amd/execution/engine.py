@@ -507,8 +507,26 @@ class GroupedAggState(AggState):
 
     def finish(self):
         self.eng.drain()
-        return _grouped_call(len(self.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_state_finish_grouped(
+        self._last = _grouped_call(len(self.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_state_finish_grouped(
             self.eng.ctx, self.handle, cap, keys, vals, ng, err))
+        return self._last
+
+    def key_strings(self) -> List[Optional[bytes]]:
+        """The Utf8 keys of the groups of the last finish(), in its order
+        (None for the null key): dfmi_agg_state_group_keys_utf8."""
+        self.eng.drain()
+        L = _abi.lib()
+        err = _abi.dfmi_error()
+        ln = C.c_int64()
+        L.dfmi_agg_state_group_keys_utf8(self.handle, None, 0, None, 0, C.byref(ln), C.byref(err))
+        keys, _ = self._last
+        offs = np.zeros(len(keys) + 1, np.int32)
+        data = np.zeros(max(1, ln.value), np.uint8)
+        rc = L.dfmi_agg_state_group_keys_utf8(self.handle, offs.ctypes.data, offs.size, data.ctypes.data, data.size,
+                                              C.byref(ln), C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        return [None if k.is_null else bytes(data[offs[g]:offs[g + 1]]) for g, k in enumerate(keys)]
 
     def partial(self) -> bytes:
         """The exact per-group partial state (dfmi_agg_state_grouped_partial)."""

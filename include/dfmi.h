@@ -417,10 +417,14 @@ int32_t dfmi_last_error_order(const dfmi_context* ctx, uint64_t* key);
  *   MIN/MAX(e): NaN values are skipped (a set of only NaNs gives the
  *             canonical NaN), -0.0 orders below +0.0;
  *   SUM/MIN/MAX over no non-null value is null.
- * GROUP BY (dfmi_agg_state_create_grouped): one key, Boolean or integer;
+ * GROUP BY (dfmi_agg_state_create_grouped): one key of any type the
+ * reference's values take -- Boolean, integer, Float32 / Float64 or Utf8;
  * per group the aggregates above. Groups come out in key order (false <
- * true, integers numerically) with the null key last -- the order of the
- * reference's expected/csv_aggregate_by_c_bool.csv. A batch whose selected
+ * true, integers numerically, floats by IEEE 754 totalOrder with one group
+ * per bit pattern -- -NaN < -inf < ... < -0.0 < +0.0 < ... < +inf < +NaN, as
+ * Rust's total_cmp --, Utf8 bytewise) with the null key last -- the order of
+ * the reference's expected/csv_aggregate_by_c_bool.csv. Float and Utf8 keys
+ * are merged on the host for every batch (below). A batch whose selected
  * keys lie within 16 consecutive integer values runs the grouped kernel; a
  * wider batch runs the key and the arguments through the fused Selection +
  * Projection pass and is merged into the groups on the host with the same
@@ -478,9 +482,9 @@ int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, int32_t num_a
                                 dfmi_error* err);
 /* GROUP BY extension: LogicalPlan::Aggregate{group_expr: [key]}
  * (sqlplanner.rs:91-117; the reference's executor stops at context.rs:161).
- * `key` compiled by dfmi_compile_scalar_expr over the same schema (Boolean or
- * an integer type; otherwise NotImplemented "GROUP BY over <type>"), at most
- * 15 aggregates. Batches go through dfmi_aggregate_batch. */
+ * `key` compiled by dfmi_compile_scalar_expr over the same schema (Boolean,
+ * integer, Float32 / Float64 or Utf8), at most 15 aggregates. Batches go
+ * through dfmi_aggregate_batch. */
 int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key, const dfmi_aggregate* const* aggs,
                                       int32_t num_aggs, dfmi_agg_state** out, dfmi_error* err);
 /* The groups so far, in key order: keys[g] (type = the key's type, is_null,
@@ -489,11 +493,18 @@ int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key
  * `capacity` (then DFMI_ERR_INVALID_ARGUMENT and nothing is written). */
 int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_state* state, int64_t capacity, dfmi_agg_value* keys,
                                       dfmi_agg_value* values, int64_t* num_groups, dfmi_error* err);
+/* The Utf8 keys of the groups of the last dfmi_agg_state_finish_grouped, in
+ * the same order, as an arrow BinaryArray: offsets[0..num_groups] (from 0)
+ * and the bytes (the null key's slot is empty; keys[g].is_null says which).
+ * *data_length is set even when a capacity is too small (then
+ * DFMI_ERR_CAPACITY and nothing is written). */
+int32_t dfmi_agg_state_group_keys_utf8(const dfmi_agg_state* state, int32_t* offsets, int64_t num_offsets, uint8_t* data,
+                                       int64_t data_capacity, int64_t* data_length, dfmi_error* err);
 /* Multi-GPU GROUP BY: the exact per-group partial state (key, the group's
  * selected rows, every aggregate's partial) as host bytes -- size first
  * (negative: -status) -- and the merge of every shard's bytes into the groups
  * one state over all the shards' rows would hold, in key order (output as
- * dfmi_agg_state_finish_grouped). */
+ * dfmi_agg_state_finish_grouped). Utf8 keys: NotImplemented. */
 int64_t dfmi_agg_state_grouped_partial_bytes(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
 int32_t dfmi_agg_state_grouped_partial(dfmi_context* ctx, dfmi_agg_state* state, void* host_out, int64_t bytes,
                                        dfmi_error* err);

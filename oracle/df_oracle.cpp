@@ -1078,28 +1078,45 @@ void agg_accumulate_row(AggState& st, const Array& a, int64_t i) {
 // GROUP BY key of row i of the key array: (null, order value, bits). Groups
 // are ordered by key value -- false < true, integers numerically -- with the
 // null group last (the order of expected/csv_aggregate_by_c_bool.csv).
+// Floating-point keys (build-defined, parity unpinned: the reference
+// executes no Aggregate): one group per bit pattern, ordered by IEEE 754
+// totalOrder (Rust's f64::total_cmp: -NaN < -inf < ... < -0.0 < +0.0 < ... <
+// +inf < +NaN). Utf8 keys: bytewise order, a shorter prefix first.
 struct GroupKey {
     bool null;
     __int128 ord;
-    bool operator<(const GroupKey& o) const { return null != o.null ? !null : (!null && ord < o.ord); }
+    std::string s;
+    bool operator<(const GroupKey& o) const {
+        if (null != o.null) return !null;
+        if (null) return false;
+        return ord != o.ord ? ord < o.ord : s < o.s;
+    }
 };
 GroupKey group_key(const Array& a, int64_t i, uint64_t* bits) {
     *bits = 0;
-    if (a.is_null(i)) return {true, 0};
+    if (a.is_null(i)) return {true, 0, {}};
     if (a.type == DFMI_TYPE_BOOLEAN) {
         *bits = a.bool_value(i) ? 1 : 0;
-        return {false, (__int128)*bits};
+        return {false, (__int128)*bits, {}};
     }
+    if (a.type == DFMI_TYPE_UTF8)
+        return {false, 0, std::string((const char*)a.values + a.offsets[i], (size_t)(a.offsets[i + 1] - a.offsets[i]))};
     __int128 ord = 0;
     dispatch_numeric(a.type, [&](auto tag) {
         using T = decltype(tag);
+        const T v = a.value<T>(i);
+        *bits = to_bits64(v);
         if constexpr (std::is_integral<T>::value) {
-            const T v = a.value<T>(i);
-            *bits = to_bits64(v);
             ord = (__int128)v;
+        } else if constexpr (sizeof(T) == 8) {
+            const uint64_t b = *bits;
+            ord = (__int128)((b >> 63) ? ~b : (b | (1ull << 63)));
+        } else {
+            const uint32_t b = (uint32_t)*bits;
+            ord = (__int128)((b >> 31) ? (uint32_t)~b : (b | 0x80000000u));
         }
     });
-    return {false, ord};
+    return {false, ord, {}};
 }
 
 dfmi_agg_value agg_result(const AggState& st) {
@@ -1298,14 +1315,15 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
                                  const int32_t* arg_lens, const int32_t* return_types, int32_t n,
                                  const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
                                  uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
-                                 int64_t* num_groups, dfmi_error* err) {
+                                 int64_t* num_groups, int32_t* key_offsets, uint8_t* key_data, int64_t key_data_cap,
+                                 dfmi_error* err) {
     try {
         set_err(err, DFMI_OK, "");
         if (!(flags & DFMI_FLAG_EXT_AGGREGATE)) fail(DFMI_ERR_PANIC, "not yet implemented");  // context.rs:161
         Plan p = make_plan(pred_nodes, pred_len, nullptr, nullptr, 0, schema, flags);
         ExprP kt = build_tree(key_nodes, key_len);
         Runtime key = compile(*kt, *schema, flags);
-        if (key.t != DFMI_TYPE_BOOLEAN && !(is_numeric(key.t) && key.t != DFMI_TYPE_FLOAT32 && key.t != DFMI_TYPE_FLOAT64))
+        if (key.t != DFMI_TYPE_BOOLEAN && !is_numeric(key.t) && key.t != DFMI_TYPE_UTF8)
             fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_name(key.t));
         std::vector<Runtime> args;
         std::vector<AggState> proto(n);
@@ -1342,13 +1360,20 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
         }
         *num_groups = (int64_t)groups.size();
         if ((int64_t)groups.size() > cap) fail(DFMI_ERR_INVALID_ARGUMENT, "group capacity too small");
-        int64_t g = 0;
+        int64_t g = 0, pos = 0;
+        if (key.t == DFMI_TYPE_UTF8 && key_offsets) key_offsets[0] = 0;
         for (const auto& [gk, v] : groups) {
             keys[g].type = key.t;
             keys[g].is_null = gk.null ? 1 : 0;
             keys[g].bits = v.first;
             keys[g].count = rows_of[gk];
             for (int j = 0; j < n; ++j) out[g * n + j] = agg_result(v.second[j]);
+            if (key.t == DFMI_TYPE_UTF8 && key_offsets) {  // the key column as a BinaryArray
+                if (pos + (int64_t)gk.s.size() > key_data_cap) fail(DFMI_ERR_INVALID_ARGUMENT, "key bytes capacity");
+                memcpy(key_data + pos, gk.s.data(), gk.s.size());
+                pos += (int64_t)gk.s.size();
+                key_offsets[g + 1] = (int32_t)pos;
+            }
             ++g;
         }
         return DFMI_OK;

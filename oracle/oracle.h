@@ -63,13 +63,16 @@ int32_t oracle_aggregate(const dfmi_expr_node* pred_nodes, int32_t pred_len, con
                          const int32_t* return_types, int32_t num_aggs, const dfmi_schema* schema,
                          const dfmi_batch* input, int64_t batch_rows, uint32_t flags, dfmi_agg_value* out,
                          dfmi_error* err);
-/* GROUP BY extension: one Boolean / integer key; groups in key order, null last. */
+/* GROUP BY extension: one key (Boolean, integer, float -- totalOrder, one
+ * group per bit pattern --, Utf8 -- bytewise, the keys' bytes into
+ * key_offsets / key_data); groups in key order, null last. */
 int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_len, const dfmi_expr_node* key_nodes,
                                  int32_t key_len, const char* const* names, const dfmi_expr_node* const* arg_nodes,
                                  const int32_t* arg_lens, const int32_t* return_types, int32_t n,
                                  const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
                                  uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
-                                 int64_t* num_groups, dfmi_error* err);
+                                 int64_t* num_groups, int32_t* key_offsets, uint8_t* key_data, int64_t key_data_cap,
+                                 dfmi_error* err);
 
 /* Synthetic tables, bit-identical to the device generator. */
 uint64_t oracle_splitmix64(uint64_t x);

@@ -52,7 +52,7 @@ def oracle_lib() -> C.CDLL:
                                            P(C.c_char_p), P(P(_abi.dfmi_expr_node)), P(C.c_int32), P(C.c_int32),
                                            C.c_int32, P(_abi.dfmi_schema), P(_abi.dfmi_batch), C.c_int64, C.c_uint32,
                                            C.c_int64, P(_abi.dfmi_agg_value), P(_abi.dfmi_agg_value), P(C.c_int64),
-                                           P(_abi.dfmi_error)]
+                                           C.c_void_p, C.c_void_p, C.c_int64, P(_abi.dfmi_error)]
     L.oracle_aggregate_grouped.restype = C.c_int32
     L.oracle_gen_unit_f64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_void_p]
     L.oracle_gen_i64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_void_p]
@@ -219,11 +219,12 @@ def oracle_aggregate(schema: Schema, batch: RecordBatch, pred: Optional[Expr], a
 
 
 def oracle_aggregate_grouped(schema: Schema, batch: RecordBatch, pred: Optional[Expr], key: Expr, aggs: Sequence,
-                             flags: int = None, batch_rows: int = 0, cap: int = 0):
+                             flags: int = None, batch_rows: int = 0, cap: int = 0, key_strings: bool = False):
     """Aggregate{group_expr: [key]}(Selection?(scan)) on the oracle: returns
     (keys, values) -- one dfmi_agg_value key per group (key order, null
     last) and per group the list of aggregate values -- or raises
-    ExecutionError."""
+    ExecutionError. key_strings: also the Utf8 keys' bytes per group
+    (keys, values, [bytes | None])."""
     if flags is None:
         flags = _abi.DFMI_FLAG_EXT_AGGREGATE
     L = oracle_lib()
@@ -243,10 +244,20 @@ def oracle_aggregate_grouped(schema: Schema, batch: RecordBatch, pred: Optional[
     out = (_abi.dfmi_agg_value * (cap * max(1, n)))()
     ng = C.c_int64()
     err = _abi.dfmi_error()
+    koff = np.zeros(cap + 1, np.int32)
+    kcap = 1 << 12
+    for c in batch.columns:  # the key's bytes are at most every Utf8 column's bytes
+        if c.data_type == DataType.Utf8:
+            kcap += c.values.numel()
+    kdata = np.zeros(kcap, np.uint8)
     rc = L.oracle_aggregate_grouped(pn.array if pn else None, pn.length if pn else 0, kn.array, kn.length, names, arr,
                                     lens, rts, n, C.byref(sch), C.byref(hb.cb), batch_rows, flags, cap, keys, out,
-                                    C.byref(ng), C.byref(err))
+                                    C.byref(ng), koff.ctypes.data, kdata.ctypes.data, kcap, C.byref(err))
     if rc != _abi.DFMI_OK:
         raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
     g = ng.value
-    return list(keys[:g]), [list(out[i * n:(i + 1) * n]) for i in range(g)]
+    res = (list(keys[:g]), [list(out[i * n:(i + 1) * n]) for i in range(g)])
+    if not key_strings:
+        return res
+    strs = [None if keys[i].is_null else bytes(kdata[koff[i]:koff[i + 1]]) for i in range(g)]
+    return res + (strs,)

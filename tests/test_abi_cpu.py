@@ -27,7 +27,7 @@ def test_header_symbols_exported():
     declared = set()
     for h in os.listdir(os.path.join(ROOT, "include")):
         hdr = open(os.path.join(ROOT, "include", h)).read()
-        declared |= set(re.findall(r"\b(dfmi_[a-z_]+)\s*\(", hdr))
+        declared |= set(re.findall(r"\b(dfmi_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(_abi.EXPORTED)
     L = _abi.lib()
     for name in declared:

@@ -276,11 +276,25 @@ def test_grouped_aggregate_kernels_compile():
             assert "GS = %d" % slots in src and "gsl[k]" in src and "fsum_add(S[g_]" in src
 
 
-def test_grouped_state_rejects_float_keys():
-    """GROUP BY over a float key is NotImplemented -- on the oracle too."""
+def test_oracle_groups_float_and_utf8_keys():
+    """GROUP BY over float and Utf8 keys on the oracle (build-defined, parity
+    unpinned: the reference executes no Aggregate): floats one group per bit
+    pattern in IEEE 754 totalOrder (-NaN < -inf < ... < -0.0 < +0.0 < ... <
+    +inf < +NaN), Utf8 bytewise (a shorter prefix first), the null key last."""
     from oracle_ffi import oracle_aggregate_grouped
-    s = Schema([Field("x", DataType.Float64, False)])
-    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, np.zeros(3))])
-    with pytest.raises(ExecutionError) as ei:
-        oracle_aggregate_grouped(s, b, None, Column(0), [agg("COUNT", Column(0), s)])
-    assert ei.value.kind == "NotImplemented" and ei.value.message == "GROUP BY over Float64"
+    nan = np.frombuffer(np.array([0x7FF8000000000000], np.uint64).tobytes(), np.float64)[0]
+    nneg = np.frombuffer(np.array([0xFFF8000000000001], np.uint64).tobytes(), np.float64)[0]
+    x = np.array([1.0, -0.0, 0.0, nan, nneg, np.inf, -np.inf, 1.0, 5.0])
+    valid = np.array([True] * 8 + [False])
+    s = Schema([Field("x", DataType.Float64, True), Field("t", DataType.Utf8, True)])
+    t = [b"b", b"", b"a", b"ab", b"\xff", b"a", None, b"ab", b"a"]
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, x, valid), Array.from_strings(t)])
+    keys, vals = oracle_aggregate_grouped(s, b, None, Column(0), [agg("COUNT", Column(1), s)])
+    got = [None if k.is_null else int(k.bits) for k in keys]
+    bits = lambda v: int(np.array([v], np.float64).view(np.uint64)[0])
+    assert got == [bits(nneg), bits(-np.inf), bits(-0.0), bits(0.0), bits(1.0), bits(np.inf), bits(nan), None]
+    assert [k.count for k in keys] == [1, 1, 1, 1, 2, 1, 1, 1]
+    keys, vals, strs = oracle_aggregate_grouped(s, b, None, Column(1), [agg("COUNT", Column(0), s)], key_strings=True)
+    assert strs == [b"", b"a", b"ab", b"b", b"\xff", None]
+    assert [k.count for k in keys] == [1, 3, 2, 1, 1, 1]
+    assert [v[0].bits for v in vals] == [1, 2, 2, 1, 1, 1]  # COUNT(x): non-null x per group

@@ -271,6 +271,9 @@ def run_grouped(schema, batch, pred, key, aggs, flags=AGG, batch_rows=0):
         return None
     (dk, dv), (rk, rv) = dev, ref
     assert [(k.type, k.is_null, k.bits, k.count) for k in dk] == [(k.type, k.is_null, k.bits, k.count) for k in rk]
+    if rk and rk[0].type == int(DataType.Utf8):  # the keys' bytes (dfmi_agg_state_group_keys_utf8)
+        rs = oracle_aggregate_grouped(schema, batch, pred, key, aggs, flags, batch_rows, key_strings=True)[2]
+        assert st.key_strings() == rs
     for g in range(len(rk)):
         for a, d, r in zip(aggs, dv[g], rv[g]):
             assert (d.type, d.is_null, d.count) == (r.type, r.is_null, r.count), (g, repr(a))
@@ -387,3 +390,96 @@ def test_group_by_random_keys_wide(batch_rows):
         for p in (None, pred):
             out = run_grouped(s, b, p, Column(c), aggs, fl, batch_rows=batch_rows)
             assert out is not None and len(out[0]) > 1000
+
+
+def _nan(bits):
+    return np.array([bits], np.uint64).view(np.float64)[0]
+
+
+@pytest.mark.parametrize("batch_rows", [0, 7_001])
+def test_group_by_float64_keys(batch_rows):
+    """10,000 distinct Float64 keys plus -0.0 / +0.0, +-inf and NaNs of several
+    payloads and signs (one group per bit pattern, IEEE 754 totalOrder, the
+    null key last; build-defined, parity unpinned), with and without a
+    predicate, over one batch or many -- keys, per-group row counts and every
+    aggregate bit-exact against the oracle."""
+    rng = np.random.default_rng(51)
+    n = 50_003
+    pool = np.concatenate([rng.standard_normal(10_000) * 1e3,
+                           [0.0, -0.0, np.inf, -np.inf, _nan(0x7FF8000000000000), _nan(0xFFF8000000000000),
+                            _nan(0x7FF0000000000001), _nan(0x7FF8DEADBEEF0000)]])
+    k = pool[rng.integers(0, len(pool), n)]
+    s = Schema([Field("k", DataType.Float64, True), Field("x", DataType.Float64, True), Field("v", DataType.Int64, True)])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float64, k, rng.random(n) >= 0.02),
+                        Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.1),
+                        Array.from_numpy(DataType.Int64, rng.integers(-2 ** 40, 2 ** 40, n), rng.random(n) >= 0.1)])
+    aggs = [agg("SUM", Column(1), s), agg("MIN", Column(1), s), agg("MAX", Column(2), s), agg("COUNT", Column(1), s),
+            agg("SUM", Column(2), s)]
+    fl = AGG | _abi.DFMI_FLAG_EXT_GATHER_ALL
+    pred = BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5)))
+    for p in (None, pred):
+        out = run_grouped(s, b, p, Column(0), aggs, fl, batch_rows=batch_rows)
+        assert out is not None and len(out[0]) > 5000
+
+
+def test_group_by_float32_key_and_expression_key():
+    """A Float32 key column and a Float64-valued key expression."""
+    rng = np.random.default_rng(52)
+    n = 20_011
+    s = Schema([Field("f", DataType.Float32, True), Field("x", DataType.Float64, False)])
+    f = (rng.integers(-300, 300, n) / 8).astype(np.float32)
+    f[::97] = -0.0
+    b = RecordBatch(s, [Array.from_numpy(DataType.Float32, f, rng.random(n) >= 0.05),
+                        Array.from_numpy(DataType.Float64, rng.random(n))])
+    aggs = [agg("COUNT", Column(1), s), agg("SUM", Column(1), s)]
+    fl = AGG | _abi.DFMI_FLAG_EXT_GATHER_ALL
+    assert run_grouped(s, b, None, Column(0), aggs, fl) is not None
+    key = BinaryExpr(Column(1), Operator.Multiply, Literal(Float64(16.0)))  # a computed key
+    assert run_grouped(s, b, BinaryExpr(Column(1), Operator.Gt, Literal(Float64(0.9))), key, aggs, fl) is not None
+
+
+@pytest.mark.parametrize("batch_rows", [0, 4_099])
+def test_group_by_utf8_keys(batch_rows):
+    """1,000 distinct Utf8 keys (empty, multi-byte UTF-8, bytes >= 0x80,
+    prefixes of each other), a nullable key column, with and without a
+    predicate, one batch or many: keys (bytewise order, null last), their
+    bytes, row counts and aggregates bit-exact against the oracle."""
+    rng = np.random.default_rng(53)
+    n = 40_009
+    words = [bytes(rng.integers(97, 123, int(rng.integers(0, 12))).astype(np.uint8)) for _ in range(990)]
+    words += [b"", b"a", b"ab", b"abc", "\u20ac".encode(), "\u20acx".encode(), b"\xff", b"\xfe\xff", b"w17", b"w1"]
+    keys = [words[i] for i in rng.integers(0, len(words), n)]
+    kv = [None if rng.random() < 0.03 else x for x in keys]
+    s = Schema([Field("s", DataType.Utf8, True), Field("x", DataType.Float64, True)])
+    b = RecordBatch(s, [Array.from_strings(kv), Array.from_numpy(DataType.Float64, wild_doubles(rng, n),
+                                                                  rng.random(n) >= 0.1)])
+    aggs = [agg("COUNT", Column(1), s), agg("SUM", Column(1), s), agg("MIN", Column(1), s), agg("MAX", Column(1), s)]
+    fl = AGG | _abi.DFMI_FLAG_EXT_GATHER_ALL
+    for p in (None, BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.3)))):
+        out = run_grouped(s, b, p, Column(0), aggs, fl, batch_rows=batch_rows)
+        assert out is not None and len(out[0]) > 500
+
+
+def test_group_by_utf8_key_through_sql():
+    """SELECT s, COUNT(x), SUM(x) FROM t WHERE x > 0.2 GROUP BY s through
+    ctx.sql: the AggregateRelation's key column is a Utf8 array in key order."""
+    from datafusion_amd.execution import ExecutionContext, MemoryDataSource
+    from oracle_ffi import oracle_aggregate_grouped
+    rng = np.random.default_rng(54)
+    n = 10_000
+    words = [b"pear", b"apple", b"fig", b"", b"banana"]
+    st = [words[i] for i in rng.integers(0, len(words), n)]
+    s = Schema([Field("s", DataType.Utf8, False), Field("x", DataType.Float64, False)])
+    x = rng.random(n)
+    b = RecordBatch(s, [Array.from_strings(st), Array.from_numpy(DataType.Float64, x)])
+    ctx = ExecutionContext(flags=AGG | _abi.DFMI_FLAG_EXT_GATHER_ALL)
+    ctx.register_datasource("t", MemoryDataSource(s, [b.to(engine().device)]))
+    (rb,) = list(ctx.sql("SELECT s, COUNT(x), SUM(x) FROM t WHERE x > 0.2 GROUP BY s"))
+    assert rb.columns[0].to_pylist() == ["", "apple", "banana", "fig", "pear"]
+    pred = BinaryExpr(Column(1), Operator.Gt, Literal(Float64(0.2)))
+    rk, rv, rs = oracle_aggregate_grouped(s, b, pred, Column(0), [agg("COUNT", Column(1), s), agg("SUM", Column(1), s)],
+                                          AGG | _abi.DFMI_FLAG_EXT_GATHER_ALL, key_strings=True)
+    assert rs == [w.encode() if isinstance(w, str) else w for w in rb.columns[0].to_pylist()]
+    assert rb.columns[1].to_pylist() == [v[0].bits for v in rv]
+    assert [int(np.array([y], np.float64).view(np.uint64)[0]) for y in rb.columns[2].to_pylist()] == \
+        [v[1].bits for v in rv]

@@ -418,6 +418,17 @@ def test_utf8_ring_gather(monkeypatch):
     test_utf8_many_tiles()
 
 
+@pytest.mark.parametrize("chunks", ["512", "64"])
+def test_utf8_equality_dense_variant(monkeypatch, chunks):
+    """Utf8 `col = literal` with the wave's whole source spans staged into LDS
+    (DFMI_UTF8_EQ_DENSE: arena chunks per wave; 64 = most slices over the arena,
+    compared from global memory) against the oracle."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_UTF8_EQ_DENSE", chunks)
+    test_utf8_gather_and_equality()
+    test_utf8_many_tiles()
+
+
 @pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q", "4w", "4wd"])
 def test_utf8_gather_variants(monkeypatch, variant):
     """The Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG: 3 = two
