@@ -574,6 +574,10 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
         st->failure = e;
         throw Fail{e.code, e.message};
     }
+    // a passthrough-only pass launches nothing, and a sliced batch's shifted
+    // bitmaps (slice.cpp) are written on ctx->stream: order the synchronous
+    // null-stream copies below after them
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     const int64_t m = outs[0].length;  // selected rows
     // host copies of values (fixed width) and validity
     std::vector<std::vector<uint8_t>> hv(no), hb(no);

@@ -1298,7 +1298,7 @@ std::string generate(const Plan& P, Launch& X) {
              (unsigned long long)(h & 0xffffffffull));
     X.kname = nm;
     body.replace(body.find("DFMI_KNAME"), 10, X.kname);
-    return std::string(dfmi_skeleton_src) + body;
+    return (X.light_copy ? std::string("#define DFMI_LIGHT_COPY 1\n") : std::string()) + dfmi_skeleton_src + body;
 }
 
 // ------------------------------------------------------- shape fast path
@@ -1347,7 +1347,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring, X.eq_dense};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring, X.eq_dense, X.light_copy};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);
@@ -1390,7 +1390,8 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
         }
     }
     std::string src = generate(P, X);
-    if (getenv("DFMI_JIT_PRINT")) fprintf(stderr, "%s\n", src.c_str() + strlen(dfmi_skeleton_src));
+    if (getenv("DFMI_JIT_PRINT"))  // the generated body (after the skeleton)
+        fprintf(stderr, "%s\n", src.c_str() + std::min(src.size(), strlen(dfmi_skeleton_src) + (X.light_copy ? 26 : 0)));
     ShapeHit h;
     std::shared_ptr<Compiled> c = compile(device, src, X.kname, compile_ms);
     if (X.waves_soft && X.waves_per_eu > 0) {

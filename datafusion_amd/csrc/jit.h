@@ -81,6 +81,9 @@ struct Launch {
     // Utf8 `col = literal` predicates: stage the wave's whole source spans into
     // an LDS arena of eq_dense 16-byte chunks and compare from there (diagnostic A/B)
     int eq_dense = 0;
+    // Utf8 gather: the rare per-lane fallback copy (a span over the stage) as
+    // a register-light byte loop instead of utf8_copy's 8-word chunks
+    int light_copy = 0;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

@@ -22,6 +22,9 @@ typedef int i32;
 typedef unsigned short u16;
 typedef unsigned u32;
 
+#ifndef DFMI_LIGHT_COPY
+#define DFMI_LIGHT_COPY 0
+#endif
 namespace dfmi {
 
 constexpr int kArgCols = 16;   // numeric / Boolean input columns
@@ -1394,7 +1397,17 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         // a span over the stage, or (LDS image) an output over the image: each lane copies its string
         if (nch > scap || ((emit == 1 || emit == 4) && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST) ||
             (emit == 3 && ((sh + (int)Ls + 3) >> 2) > 4 * IM)) {
-            if (sel && L) utf8_copy(src + s[k], out + ob0 + rel, L);
+            if (sel && L) {
+#if DFMI_LIGHT_COPY
+                // the rare per-lane fallback, register-light (Launch::light_copy)
+                const u8* sp = src + s[k];
+                u8* dp = out + ob0 + rel;
+#pragma unroll 1
+                for (unsigned i = 0; i < L; ++i) dp[i] = sp[i];
+#else
+                utf8_copy(src + s[k], out + ob0 + rel, L);
+#endif
+            }
             continue;
         }
         u8* const w0 = out + ((i64)ob0 - sh);        // the aligned word (chunk) holding the slice's first byte

@@ -35,7 +35,11 @@ NP = {DataType.Int8: np.int8, DataType.Int16: np.int16, DataType.Int32: np.int32
 
 
 def slice_batch(b: RecordBatch, r0: int, n: int) -> RecordBatch:
-    """Rows [r0, r0+n) (r0 a multiple of 8) as a view of the same buffers."""
+    """Rows [r0, r0+n) as a view of the same buffers: offset-0 views of the
+    sliced ranges when r0 is a multiple of 8, else arrow slices (a non-zero
+    dfmi_column.offset, unsliced at the boundary)."""
+    if r0 % 8:
+        return RecordBatch(b.schema, [a.slice(r0, n) for a in b.columns])
     cols = []
     for a in b.columns:
         t = a.data_type

@@ -34,7 +34,7 @@ def main(src, dst):
         if not os.path.isdir(s):
             continue
         os.makedirs(d, exist_ok=True)
-        for f in ("bench.json", "fetch_bench.json", "write_bench.json", "traffic.json"):
+        for f in ("bench.json", "fetch_bench.json", "write_bench.json", "traffic.json", "box.txt"):
             if os.path.exists(os.path.join(s, f)):
                 shutil.copy(os.path.join(s, f), os.path.join(d, f))
         shutil.copy(os.path.join(s, "kt", "kt_kernel_stats.csv"), os.path.join(d, "kernel_stats.csv"))

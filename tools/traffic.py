@@ -75,7 +75,12 @@ def main():
                       "read_correction": "2 x FETCH_SIZE x 1024"})
             e["traffic_gbs_at_avg"] = round(e["traffic_bytes"] / e["avg_ns"], 1)
         kernels.append(e)
-    out = {"source": d, "kernels": kernels,
+    box = None  # the box the profile ran on (tools/profile_r05.sh writes it): bench lines name theirs too
+    if os.path.exists(os.path.join(d, "box.txt")):
+        box = open(os.path.join(d, "box.txt")).read().strip()
+        for e in kernels:
+            e["box"] = box
+    out = {"source": d, "box": box, "kernels": kernels,
            "note": "avg_ns from the kernel trace of the same bench command; traffic per launch from separate "
                    "FETCH_SIZE / WRITE_SIZE passes of it"}
     json.dump(out, open(os.path.join(d, "traffic.json"), "w"), indent=1)
