@@ -256,6 +256,10 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             X.BLOCK = 256;
             X.waves_per_eu = 7;
             X.waves_soft = true;
+            // ... and a 16-predecessor look-back window: 8 / 12 / 16 / 24 / 32
+            // -> 1.121 / 1.099 / 1.108 / 1.122 / 1.141 ms per C3 batch, with
+            // the light fallback copy 1.094 (profiles/r05/c3_light_copy_ab2.log)
+            X.window = 16;
             // ... at high selectivity, the ring-staged gather (one loader wave)
             // when kRingDefault: same-box A/B (profiles/r05/c3_ring_ab.log) put it
             // within the box's spread of the per-wave gather (1.135-1.153 vs

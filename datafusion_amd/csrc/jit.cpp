@@ -37,6 +37,12 @@
 #include "jit.h"
 
 extern const char dfmi_skeleton_src[];  // jit_skeleton.hip, embedded by the Makefile
+namespace {
+const std::string& skeleton_text() {
+    static const std::string s(dfmi_skeleton_src);
+    return s;
+}
+}  // namespace
 
 namespace dfmi {
 namespace jit {
@@ -1288,17 +1294,21 @@ std::string generate(const Plan& P, Launch& X) {
           << "    const u64 v_ = __hip_atomic_load(h_ + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
           << "    A0.hdr_out[(i64)b_ * 32 + tid] = v_;\n    h_[tid] = 0;\n  }\n";
     o << "}\n";
-    // kernel name: the plan kind and a hash of the generated body, so that
-    // rocprofv3 reports every query shape as its own kernel
+    // kernel name: the plan kind and a hash of the whole generated source
+    // (prefix, skeleton, body), so that rocprofv3 reports every query shape
+    // as its own kernel and a skeleton change renames every kernel (a
+    // committed profile never matches code it did not measure)
     std::string body = o.str();
+    const std::string prefix = X.light_copy ? "#define DFMI_LIGHT_COPY 1\n" : "";
     uint64_t h = 1469598103934665603ull;  // FNV-1a
-    for (unsigned char ch : body) h = (h ^ ch) * 1099511628211ull;
+    for (const std::string* part : {&prefix, &skeleton_text(), (const std::string*)&body})
+        for (unsigned char ch : *part) h = (h ^ ch) * 1099511628211ull;
     char nm[64];
     snprintf(nm, sizeof nm, "dfmi_%s_%08llx", !P.aggs.empty() ? "agg" : (P.pred ? "filter" : "project"),
              (unsigned long long)(h & 0xffffffffull));
     X.kname = nm;
     body.replace(body.find("DFMI_KNAME"), 10, X.kname);
-    return (X.light_copy ? std::string("#define DFMI_LIGHT_COPY 1\n") : std::string()) + dfmi_skeleton_src + body;
+    return prefix + skeleton_text() + body;
 }
 
 // ------------------------------------------------------- shape fast path
@@ -1391,7 +1401,7 @@ hipFunction_t get_kernel(int device, const Plan& P, Launch& X, double* compile_m
     }
     std::string src = generate(P, X);
     if (getenv("DFMI_JIT_PRINT"))  // the generated body (after the skeleton)
-        fprintf(stderr, "%s\n", src.c_str() + std::min(src.size(), strlen(dfmi_skeleton_src) + (X.light_copy ? 26 : 0)));
+        fprintf(stderr, "%s\n", src.c_str() + std::min(src.size(), src.find(skeleton_text()) + skeleton_text().size()));
     ShapeHit h;
     std::shared_ptr<Compiled> c = compile(device, src, X.kname, compile_ms);
     if (X.waves_soft && X.waves_per_eu > 0) {

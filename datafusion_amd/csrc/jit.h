@@ -81,9 +81,11 @@ struct Launch {
     // Utf8 `col = literal` predicates: stage the wave's whole source spans into
     // an LDS arena of eq_dense 16-byte chunks and compare from there (diagnostic A/B)
     int eq_dense = 0;
-    // Utf8 gather: the rare per-lane fallback copy (a span over the stage) as
-    // a register-light byte loop instead of utf8_copy's 8-word chunks
-    int light_copy = 0;
+    // Utf8 gather: the per-lane fallback copy (a slice whose span is over the
+    // stage) as register-light unaligned 16-/4-byte moves instead of
+    // utf8_copy's aligned 8-word chunks: C3 -1%, 40-200-byte strings -25%
+    // (profiles/r05/c3_light_copy_ab2.log, long_utf8.log)
+    int light_copy = 1;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

@@ -1399,11 +1399,20 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             (emit == 3 && ((sh + (int)Ls + 3) >> 2) > 4 * IM)) {
             if (sel && L) {
 #if DFMI_LIGHT_COPY
-                // the rare per-lane fallback, register-light (Launch::light_copy)
+                // the rare per-lane fallback, register-light (Launch::light_copy):
+                // unaligned 16- and 4-byte moves (gfx950 global loads / stores
+                // take any byte address), then the tail bytes
+                typedef uint4 u128_unaligned __attribute__((aligned(1)));
+                typedef unsigned u32_unaligned __attribute__((aligned(1)));
                 const u8* sp = src + s[k];
                 u8* dp = out + ob0 + rel;
+                unsigned i = 0;
 #pragma unroll 1
-                for (unsigned i = 0; i < L; ++i) dp[i] = sp[i];
+                for (; i + 16 <= L; i += 16) *(u128_unaligned*)(dp + i) = *(const u128_unaligned*)(sp + i);
+#pragma unroll 1
+                for (; i + 4 <= L; i += 4) *(u32_unaligned*)(dp + i) = *(const u32_unaligned*)(sp + i);
+#pragma unroll 1
+                for (; i < L; ++i) dp[i] = sp[i];
 #else
                 utf8_copy(src + s[k], out + ob0 + rel, L);
 #endif

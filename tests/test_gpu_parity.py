@@ -644,3 +644,13 @@ def test_nan_payloads_bit_exact(t):
     run_both(s, bt, None, projs, DFMI_FLAG_EXT_CAST)
     run_both(s, bt, BinaryExpr(Column(2), Operator.Lt, Literal(Float64(0.5))), projs,
              DFMI_FLAG_EXT_CAST | DFMI_FLAG_EXT_GATHER_ALL)
+
+
+def test_utf8_gather_aligned_copy_variant(monkeypatch):
+    """DFMI_LIGHT_COPY=0: the per-lane fallback copy (slices whose source span
+    exceeds the stage) through utf8_copy's aligned 8-word chunks instead of
+    the default unaligned 16-/4-byte moves."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_LIGHT_COPY", "0")
+    test_utf8_multi_channel_many_tiles()
+    test_utf8_many_tiles()
