@@ -247,19 +247,20 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         // rows are selected)
         X.gather = 4;
         if (!X.utf8_outs.empty() && pred) {
-            // latency-bound gather: a 2 KiB staging arena per wave and a soft
-            // occupancy hint -- 256-thread blocks at 7 waves/SIMD give the
-            // allocator 72 VGPRs (less scratch than 64 at 8 waves): C3 gather
-            // 1.45 -> 1.36 (8 waves, 512-thread blocks) -> 1.165 ms per
-            // 1.25e8-row batch
+            // latency-bound gather: a 2 KiB staging arena per wave, 256-thread
+            // blocks and a soft occupancy hint (a shape that would spill at it
+            // is compiled again without it)
             X.arena = 128;
             X.BLOCK = 256;
-            X.waves_per_eu = 7;
             X.waves_soft = true;
             // ... and a 16-predecessor look-back window: 8 / 12 / 16 / 24 / 32
             // -> 1.121 / 1.099 / 1.108 / 1.122 / 1.141 ms per C3 batch, with
             // the light fallback copy 1.094 (profiles/r05/c3_light_copy_ab2.log)
             X.window = 16;
+            // ... which needs 61 VGPRs: 8 waves/SIMD fit without spills, 1.045
+            // -> 1.021 ms (7 waves: 72 VGPRs were the budget of utf8_copy's
+            // 8-word chunks; profiles/r05/c3_combo.log)
+            X.waves_per_eu = 8;
             // ... at high selectivity, the ring-staged gather (one loader wave)
             // when kRingDefault: same-box A/B (profiles/r05/c3_ring_ab.log) put it
             // within the box's spread of the per-wave gather (1.135-1.153 vs
