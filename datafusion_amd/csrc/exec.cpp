@@ -251,21 +251,24 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             // blocks and a soft occupancy hint (a shape that would spill at it
             // is compiled again without it)
             X.arena = 128;
-            X.BLOCK = 256;
             X.waves_soft = true;
-            // ... and a 16-predecessor look-back window: 8 / 12 / 16 / 24 / 32
-            // -> 1.121 / 1.099 / 1.108 / 1.122 / 1.141 ms per C3 batch, with
-            // the light fallback copy 1.094 (profiles/r05/c3_light_copy_ab2.log)
-            X.window = 16;
-            // ... which needs 61 VGPRs: 8 waves/SIMD fit without spills, 1.045
-            // -> 1.021 ms (7 waves: 72 VGPRs were the budget of utf8_copy's
-            // 8-word chunks; profiles/r05/c3_combo.log)
+            // ... 61 VGPRs since the light fallback copy: 8 waves/SIMD fit
+            // without spills (256-thread blocks: 1.045 -> 1.021 ms per C3
+            // batch; 7 waves and 72 VGPRs were the budget of utf8_copy's
+            // 8-word chunks; profiles/r05/c3_combo.log) ...
             X.waves_per_eu = 8;
+            // ... where 512-thread blocks (4096-row tiles: half the look-backs)
+            // beat 256 with a 12-predecessor window: 1.076 -> 1.032-1.042 ms
+            // same box (1024: 1.087-1.096; windows 4 / 8 / 12 / 32 at 512:
+            // 1.077 / 1.036-1.042 / 1.032 / 1.061; profiles/r05/c3_block_ab.log)
+            X.BLOCK = 512;
+            X.window = 12;
             // ... at high selectivity, the ring-staged gather (one loader wave)
             // when kRingDefault: same-box A/B (profiles/r05/c3_ring_ab.log) put it
             // within the box's spread of the per-wave gather (1.135-1.153 vs
             // 1.138-1.143 ms per C3 batch), so it stays a diagnostic variant
-            if (kRingDefault && B.ring_ok && X.utf8_outs.size() == 1 && !X.pred_slots.empty()) X.ring = kRingSlot;
+            if (kRingDefault && B.ring_ok && X.utf8_outs.size() == 1 && !X.pred_slots.empty())
+                X.ring = kRingSlot, X.BLOCK = 256, X.window = 16;
         } else if (pred && B.low_sel && !X.pred_slots.empty() && X.utf8_cols.empty() && n >= kSubtileMinRows) {
             // a numeric predicate that selected < 4% last time: M sub-tiles
             // share one look-back, a sparse output pass re-reads only the
@@ -291,7 +294,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_LOOKBACK_SPREAD")) X.spread = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_LOOKBACK_W")) X.window = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;
-        if (const char* e = getenv("DFMI_UTF8_PRESTAGE")) X.prestage = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_UTF8_PRESTAGE")) X.prestage = atoi(e) & 3;  // 2: not the look-back wave
         if (const char* e = getenv("DFMI_GATHER_PHASES")) X.gather_phases = atoi(e) & 1;
         if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 6;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
@@ -304,8 +307,10 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             if (X.eq_dense) X.waves_per_eu = 0;  // LDS-limited occupancy: no register hint
         }
         if (const char* e = getenv("DFMI_UTF8_RING"))  // 0: off; > 0: on (slot chunks) where it applies
-            if (pred && X.utf8_outs.size() == 1 && !X.pred_slots.empty() && X.BLOCK == 256 && X.M == 1)
+            if (pred && X.utf8_outs.size() == 1 && !X.pred_slots.empty() && X.M == 1) {
                 X.ring = atoi(e) > 1 ? atoi(e) : (atoi(e) == 1 ? kRingSlot : 0);
+                if (X.ring) X.BLOCK = 256, X.window = 16;  // a step = one 64-row slice per wave of 4
+            }
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));
         // the numeric sub-tile kernel at any size (parity tests, A/B runs)

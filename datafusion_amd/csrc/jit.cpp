@@ -1101,8 +1101,11 @@ std::string generate(const Plan& P, Launch& X) {
             // the first Utf8 output's first staging round goes out before the
             // look-back, whose wait then hides it
             const bool pre = !X.utf8_outs.empty() && (X.gather == 1 || X.gather >= 4) && X.prestage;
+            // (prestage 2: every wave but wave 0, whose look-back polls would
+            // otherwise wait behind its staging loads -- vmcnt counts in order)
             if (pre)
-                o << "  const int pre_ = dfmi::utf8_gather_prestage<K, " << (X.dbuf ? "ARENA / 2" : "ARENA") << ">(A, "
+                o << "  const int pre_ = " << (X.prestage == 2 ? "wave == 0 ? -1 : " : "")
+                  << "dfmi::utf8_gather_prestage<K, " << (X.dbuf ? "ARENA / 2" : "ARENA") << ">(A, "
                   << X.utf8_outs[0].second
                   << ", wm, us" << offs_name(X.utf8_outs[0].second) << ", ux" << offs_name(X.utf8_outs[0].second)
                   << ", G[wave], lane);\n";
