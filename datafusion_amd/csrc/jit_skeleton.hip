@@ -1402,7 +1402,7 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
                 // the rare per-lane fallback, register-light (Launch::light_copy):
                 // unaligned 16- and 4-byte moves (gfx950 global loads / stores
                 // take any byte address), then the tail bytes
-                typedef uint4 u128_unaligned __attribute__((aligned(1)));
+                typedef unsigned u128_unaligned __attribute__((ext_vector_type(4), aligned(1)));
                 typedef unsigned u32_unaligned __attribute__((aligned(1)));
                 const u8* sp = src + s[k];
                 u8* dp = out + ob0 + rel;
