@@ -296,7 +296,8 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_NT")) X.nt = atoi(e) & 3;
         if (const char* e = getenv("DFMI_UTF8_PRESTAGE")) X.prestage = atoi(e) & 3;  // 2: not the look-back wave
         if (const char* e = getenv("DFMI_GATHER_PHASES")) X.gather_phases = atoi(e) & 1;
-        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 6;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan
+        if (const char* e = getenv("DFMI_UTF8_GATHER")) X.gather = atoi(e) % 7;  // 2 = serial, 3 = two-pass, 4 = LDS image, 5 = marker scan, 6 = direct
+        if (const char* e = getenv("DFMI_UTF8_DIRECT_GROUP")) X.direct_grp = atoi(e);
         if (const char* e = getenv("DFMI_LATE_PROJ")) X.late_proj = atoi(e) & 1;
         if (const char* e = getenv("DFMI_PROJ_DENSE")) X.proj_dense = atoi(e) & 1;
         if (const char* e = getenv("DFMI_TICKET")) X.ticket = atoi(e) & 1;  // ticket-ordered tiles from the start
@@ -341,6 +342,8 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         }
     if (X.dbuf && X.arena < 128) X.dbuf = 0;  // halves of >= 64 chunks (longer spans copy per lane)
     if (X.M == 1 || X.KO == 0) X.KO = X.K;
+    if (X.direct_grp < 1) X.direct_grp = 1;
+    while (X.K % X.direct_grp || X.KO % X.direct_grp) X.direct_grp >>= 1;  // divides the slices it groups
     if (X.KO < 1 || X.KO > X.K || X.K % X.KO) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};
     if (X.K < 1 || X.K > 32 || X.BLOCK < 64 || X.BLOCK > 1024 || X.BLOCK % 64 || X.K * X.M * X.BLOCK / 64 > 256)
         throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad tile shape"};

@@ -1056,6 +1056,9 @@ std::string generate(const Plan& P, Launch& X) {
                 else if (X.gather == 0)
                     o << "  dfmi::utf8_gather_lane<BLOCK, K, NCH>(A, T, " << (j + 1) << ", " << u << ", "
                       << X.utf8_outs[j].first << ", selm, dst" << tail << "lane, wave, " << kb << ");\n";
+                else if (X.gather == 6)
+                    o << "  dfmi::utf8_gather_direct<BLOCK, K, NCH, " << X.direct_grp << ">(A, T, " << (j + 1) << ", "
+                      << u << ", " << X.utf8_outs[j].first << ", selm, dst" << tail << "lane, wave, " << kb << ");\n";
                 else
                     o << "  dfmi::utf8_gather" << (X.gather == 2 ? "_serial" : "") << "<BLOCK, K, NCH, ARENA>(A, T, "
                       << (j + 1) << ", " << u << ", " << X.utf8_outs[j].first << ", selm, wm, dst" << tail
@@ -1082,7 +1085,7 @@ std::string generate(const Plan& P, Launch& X) {
         if (X.ring)
             o << "  __shared__ dfmi::Utf8Ring<" << X.ring << "> RG;\n";
         if (X.eq_dense) o << "  __shared__ uint4 EQA[WAVES][" << X.eq_dense << "];\n";
-        if (!X.utf8_outs.empty() && X.gather && X.gather != 3 && !(X.ring && X.utf8_outs.size() == 1))
+        if (!X.utf8_outs.empty() && X.gather && X.gather != 3 && X.gather != 6 && !(X.ring && X.utf8_outs.size() == 1))
             o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA, "
               << (X.gather == 1 ? 32 : X.gather == 5 ? 72 : X.gather == 2 ? 129 : X.image) << "> G[WAVES];\n";
         o << "  const unsigned t = tile_;\n";
@@ -1360,7 +1363,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring, X.eq_dense, X.light_copy};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring, X.eq_dense, X.light_copy, X.direct_grp};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

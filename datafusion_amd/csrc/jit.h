@@ -86,6 +86,8 @@ struct Launch {
     // utf8_copy's aligned 8-word chunks: C3 -1%, 40-200-byte strings -25%
     // (profiles/r05/c3_light_copy_ab2.log, long_utf8.log)
     int light_copy = 1;
+    // gather == 6 (utf8_gather_direct): slices whose loads go out together
+    int direct_grp = 2;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)
     // sub-tiles per tile (> 1: latency-bound predicates): a block runs the
     // predicate over M sub-tiles of BLOCK * K rows, keeping only their

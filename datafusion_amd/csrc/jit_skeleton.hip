@@ -743,6 +743,113 @@ __device__ __forceinline__ void utf8_gather_lane(const Args& A, const Tile<BLOCK
     }
 }
 
+// Direct per-lane Utf8 gather (Launch::gather == 6): gfx950 global loads and
+// stores take any byte address, so each selected lane moves its string with
+// one or two unaligned 16-byte loads straight into registers and stores
+// exactly its bytes back (16 / 8 / 4 / 2 / 1-byte pieces: lanes write disjoint
+// byte ranges, no LDS image, no staging round, no edge merge). The loads of
+// GRP slices go out together before any of their stores. A 16-byte load may
+// read past the string, never past the column's last byte (offs[n_rows]);
+// a lane whose string is longer than 32 bytes or ends within 32 bytes of
+// that copies with the light per-lane loop.
+typedef unsigned v4u_ua __attribute__((ext_vector_type(4), aligned(1)));
+typedef unsigned v2u_ua __attribute__((ext_vector_type(2), aligned(1)));
+typedef unsigned u32_ua __attribute__((aligned(1)));
+typedef unsigned short u16_ua __attribute__((aligned(1)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+
+// bytes [0, L) (1 <= L <= 32) of the 32-byte register string {x0, x1} to dst
+__device__ __forceinline__ void store_exact32(u8* d, v4u x0, v4u x1, unsigned L) {
+    v4u a = x0;
+    if (L >= 16) {
+        *(v4u_ua*)d = x0;
+        d += 16;
+        a = x1;
+    }
+    const unsigned r = L >= 16 ? L - 16 : L;  // 0..16
+    if (r == 16) {
+        *(v4u_ua*)d = a;
+        return;
+    }
+    unsigned w0 = a.x, w1 = a.y;
+    if (r & 8) {
+        *(v2u_ua*)d = (v2u){a.x, a.y};
+        d += 8;
+        w0 = a.z;
+        w1 = a.w;
+    }
+    if (r & 4) {
+        *(u32_ua*)d = w0;
+        d += 4;
+        w0 = w1;
+    }
+    if (r & 2) {
+        *(u16_ua*)d = (unsigned short)w0;
+        d += 2;
+        w0 >>= 16;
+    }
+    if (r & 1) *d = (u8)w0;
+}
+
+__device__ __forceinline__ void light_copy(const u8* sp, u8* dp, unsigned L) {
+    unsigned i = 0;
+#pragma unroll 1
+    for (; i + 16 <= L; i += 16) *(v4u_ua*)(dp + i) = *(const v4u_ua*)(sp + i);
+#pragma unroll 1
+    for (; i + 4 <= L; i += 4) *(u32_ua*)(dp + i) = *(const u32_ua*)(sp + i);
+#pragma unroll 1
+    for (; i < L; ++i) dp[i] = sp[i];
+}
+
+template <int BLOCK, int K, int NCH, int GRP, int KT = K>
+__device__ __forceinline__ void utf8_gather_direct(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
+                                                   unsigned selm, const unsigned (&dst)[K], const int (&s)[K],
+                                                   const int (&nx)[K], int lane, int wave, int kb = 0) {
+    static_assert(K % GRP == 0, "slices per group divide the tile's slices");
+    constexpr int WAVES = BLOCK / 64;
+    const u64 bpre = T.prefix[ch];
+    const i64 obase = (i64)T.prefix[0];
+    const u8* src = A.bytes[u];
+    u8* out = A.out_data[o];
+    const int endb = A.offs[u][A.n_rows];  // the column's last byte + 1 (uniform)
+#pragma unroll
+    for (int g = 0; g < K; g += GRP) {
+        v4u q0[GRP], q1[GRP];
+        u64 ob[GRP];
+        unsigned Lg[GRP];
+        bool fast[GRP];
+#pragma unroll
+        for (int j = 0; j < GRP; ++j) {
+            const int k = g + j;
+            const bool sel = (selm >> k) & 1;
+            const int e = utf8_end(s[k], nx[k], lane);  // every lane (DPP)
+            const unsigned L = sel ? (unsigned)(e - s[k]) : 0u;
+            const unsigned incl = wave_incl_scan32(L, lane);
+            ob[j] = bpre + T.excl[ch][(kb + k) * WAVES + wave] + (incl - L);
+            Lg[j] = L;
+            if (sel) A.out_offs[o][obase + dst[k]] = (int)ob[j];
+            fast[j] = L > 0 && L <= 32 && s[k] + 32 <= endb;
+            if (fast[j]) {
+                q0[j] = *(const v4u_ua*)(src + s[k]);
+                if (L > 16) q1[j] = *(const v4u_ua*)(src + s[k] + 16);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GRP; ++j) {
+            const int k = g + j;
+            const unsigned L = Lg[j];
+            if (L == 0) continue;
+            if ((i64)(ob[j] + L) > A.out_cap[o]) {
+                report_err(A.err, 0, 0, ERRK_CAPACITY);
+                continue;
+            }
+            if (fast[j]) store_exact32(out + ob[j], q0[j], q1[j], L);
+            else light_copy(src + s[k], out + ob[j], L);
+        }
+    }
+}
+
 // LDS staging of one wave's Utf8 gather.
 constexpr int kStageChunks = 128;  // 16-byte source chunks of one slice's span: 2 KiB (longer: per-lane copy)
 template <int ARENA = kStageChunks, int DST = kStageChunks + 1>
@@ -1400,19 +1507,8 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
             if (sel && L) {
 #if DFMI_LIGHT_COPY
                 // the rare per-lane fallback, register-light (Launch::light_copy):
-                // unaligned 16- and 4-byte moves (gfx950 global loads / stores
-                // take any byte address), then the tail bytes
-                typedef unsigned u128_unaligned __attribute__((ext_vector_type(4), aligned(1)));
-                typedef unsigned u32_unaligned __attribute__((aligned(1)));
-                const u8* sp = src + s[k];
-                u8* dp = out + ob0 + rel;
-                unsigned i = 0;
-#pragma unroll 1
-                for (; i + 16 <= L; i += 16) *(u128_unaligned*)(dp + i) = *(const u128_unaligned*)(sp + i);
-#pragma unroll 1
-                for (; i + 4 <= L; i += 4) *(u32_unaligned*)(dp + i) = *(const u32_unaligned*)(sp + i);
-#pragma unroll 1
-                for (; i < L; ++i) dp[i] = sp[i];
+                // unaligned 16- and 4-byte moves, then the tail bytes
+                light_copy(src + s[k], out + ob0 + rel, L);
 #else
                 utf8_copy(src + s[k], out + ob0 + rel, L);
 #endif

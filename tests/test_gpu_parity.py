@@ -429,17 +429,21 @@ def test_utf8_equality_dense_variant(monkeypatch, chunks):
     test_utf8_many_tiles()
 
 
-@pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q", "4w", "4wd"])
+@pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q", "4w", "4wd", "6", "6g1", "6g4"])
 def test_utf8_gather_variants(monkeypatch, variant):
     """The Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG: 3 = two
     passes -- offsets + source starts in the query kernel, bytes by
     k_utf8_copy_rows --, 2 = one staged slice per round trip, 0 = per-lane
     copy, 4 = slices assembled in an LDS image, 1 = output words' strings by
-    binary search, 5 = by marker scan; p: first staging round before the
+    binary search, 5 = by marker scan, 6 = per-lane unaligned 16-byte loads and
+    exact-length stores (g: slices per load group); p: first staging round before the
     look-back; d: double-buffered staging; q: slices' images in pairs; w: the
     image stored in 16-byte chunks) against
     the oracle on the Utf8 parity cases above."""
-    plain = variant in ("3", "4")  # the defaults' multi-channel case runs for these (suffixed: diagnostics)
+    plain = variant in ("3", "4") or variant.startswith("6")  # the multi-channel case runs for these
+    if "g" in variant:  # direct gather: slices whose loads go out together
+        variant, grp = variant.split("g")
+        monkeypatch.setenv("DFMI_UTF8_DIRECT_GROUP", grp)
     if variant.endswith("p"):
         monkeypatch.setenv("DFMI_UTF8_PRESTAGE", "1")
         variant = variant[:-1]
