@@ -52,6 +52,7 @@ struct Built {
     int64_t n_tiles = 0;
     bool low_sel = false;  // in: this query shape selected few rows last time (dfmi_context::sel_hint)
     bool ring_ok = false;  // in: ... selected many rows with short Utf8 strings (the ring-staged gather)
+    bool long_utf8 = false;  // in: ... selected long Utf8 strings (the long per-lane fallback copy)
 };
 
 // The ring-staged Utf8 gather stages every byte of a 256-row step (not only
@@ -62,6 +63,7 @@ struct Built {
 constexpr int kRingSlot = 256;
 constexpr double kRingSel = 0.15;
 constexpr double kRingLen = 14.5;
+constexpr double kLongLen = 24.0;  // selected Utf8 bytes per row from which slices tend to overflow the 2 KiB stage
 constexpr bool kRingDefault = false;
 
 // A numeric predicate over a large batch that selects few rows runs the
@@ -263,6 +265,11 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             // 1.077 / 1.036-1.042 / 1.032 / 1.061; profiles/r05/c3_block_ab.log)
             X.BLOCK = 512;
             X.window = 12;
+            // ... and where the last large batch selected long strings (slices
+            // over the stage), the per-lane fallback with 64 bytes in flight
+            // and no occupancy hint (81 VGPRs): 40-200-byte strings 1.29 ->
+            // 0.79 ms per 1e7 rows (profiles/r05/long_utf8_copy.log)
+            if (B.long_utf8) X.long_copy = 1, X.waves_per_eu = 0;
             // ... at high selectivity, the ring-staged gather (one loader wave)
             // when kRingDefault: same-box A/B (profiles/r05/c3_ring_ab.log) put it
             // within the box's spread of the per-wave gather (1.135-1.153 vs
@@ -303,6 +310,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_TICKET")) X.ticket = atoi(e) & 1;  // ticket-ordered tiles from the start
         if (const char* e = getenv("DFMI_UTF8_EARLY")) X.early = atoi(e) & 1;
         if (const char* e = getenv("DFMI_LIGHT_COPY")) X.light_copy = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_LONG_COPY")) X.long_copy = atoi(e) & 1;
         if (const char* e = getenv("DFMI_UTF8_EQ_DENSE")) {  // chunks of the per-wave arena (dense equality A/B)
             X.eq_dense = std::max(0, std::min(1024, atoi(e)));
             if (X.eq_dense) X.waves_per_eu = 0;  // LDS-limited occupancy: no register hint
@@ -515,6 +523,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             const auto lt = ctx->utf8_len_hint.find(hint_key);
             B.ring_ok = it != ctx->sel_hint.end() && it->second >= kRingSel && lt != ctx->utf8_len_hint.end() &&
                         lt->second <= kRingLen;
+            B.long_utf8 = lt != ctx->utf8_len_hint.end() && lt->second >= kLongLen;
         }
         build_plan(pred, projs, np, in, outs, flags, B);
         if (ctx->shared) B.X.ticket = 1;  // shared GPU: ticket-ordered tiles from the start

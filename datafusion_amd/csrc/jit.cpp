@@ -1305,7 +1305,8 @@ std::string generate(const Plan& P, Launch& X) {
     // as its own kernel and a skeleton change renames every kernel (a
     // committed profile never matches code it did not measure)
     std::string body = o.str();
-    const std::string prefix = X.light_copy ? "#define DFMI_LIGHT_COPY 1\n" : "";
+    const std::string prefix = std::string(X.light_copy ? "#define DFMI_LIGHT_COPY 1\n" : "") +
+                               (X.long_copy ? "#define DFMI_LONG_COPY 1\n" : "");
     uint64_t h = 1469598103934665603ull;  // FNV-1a
     for (const std::string* part : {&prefix, &skeleton_text(), (const std::string*)&body})
         for (unsigned char ch : *part) h = (h ^ ch) * 1099511628211ull;
@@ -1363,7 +1364,7 @@ std::string shape_key(int device, const Plan& P, const Launch& X) {
         put(k, (char)os.nullable);
     }
     const int tile[] = {X.K,  X.BLOCK,  X.waves_per_eu, X.R,     X.sleep,          X.spread,
-                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring, X.eq_dense, X.light_copy, X.direct_grp};
+                        X.window, X.nt, X.gather,       X.late_proj, X.arena, (int)X.batched, X.M, X.KO, X.prestage, X.prefetch, X.gather_phases, X.image, X.dbuf, X.sparse, X.pairs, X.st16, X.proj_dense, X.hdr_out, X.ticket, X.early, X.ring, X.eq_dense, X.light_copy, X.direct_grp, X.long_copy};
     k.append((const char*)tile, sizeof tile);
     for (int c : X.num_cols) {
         put(k, c);

@@ -86,6 +86,10 @@ struct Launch {
     // utf8_copy's aligned 8-word chunks: C3 -1%, 40-200-byte strings -25%
     // (profiles/r05/c3_light_copy_ab2.log, long_utf8.log)
     int light_copy = 1;
+    // Utf8 gather's per-lane fallback for long strings (long_copy): 64 bytes
+    // in flight per lane (exec.cpp: the query's last large batch selected
+    // strings of >= kLongLen bytes on average)
+    int long_copy = 0;
     // gather == 6 (utf8_gather_direct): slices whose loads go out together
     int direct_grp = 2;
     int proj_dense = 0;  // projection-only columns loaded for every row with the predicate's columns (not lane-masked)

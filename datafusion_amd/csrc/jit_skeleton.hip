@@ -25,6 +25,9 @@ typedef unsigned u32;
 #ifndef DFMI_LIGHT_COPY
 #define DFMI_LIGHT_COPY 0
 #endif
+#ifndef DFMI_LONG_COPY
+#define DFMI_LONG_COPY 0
+#endif
 namespace dfmi {
 
 constexpr int kArgCols = 16;   // numeric / Boolean input columns
@@ -802,6 +805,43 @@ __device__ __forceinline__ void light_copy(const u8* sp, u8* dp, unsigned L) {
     for (; i < L; ++i) dp[i] = sp[i];
 }
 
+// The per-lane copy for long strings (Launch::long_copy, chosen when the
+// query's last large batch selected strings of >= kLongLen bytes on average,
+// whose slices overflow the stage): 64 bytes per round -- four unaligned
+// 16-byte loads in flight, then their stores -- and the last < 64 bytes as
+// up to four loads and exact-length stores; a load never reads past the
+// column's last byte (endb = offs[n_rows]), the light loop covers that edge.
+__device__ __forceinline__ void long_copy(const u8* src, int s, u8* dp, unsigned L, int endb) {
+    const u8* sp = src + s;
+    unsigned i = 0;
+#pragma unroll 1
+    for (; i + 64 <= L; i += 64) {
+        const v4u a = *(const v4u_ua*)(sp + i), b = *(const v4u_ua*)(sp + i + 16);
+        const v4u c = *(const v4u_ua*)(sp + i + 32), d = *(const v4u_ua*)(sp + i + 48);
+        *(v4u_ua*)(dp + i) = a;
+        *(v4u_ua*)(dp + i + 16) = b;
+        *(v4u_ua*)(dp + i + 32) = c;
+        *(v4u_ua*)(dp + i + 48) = d;
+    }
+    const unsigned r = L - i;  // < 64
+    if (!r) return;
+    if ((i64)s + i + ((r + 15) & ~15u) > (i64)endb) {
+        light_copy(sp + i, dp + i, r);
+        return;
+    }
+    v4u c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (16u * j < r) c[j] = *(const v4u_ua*)(sp + i + 16 * j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (16u * j < r) {
+            const unsigned rem = r - 16u * j;
+            if (rem >= 16) *(v4u_ua*)(dp + i + 16 * j) = c[j];
+            else store_exact32(dp + i + 16 * j, c[j], c[j], rem);
+        }
+}
+
 template <int BLOCK, int K, int NCH, int GRP, int KT = K>
 __device__ __forceinline__ void utf8_gather_direct(const Args& A, const Tile<BLOCK, KT, NCH>& T, int ch, int u, int o,
                                                    unsigned selm, const unsigned (&dst)[K], const int (&s)[K],
@@ -1505,7 +1545,10 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         if (nch > scap || ((emit == 1 || emit == 4) && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST) ||
             (emit == 3 && ((sh + (int)Ls + 3) >> 2) > 4 * IM)) {
             if (sel && L) {
-#if DFMI_LIGHT_COPY
+#if DFMI_LONG_COPY
+                // long strings (Launch::long_copy): 64 bytes in flight per lane
+                long_copy(src, s[k], out + ob0 + rel, L, A.offs[u][A.n_rows]);
+#elif DFMI_LIGHT_COPY
                 // the rare per-lane fallback, register-light (Launch::light_copy):
                 // unaligned 16- and 4-byte moves, then the tail bytes
                 light_copy(src + s[k], out + ob0 + rel, L);

@@ -658,3 +658,49 @@ def test_utf8_gather_aligned_copy_variant(monkeypatch):
     monkeypatch.setenv("DFMI_LIGHT_COPY", "0")
     test_utf8_multi_channel_many_tiles()
     test_utf8_many_tiles()
+
+
+def test_utf8_long_copy_variant(monkeypatch):
+    """DFMI_LONG_COPY=1: the per-lane fallback for slices over the stage with
+    64 bytes in flight per lane (four unaligned 16-byte loads, then exact-length
+    stores of the last < 64 bytes) on the Utf8 parity cases."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_LONG_COPY", "1")
+    test_utf8_multi_channel_many_tiles()
+    test_utf8_many_tiles()
+
+
+def test_utf8_long_strings_choose_long_copy():
+    """A large batch of long strings (30-300 bytes): its first call records
+    the selected bytes per row, the next call of the same query compiles the
+    long-copy fallback (exec.cpp kLongLen). Both against the oracle, including
+    a data buffer that ends exactly at the last string's last byte (the
+    loads past a string's end stop at offs[n_rows])."""
+    import torch
+    n = (1 << 22) + 77
+    rng = np.random.default_rng(97)
+    lens = rng.integers(30, 301, n)
+    lens[-5:] = [299, 17, 300, 64, 63]
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    assert offs[-1] < 2 ** 31
+    data = rng.integers(32, 127, int(offs[-1])).astype(np.uint8)
+    dev = engine().device
+    s_arr = Array(DataType.Utf8, n, torch.from_numpy(data).to(dev), None,
+                  torch.from_numpy(offs.astype(np.int32)).to(dev), 0)
+    v = gen_unit_f64(11, 0, 0, n)
+    s = Schema([Field("s", DataType.Utf8, False), Field("v", DataType.Float64, False)])
+    b = RecordBatch(s, [s_arr, Array.from_numpy(DataType.Float64, v).to(dev)])
+    hb = RecordBatch(s, [a.cpu() for a in b.columns])
+    pred = BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.7)))
+    p = compile_scalar_expr(None, pred, s)
+    cp = [compile_scalar_expr(None, e, s) for e in (Column(0), Column(1))]
+    ref = oracle_filter_project(s, hb, pred, [Column(0), Column(1)])
+    from datafusion_amd import _abi
+    names = []
+    for _ in range(2):
+        got = engine().filter_project(p, cp, b)
+        names.append(_abi.lib().dfmi_last_kernel_name(engine().ctx))
+        for d, (_, r) in zip(got, ref):
+            assert_same(d.cpu(), r, "long strings")
+    assert names[0] != names[1]  # the second call compiled the long-copy shape
