@@ -51,6 +51,7 @@ struct Built {
     bool any_kernel_out = false;
     int64_t n_tiles = 0;
     bool low_sel = false;  // in: this query shape selected few rows last time (dfmi_context::sel_hint)
+    bool high_sel = false;  // in: ... or at least kLowSel of them
     bool ring_ok = false;  // in: ... selected many rows with short Utf8 strings (the ring-staged gather)
     bool long_utf8 = false;  // in: ... selected long Utf8 strings (the long per-lane fallback copy)
 };
@@ -231,7 +232,10 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
     // a predicate over Utf8 columns only reads ~4 B/row of offsets: its tiles
     // are latency-bound, and 4-wave blocks keep more of them resident
     // (C3 equality 4.94 -> 4.53 ms)
-    if (pred && X.pred_slots.empty() && !X.utf8_cols.empty()) {
+    // (... unless the same query selected >= kLowSel of a large batch last
+    // time -- `s != 'w17...'`, 99.9%: the one-tile kernel with the LDS-image
+    // gather below, 2.37 -> 1.63 ms per C3 batch; profiles/r05/c3_ne_probe*.log)
+    if (pred && X.pred_slots.empty() && !X.utf8_cols.empty() && !B.high_sel) {
         X.BLOCK = 256;
         // ... and are latency-bound on the look-back: a 16-predecessor poll
         // window and 8 waves/SIMD (a few spilled registers) measured faster
@@ -520,6 +524,7 @@ extern "C" int32_t dfmi_filter_project(dfmi_context* ctx, const dfmi_program* pr
             hint_key = sel_hint_key(pred, projs, np, in, flags);
             auto it = ctx->sel_hint.find(hint_key);
             B.low_sel = it != ctx->sel_hint.end() && it->second < kLowSel;
+            B.high_sel = it != ctx->sel_hint.end() && it->second >= kLowSel;
             const auto lt = ctx->utf8_len_hint.find(hint_key);
             B.ring_ok = it != ctx->sel_hint.end() && it->second >= kRingSel && lt != ctx->utf8_len_hint.end() &&
                         lt->second <= kRingLen;

@@ -107,6 +107,7 @@ struct Launch {
                      // 3 = two passes: offsets + source starts, then k_utf8_copy_rows
                      // 4 = as 1, but each slice assembled in an LDS image (round 2's form);
                      // 5 = as 1, output words' strings found by a marker max-scan
+                     // 6 = per-lane unaligned loads into registers, exact-length stores (no LDS)
     int arena = 128; // Utf8 gather staging arena per wave, 16-byte chunks
     int pairs = 0;     // gather 4: two slices' LDS images assembled together (image = 2 x 65 chunks)
     int dbuf = 0;      // gather 1 / 4 / 5: the arena's halves double-buffer the staging (ARENA >= 256)

@@ -704,3 +704,41 @@ def test_utf8_long_strings_choose_long_copy():
         for d, (_, r) in zip(got, ref):
             assert_same(d.cpu(), r, "long strings")
     assert names[0] != names[1]  # the second call compiled the long-copy shape
+
+
+def test_utf8_only_predicate_high_selectivity_switches_to_one_tile():
+    """`s != 'w'` over a large batch selects almost every row: its first call
+    runs the sub-tile kernel (no hint yet), the next the one-tile kernel with
+    the LDS-image gather (exec.cpp: high_sel). Both against the oracle, with
+    nulls in the Utf8 column and a nullable numeric projection."""
+    import torch
+    from datafusion_amd import _abi
+    n = (1 << 22) + 5
+    rng = np.random.default_rng(5)
+    words = [bytes(rng.integers(97, 123, int(rng.integers(0, 25))).astype(np.uint8)) for _ in range(300)]
+    idx = rng.integers(0, len(words), n)
+    lens = np.array([len(w) for w in words])[idx]
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    flat = np.frombuffer(b"".join([words[i] for i in idx]), np.uint8).copy()
+    valid = rng.random(n) >= 0.03
+    dev = engine().device
+    from datafusion_amd.arrow import pack_bits
+    vb = torch.from_numpy(pack_bits(valid)).to(dev)
+    s_arr = Array(DataType.Utf8, n, torch.from_numpy(flat).to(dev), vb,
+                  torch.from_numpy(offs.astype(np.int32)).to(dev), int(n - valid.sum()))
+    s = Schema([Field("s", DataType.Utf8, True), Field("v", DataType.Float64, True)])
+    v = Array.from_numpy(DataType.Float64, gen_unit_f64(12, 0, 0, n), rng.random(n) >= 0.1)
+    b = RecordBatch(s, [s_arr, v.to(dev)])
+    hb = RecordBatch(s, [a.cpu() for a in b.columns])
+    pred = BinaryExpr(Column(0), Operator.NotEq, Literal(Utf8(words[7].decode())))
+    p = compile_scalar_expr(None, pred, s, DFMI_FLAG_EXT_UTF8_COMPARE)
+    cp = [compile_scalar_expr(None, e, s, DFMI_FLAG_EXT_UTF8_COMPARE) for e in (Column(0), Column(1))]
+    ref = oracle_filter_project(s, hb, pred, [Column(0), Column(1)], DFMI_FLAG_EXT_UTF8_COMPARE)
+    names = []
+    for _ in range(2):
+        got = engine().filter_project(p, cp, b, DFMI_FLAG_EXT_UTF8_COMPARE)
+        names.append(_abi.lib().dfmi_last_kernel_name(engine().ctx))
+        for d, (_, r) in zip(got, ref):
+            assert_same(d.cpu(), r, "s != literal")
+    assert names[0] != names[1]

@@ -49,6 +49,8 @@ def main():
         "eq": BinaryExpr(Column(0), Operator.Eq, Literal(Utf8(w17))),
         "lt": BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5))),
     }
+    if os.environ.get("C3_PROBE_NE"):  # a Utf8-only predicate selecting ~all rows (sub-tile kernel, dense output)
+        queries["ne"] = BinaryExpr(Column(0), Operator.NotEq, Literal(Utf8(w17)))
     variants = sys.argv[1:] or ["-"]
     ref = {}
     # the box runs slower for its first ~minute of GPU work (clocks / memory
