@@ -273,13 +273,19 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             // over the stage), the per-lane fallback with 64 bytes in flight
             // and no occupancy hint (81 VGPRs): 40-200-byte strings 1.29 ->
             // 0.79 ms per 1e7 rows (profiles/r05/long_utf8_copy.log)
-            if (B.long_utf8) X.long_copy = 1, X.waves_per_eu = 0;
+            if (B.long_utf8) {
+                X.long_copy = 1;
+                X.waves_per_eu = 0;
+            }
             // ... at high selectivity, the ring-staged gather (one loader wave)
             // when kRingDefault: same-box A/B (profiles/r05/c3_ring_ab.log) put it
             // within the box's spread of the per-wave gather (1.135-1.153 vs
             // 1.138-1.143 ms per C3 batch), so it stays a diagnostic variant
-            if (kRingDefault && B.ring_ok && X.utf8_outs.size() == 1 && !X.pred_slots.empty())
-                X.ring = kRingSlot, X.BLOCK = 256, X.window = 16;
+            if (kRingDefault && B.ring_ok && X.utf8_outs.size() == 1 && !X.pred_slots.empty()) {
+                X.ring = kRingSlot;
+                X.BLOCK = 256;  // a ring step = one 64-row slice per wave of 4
+                X.window = 16;
+            }
         } else if (pred && B.low_sel && !X.pred_slots.empty() && X.utf8_cols.empty() && n >= kSubtileMinRows) {
             // a numeric predicate that selected < 4% last time: M sub-tiles
             // share one look-back, a sparse output pass re-reads only the
@@ -322,7 +328,10 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_UTF8_RING"))  // 0: off; > 0: on (slot chunks) where it applies
             if (pred && X.utf8_outs.size() == 1 && !X.pred_slots.empty() && X.M == 1) {
                 X.ring = atoi(e) > 1 ? atoi(e) : (atoi(e) == 1 ? kRingSlot : 0);
-                if (X.ring) X.BLOCK = 256, X.window = 16;  // a step = one 64-row slice per wave of 4
+                if (X.ring) {  // a step = one 64-row slice per wave of 4
+                    X.BLOCK = 256;
+                    X.window = 16;
+                }
             }
         if (const char* e = getenv("DFMI_SUBTILES"))
             if (X.pred_slots.empty() && !X.utf8_cols.empty()) X.M = std::max(1, std::min(32, atoi(e)));

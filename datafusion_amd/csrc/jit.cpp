@@ -1307,8 +1307,13 @@ std::string generate(const Plan& P, Launch& X) {
     std::string body = o.str();
     const std::string prefix = std::string(X.light_copy ? "#define DFMI_LIGHT_COPY 1\n" : "") +
                                (X.long_copy ? "#define DFMI_LONG_COPY 1\n" : "");
-    uint64_t h = 1469598103934665603ull;  // FNV-1a
-    for (const std::string* part : {&prefix, &skeleton_text(), (const std::string*)&body})
+    static const uint64_t skel_h = [] {  // FNV-1a over the skeleton, once
+        uint64_t v = 1469598103934665603ull;
+        for (unsigned char ch : skeleton_text()) v = (v ^ ch) * 1099511628211ull;
+        return v;
+    }();
+    uint64_t h = skel_h;
+    for (const std::string* part : {&prefix, (const std::string*)&body})
         for (unsigned char ch : *part) h = (h ^ ch) * 1099511628211ull;
     char nm[64];
     snprintf(nm, sizeof nm, "dfmi_%s_%08llx", !P.aggs.empty() ? "agg" : (P.pred ? "filter" : "project"),

@@ -872,7 +872,7 @@ __device__ __forceinline__ void utf8_gather_direct(const Args& A, const Tile<BLO
             fast[j] = L > 0 && L <= 32 && s[k] + 32 <= endb;
             if (fast[j]) {
                 q0[j] = *(const v4u_ua*)(src + s[k]);
-                if (L > 16) q1[j] = *(const v4u_ua*)(src + s[k] + 16);
+                q1[j] = L > 16 ? *(const v4u_ua*)(src + s[k] + 16) : q0[j];
             }
         }
 #pragma unroll
