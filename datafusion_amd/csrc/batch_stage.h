@@ -64,11 +64,17 @@ struct CallProf {
         ph[i] += std::chrono::duration<double, std::micro>(u - t).count();
         t = u;
     }
+    // DFMI_CALL_PROFILE=N: the mean phase times of every N calls (N < 1: 1000)
+    const long every = [] {
+        const char* e = getenv("DFMI_CALL_PROFILE");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? v : 1000L;
+    }();
     void done() {
-        if (!on || ++n % 1000) return;
+        if (!on || ++n % every) return;
         fprintf(stderr, "dfmi call profile %s (us/call):", name);
         for (double& x : ph) {
-            fprintf(stderr, " %.2f", x / 1000);
+            fprintf(stderr, " %.2f", x / (double)every);
             x = 0;
         }
         fprintf(stderr, "\n");

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -1634,6 +1635,16 @@ extern "C" int32_t dfmi_filter_project_host_batches_into(dfmi_context* ctx, cons
                 blk_dev = device_address(blk);
             else
                 (void)hipGetLastError();
+        }
+        if (prof.on && !blk_dev) {  // diagnostics: a pageable caller block costs a copy of the outputs
+            static std::atomic<int> said{0};
+            if (said++ < 4) {
+                hipPointerAttribute_t pa{};
+                const hipError_t pe = hipPointerGetAttributes(&pa, blk);
+                (void)hipGetLastError();
+                fprintf(stderr, "dfmi host_batches_into: caller block %p not pinned (attr rc %d type %d), %zu bytes\n",
+                        (void*)blk, (int)pe, (int)pa.type, Lo.OB);
+            }
         }
         std::vector<dfmi_out_column> douts;
         dfmi_error e2{};
