@@ -33,7 +33,7 @@ from datafusion_amd.arrow import Field, Schema  # noqa: E402
 from datafusion_amd.execution.engine import engine  # noqa: E402
 from datafusion_amd.execution.expression import compile_scalar_expr  # noqa: E402
 from datafusion_amd.execution.shard import exchange_counts  # noqa: E402
-from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Float64, Literal, Operator  # noqa: E402
+from datafusion_amd.logicalplan import BinaryExpr, Column, DataType, Float64, Int64, Literal, Operator  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md "Chip-level parameters"
 COPY_CEILING_GBS = 6290.0  # measured read+write copy ceiling, MI355X_MICROARCH.md:36
@@ -64,10 +64,11 @@ class FusedStep:
     RCCL all_gather of placement records (the path a Rust caller of
     Relation::next takes on each GPU, relation.rs:27-32)."""
 
-    def __init__(self, eng, schema, cols, n, pred_e, proj_e, outs, comm=None):
+    def __init__(self, eng, schema, cols, n, pred_e, proj_e, outs, comm=None, flags=0):
         self.eng = eng
-        self.pred = compile_scalar_expr(None, pred_e, schema)
-        self.projs = [compile_scalar_expr(None, e, schema) for e in proj_e]
+        self.flags = flags
+        self.pred = compile_scalar_expr(None, pred_e, schema, flags)
+        self.projs = [compile_scalar_expr(None, e, schema, flags) for e in proj_e]
         nc, no = len(cols), len(proj_e)
         self.carr = (_abi.dfmi_column * nc)()
         for j, t in enumerate(cols):
@@ -89,10 +90,10 @@ class FusedStep:
     def __call__(self):
         if self.comm is None:
             rc = self.L.dfmi_filter_project(self.eng.ctx, self.pred.handle, self.progs, self.no, C.byref(self.cb),
-                                            self.outs, 0, C.byref(self.err))
+                                            self.outs, self.flags, C.byref(self.err))
         else:
             rc = self.L.dfmi_shard_filter_project(self.eng.ctx, self.comm.handle, self.pred.handle, self.progs,
-                                                  self.no, C.byref(self.cb), self.outs, 0, C.byref(self.place),
+                                                  self.no, C.byref(self.cb), self.outs, self.flags, C.byref(self.place),
                                                   C.byref(self.err))
             self.comm.placement, self.comm.outputs = self.place, self.outs
         if rc != 0:
@@ -753,6 +754,48 @@ def q6_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
             "roofline": roofline(kname, n * bpr, kms, n)}
 
 
+I64_RANGE = 1 << 20  # Int64 columns uniform in [0, 2^20): a*b+c never wraps
+
+
+def c2_i64_line(eng, dev, rank, world, steps, warmup, dist, rows, sel=0.5):
+    """The Int64 half of BASELINE.json configs[1]: the C2 query over three
+    Int64 columns (uniform in [0, 2^20), generated in HBM), `SELECT a, b, a*b+c
+    WHERE a > k AND b < m`. The reference's filter() rejects Int64 columns
+    (filter.rs:106-110), so this runs under the build's Int64-gather extension
+    (DFMI_FLAG_EXT_GATHER_ALL); parity: the prefix gate against the oracle,
+    and tests/test_gpu_parity.py::test_all_types_int64_on_gpu."""
+    from datafusion_amd.arrow import Array
+    n = rows
+    cols = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(3)]
+    err = _abi.dfmi_error()
+    for j, t in enumerate(cols):
+        rc = _abi.lib().dfmi_generate_column(eng.ctx, _abi.DFMI_GEN_I64, SEED + 7, j, rank * n, n, 0, I64_RANGE,
+                                              C.c_void_p(t.data_ptr()), C.byref(err))
+        assert rc == 0, err.message
+    schema = Schema([Field(c, DataType.Int64, False) for c in "abc"])
+    k, m = int(I64_RANGE * (1.0 - sel ** 0.5)), int(I64_RANGE * sel ** 0.5)
+    pred = BinaryExpr(BinaryExpr(Column(0), Operator.Gt, Literal(Int64(k))), Operator.And,
+                      BinaryExpr(Column(1), Operator.Lt, Literal(Int64(m))))
+    projs = [Column(0), Column(1), BinaryExpr(BinaryExpr(Column(0), Operator.Multiply, Column(1)), Operator.Plus,
+                                              Column(2))]
+    flags = _abi.DFMI_FLAG_EXT_GATHER_ALL
+    outs = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(3)]
+    torch.cuda.synchronize(dev)
+    step = FusedStep(eng, schema, cols, n, pred, projs, outs, flags=flags)
+    el, kms, selected = timed_steps(step, steps, warmup, dist, eng, dev)
+    kname = kernel_name(eng)
+    del outs, step
+    gate = prefix_gate(eng, schema, [Array(DataType.Int64, n, c.view(torch.uint8)) for c in cols], 1 << 22, pred,
+                       projs, flags)
+    s = selected / n
+    bpr = 24.0 + 24.0 * s  # as C2: a, b, c read; s * (a, b, a*b+c) written
+    return {"workload": "C2 over Int64: 1e9-row Int64 a,b,c per GPU (uniform [0, 2^20)), s=%.2f "
+                        "(Int64 gather: DFMI_FLAG_EXT_GATHER_ALL)" % sel,
+            "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4),
+            "selectivity": round(s, 5), "selected": selected, "parity_gate": gate,
+            "roofline": roofline(kname, n * bpr, kms, n)}
+
+
 def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
     """Real TPC-H Q6 (DFMI_FLAG_EXT_AGGREGATE): SELECT SUM(l_extendedprice *
     l_discount) FROM lineitem WHERE <Q6 predicate>, one fused predicate +
@@ -886,9 +929,10 @@ def _c3_batch(dev, g, n, dict_bytes, dict_off, dict_len):
 
 def c3_line(eng, dev, rank, world, steps, warmup, dist):
     """C3 (BASELINE.json configs[2]): 5e8 rows = 4 batches of 1.25e8 rows, a
-    nullable Float64 v and a Utf8 s. Two queries, each one launch per batch:
+    nullable Float64 v and a Utf8 s. Three queries, each one launch per batch:
       eq:  SELECT s, v WHERE s = <word 17> (Utf8 equality, DFMI_FLAG_EXT_UTF8_COMPARE)
       lt:  SELECT s, v WHERE v < 0.5     (nullable predicate, Utf8 offset/byte gather)
+      ne:  SELECT s, v WHERE s != <word 17> (Utf8-only predicate selecting ~all rows)
     Parity of both query shapes: tests/test_gpu_parity.py::test_utf8_gather_and_equality."""
     from datafusion_amd._abi import DFMI_FLAG_EXT_UTF8_COMPARE
     from datafusion_amd.execution.engine import column_struct
@@ -915,6 +959,9 @@ def c3_line(eng, dev, rank, world, steps, warmup, dist):
     queries = {
         "eq": (BinaryExpr(Column(0), Operator.Eq, Literal(Utf8(w17))), DFMI_FLAG_EXT_UTF8_COMPARE),
         "lt": (BinaryExpr(Column(1), Operator.Lt, Literal(Float64(0.5))), 0),
+        # a Utf8-only predicate selecting ~all rows: the one-tile kernel from the
+        # second call on (exec.cpp high_sel; the warm-up steps make that switch)
+        "ne": (BinaryExpr(Column(0), Operator.NotEq, Literal(Utf8(w17))), DFMI_FLAG_EXT_UTF8_COMPARE),
     }
     res = {}
     for qn, (pe, flags) in queries.items():
@@ -964,7 +1011,7 @@ def c3_line(eng, dev, rank, world, steps, warmup, dist):
         # kms sums the step's C3_BATCHES launches: roofline() gets the per-launch mean
         rl = roofline(kname, alg / C3_BATCHES, kms / C3_BATCHES, n, launches=C3_BATCHES)
         rl["kernel_ms_per_step"] = round(kms, 4)
-        res[qn] = {"query": "SELECT s, v WHERE " + ("s = '%s'" % w17 if qn == "eq" else "v < 0.5"),
+        res[qn] = {"query": "SELECT s, v WHERE " + {"eq": "s = '%s'" % w17, "lt": "v < 0.5", "ne": "s != '%s'" % w17}[qn],
                    "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3,
                    "kernel_ms": round(kms, 4), "selectivity": round(s, 5), "selected": selected,
                    "parity_gate": gate, "roofline": rl}
@@ -1132,8 +1179,8 @@ def main():
     ap.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
     ap.add_argument("--sel", type=float, default=0.5, help="headline selectivity")
     ap.add_argument("--sweep", default="0.01,0.5,0.99", help="selectivities also reported (first=headline if set)")
-    ap.add_argument("--extra", default="c4,q6,c3,batches",
-                    help="extra config lines (comma list: c4,q6,c3,batches,host,csv; empty = none)")
+    ap.add_argument("--extra", default="c4,q6,c2i64,c3,batches",
+                    help="extra config lines (comma list: c4,q6,c2i64,c3,batches,host,csv; empty = none)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", choices=("abi", "torch"), default=None,
                     help="N>1 exchange: the C-ABI RCCL path (dfmi_shard_filter_project, default under nccl) or "
@@ -1211,6 +1258,8 @@ def main():
             extra["c4"] = q6_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS, comm=step_comm)
         elif name == "q6":
             extra["q6"] = q6_agg_line(eng, dev, rank, world, args.steps, args.warmup, dist, Q6_ROWS, comm=step_comm)
+        elif name == "c2i64":
+            extra["c2i64"] = c2_i64_line(eng, dev, rank, world, args.steps, args.warmup, dist, n, args.sel)
         elif name == "host":
             if world == 1:
                 extra["host"] = host_line(eng, min(args.steps, 3), 1)

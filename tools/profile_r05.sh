@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 profile of every bench line on one MI355X: for each
-# run -- main (C2 s=0.5 + C4 + Q6 + C3 + batches), c2_s0.01 (+ C4: the
+# run -- main (C2 s=0.5 + C4 + Q6 + C2 Int64 + C3 + batches), c2_s0.01 (+ C4: the
 # low-selectivity sub-tile kernels), c2_s0.99 -- a
 # rocprofv3 kernel trace of the bench command, then separate FETCH_SIZE and
 # WRITE_SIZE PMC passes of the same command (MI355X_MICROARCH.md: the two do
@@ -16,7 +16,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for run in $RUNS; do
   case $run in
-    main) ARGS="--steps 10 --warmup 2 --sweep 0.5 --no-cpu --extra c4,q6,c3,batches";;
+    main) ARGS="--steps 10 --warmup 2 --sweep 0.5 --no-cpu --extra c4,q6,c2i64,c3,batches";;
     c2_s0.01) ARGS="--steps 10 --warmup 2 --sel 0.01 --sweep 0.01 --no-cpu --extra c4";;
     c2_s*) S=${run#c2_s}; ARGS="--steps 10 --warmup 2 --sel $S --sweep $S --no-cpu --extra ''";;
     *) echo "unknown run $run"; exit 2;;
