@@ -320,7 +320,7 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
         if (const char* e = getenv("DFMI_TICKET")) X.ticket = atoi(e) & 1;  // ticket-ordered tiles from the start
         if (const char* e = getenv("DFMI_UTF8_EARLY")) X.early = atoi(e) & 1;
         if (const char* e = getenv("DFMI_LIGHT_COPY")) X.light_copy = atoi(e) & 1;
-        if (const char* e = getenv("DFMI_LONG_COPY")) X.long_copy = atoi(e) & 1;
+        if (const char* e = getenv("DFMI_LONG_COPY")) X.long_copy = atoi(e) & 3;  // 1: per lane, 2: wave-cooperative
         if (const char* e = getenv("DFMI_UTF8_EQ_DENSE")) {  // chunks of the per-wave arena (dense equality A/B)
             X.eq_dense = std::max(0, std::min(1024, atoi(e)));
             if (X.eq_dense) X.waves_per_eu = 0;  // LDS-limited occupancy: no register hint

@@ -1306,7 +1306,7 @@ std::string generate(const Plan& P, Launch& X) {
     // committed profile never matches code it did not measure)
     std::string body = o.str();
     const std::string prefix = std::string(X.light_copy ? "#define DFMI_LIGHT_COPY 1\n" : "") +
-                               (X.long_copy ? "#define DFMI_LONG_COPY 1\n" : "");
+                               (X.long_copy ? "#define DFMI_LONG_COPY " + std::to_string(X.long_copy) + "\n" : "");
     static const uint64_t skel_h = [] {  // FNV-1a over the skeleton, once
         uint64_t v = 1469598103934665603ull;
         for (unsigned char ch : skeleton_text()) v = (v ^ ch) * 1099511628211ull;

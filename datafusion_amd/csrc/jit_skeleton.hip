@@ -1371,6 +1371,58 @@ __device__ __forceinline__ int utf8_gather_prestage(const Args& A, int u, const 
     return k0 < 0 ? -1 : utf8_stage_group<K, CAP>(src, wm, cs, cn, k0, G.src, lane, CAP < kStageChunks ? CAP : kStageChunks);
 }
 
+// Long strings, one slice whose source span overflows the stage
+// (Launch::long_copy == 2): the wave copies the slice's selected strings
+// itself, 8 lanes per string on consecutive 16-byte chunks -- each load and
+// store instruction covers eight 128-byte runs of source and of output
+// instead of 64 scattered lanes -- and 4 groups of 8 strings per round, their
+// loads in flight together. tab: 64 ints of LDS scratch (the slice's image,
+// unused by a slice that takes this path). A chunk that could read past the
+// column's last byte (endb) copies with the light loop.
+__device__ __forceinline__ void wave_copy_slice(const u8* src, u8* outb, int s_l, unsigned rel_l, unsigned L_l,
+                                                int lane, int endb, int* tab) {
+    const u64 m = __ballot(L_l > 0);
+    if (!m) return;
+    if (L_l > 0) tab[lane_rank(m)] = lane;
+    wave_lds_fence();
+    const int nsel = __builtin_popcountll(m);
+    const unsigned maxL = (unsigned)readlane_u(wave_incl_max32(L_l), 63);
+    constexpr int G = 4;  // groups of 8 strings per round
+    for (int q0 = 0; q0 < nsel; q0 += 8 * G) {
+        int sq[G];
+        unsigned dq[G], Lq[G];
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const int q = q0 + 8 * h + (lane >> 3);
+            const int sl = q < nsel ? tab[q] : lane;
+            sq[h] = __builtin_amdgcn_ds_bpermute(sl << 2, s_l);
+            dq[h] = (unsigned)__builtin_amdgcn_ds_bpermute(sl << 2, (int)rel_l);
+            const unsigned lq = (unsigned)__builtin_amdgcn_ds_bpermute(sl << 2, (int)L_l);
+            Lq[h] = q < nsel ? lq : 0u;
+        }
+        for (unsigned seg = 0; seg < maxL; seg += 128) {
+            const unsigned off = seg + 16u * (unsigned)(lane & 7);
+            v4u x[G];
+#pragma unroll
+            for (int h = 0; h < G; ++h)
+                if (off < Lq[h] && (i64)sq[h] + off + 16 <= (i64)endb) x[h] = *(const v4u_ua*)(src + sq[h] + off);
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                if (off >= Lq[h]) continue;
+                const unsigned rem = Lq[h] - off;
+                u8* d = outb + dq[h] + off;
+                if ((i64)sq[h] + off + 16 <= (i64)endb) {
+                    if (rem >= 16) *(v4u_ua*)d = x[h];
+                    else store_exact32(d, x[h], x[h], rem);
+                } else {
+                    light_copy(src + sq[h] + off, d, rem < 16 ? rem : 16u);
+                }
+            }
+        }
+    }
+    wave_lds_fence();  // tab: the next slice's image
+}
+
 // Copy the selected rows of Utf8 input u into output o (rebased i32
 // offsets + bytes, filter.rs:94-105), one 64-row slice at a time, the wave
 // cooperating: the source spans of consecutive slices are staged into the
@@ -1544,6 +1596,12 @@ __device__ __forceinline__ void utf8_gather(const Args& A, const Tile<BLOCK, KT,
         // a span over the stage, or (LDS image) an output over the image: each lane copies its string
         if (nch > scap || ((emit == 1 || emit == 4) && DST >= 32 && ((sh + (int)Ls + 3) >> 2) > 4 * DST) ||
             (emit == 3 && ((sh + (int)Ls + 3) >> 2) > 4 * IM)) {
+#if DFMI_LONG_COPY == 2
+            if (emit == 1) {  // (the image holds nothing between this path's slices)
+                wave_copy_slice(src, out + ob0, s[k], rel, L, lane, A.offs[u][A.n_rows], (int*)gd);
+                continue;
+            }
+#endif
             if (sel && L) {
 #if DFMI_LONG_COPY
                 // long strings (Launch::long_copy): 64 bytes in flight per lane

@@ -660,12 +660,14 @@ def test_utf8_gather_aligned_copy_variant(monkeypatch):
     test_utf8_many_tiles()
 
 
-def test_utf8_long_copy_variant(monkeypatch):
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_utf8_long_copy_variant(monkeypatch, mode):
     """DFMI_LONG_COPY=1: the per-lane fallback for slices over the stage with
     64 bytes in flight per lane (four unaligned 16-byte loads, then exact-length
-    stores of the last < 64 bytes) on the Utf8 parity cases."""
+    stores of the last < 64 bytes); 2: the wave copies such a slice's strings
+    8 lanes per string (wave_copy_slice) -- on the Utf8 parity cases."""
     monkeypatch.setenv("DFMI_DIAG", "1")
-    monkeypatch.setenv("DFMI_LONG_COPY", "1")
+    monkeypatch.setenv("DFMI_LONG_COPY", mode)
     test_utf8_multi_channel_many_tiles()
     test_utf8_many_tiles()
 
