@@ -270,6 +270,7 @@ class BlockArray(Array):
     values = _BlockBuffer("values", "_vo", "_vn")
     validity = _BlockBuffer("validity", "_bo", "_bn")
     offsets = _BlockBuffer("offsets", "_oo", "_on", torch.int32)
+    offset = 0  # a block array starts at its own slot 0 (the glue sets no instance `offset`)
 
 
 def _offsets_tensor(offs: np.ndarray, device) -> torch.Tensor:

@@ -239,20 +239,21 @@ static PyObject* block_array(PyTypeObject* cls, PyObject* block, uint64_t base, 
         if (o + len > size) len = size - o;
         return set_ll(d, ko, (long long)o) || set_ll(d, kn, (long long)len) ? -1 : 0;
     };
+    // (`offset` is BlockArray's class attribute 0; a buffer without its range
+    // keys -- offsets of a fixed-width array, validity without nulls -- reads
+    // as None through its descriptor: fewer dict entries per array)
     int bad = PyDict_SetItem(d, s_data_type, PyList_GET_ITEM(dtypes, r.type)) || set_ll(d, s_length, n) ||
-              set_ll(d, s_null_count, r.null_count) || set_ll(d, s_offset, 0) || PyDict_SetItem(d, s__blk, block);
+              set_ll(d, s_null_count, r.null_count) || PyDict_SetItem(d, s__blk, block);
     if (!bad) {
         if (r.type == 12) { /* Utf8: offsets + data */
             bad = range(r.offsets, (uint64_t)(n + 1) * 4, s__oo, s__on) ||
                   range(r.data, (uint64_t)r.data_length, s__vo, s__vn);
         } else {
             const uint64_t nb = r.type == 1 ? (uint64_t)(n + 7) / 8 : (uint64_t)n * width_of(r.type);
-            bad = PyDict_SetItem(d, s_offsets, Py_None) || range(r.values, nb, s__vo, s__vn);
+            bad = range(r.values, nb, s__vo, s__vn);
         }
     }
-    if (!bad)
-        bad = r.null_count > 0 ? range(r.validity, (uint64_t)(n + 7) / 8, s__bo, s__bn)
-                               : PyDict_SetItem(d, s_validity, Py_None);
+    if (!bad && r.null_count > 0) bad = range(r.validity, (uint64_t)(n + 7) / 8, s__bo, s__bn);
     if (bad) {
         Py_DECREF(a);
         return NULL;
