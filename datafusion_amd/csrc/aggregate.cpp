@@ -18,7 +18,9 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <string_view>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "exec_internal.h"
@@ -68,6 +70,23 @@ struct dfmi_agg_state {
         }
     };
     std::map<HKey, std::pair<uint64_t, std::vector<Partial_>>> groups;  // key -> (bits, partials + row count)
+    // the host merge's per-row lookup: a hash index over `groups` (views of
+    // the map's own keys; map nodes do not move), cleared with it
+    struct HKeyView {
+        bool null;
+        __int128 ord;
+        std::string_view s;
+        bool operator==(const HKeyView& o) const { return null == o.null && ord == o.ord && s == o.s; }
+    };
+    struct HKeyViewHash {
+        size_t operator()(const HKeyView& k) const {
+            const uint64_t lo = (uint64_t)k.ord, hi = (uint64_t)((unsigned __int128)k.ord >> 64);
+            uint64_t h = (lo ^ (hi * 0x9E3779B97F4A7C15ull) ^ (uint64_t)k.null) * 0xBF58476D1CE4E5B9ull;
+            if (!k.s.empty()) h ^= std::hash<std::string_view>{}(k.s) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+            return (size_t)(h ^ (h >> 31));
+        }
+    };
+    std::unordered_map<HKeyView, std::pair<uint64_t, std::vector<Partial_>>*, HKeyViewHash> index;
     // integer keys: the per-batch key window comes from MIN / MAX of the key
     // over the batch's selected rows (a pre-pass through this same extension)
     dfmi_aggregate* mm[2] = {nullptr, nullptr};
@@ -615,25 +634,35 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
                               hipMemcpyDeviceToHost));
     }
     for (int64_t i = 0; i < m; ++i) {
-        dfmi_agg_state::HKey hk{!valid(0, i), 0, {}};
+        dfmi_agg_state::HKeyView kv{!valid(0, i), 0, {}};
         uint64_t bits = 0;
-        if (!hk.null) {
+        if (!kv.null) {
             if (kt == DFMI_TYPE_UTF8) {
-                hk.s.assign((const char*)kbytes.data() + (koff[i] - koff[0]), (size_t)(koff[i + 1] - koff[i]));
+                kv.s = std::string_view((const char*)kbytes.data() + (koff[i] - koff[0]), (size_t)(koff[i + 1] - koff[i]));
             } else if (kt == DFMI_TYPE_BOOLEAN) {
                 bits = (hv[0][i >> 3] >> (i & 7)) & 1;
-                hk.ord = (__int128)bits;
+                kv.ord = (__int128)bits;
             } else {
                 const int w = jit::type_width(kt);
                 uint64_t raw = 0;
                 memcpy(&raw, hv[0].data() + (size_t)i * w, w);
                 bits = is_signed_type(kt) ? (uint64_t)(int64_t)narrow_int(raw, kt) : narrow_int(raw, kt);
-                hk.ord = key_ord(kt, bits);
+                kv.ord = key_ord(kt, bits);
             }
         }
-        auto it = st->groups.find(hk);
-        if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(n + 1))).first;
-        std::vector<Partial>& g = it->second.second;
+        std::pair<uint64_t, std::vector<Partial>>* entry;
+        auto ix = st->index.find(kv);
+        if (ix != st->index.end()) {
+            entry = ix->second;
+        } else {  // first row of this key in this state (or since a reset): the ordered map, then the index
+            dfmi_agg_state::HKey hk{kv.null, kv.ord, std::string(kv.s)};
+            auto it = st->groups.find(hk);
+            if (it == st->groups.end())
+                it = st->groups.emplace(std::move(hk), std::make_pair(bits, std::vector<Partial>(n + 1))).first;
+            entry = &it->second;
+            st->index.emplace(dfmi_agg_state::HKeyView{it->first.null, it->first.ord, it->first.s}, entry);
+        }
+        std::vector<Partial>& g = entry->second;
         ++g[n].count;  // the group's selected rows
         for (size_t j = 0; j < n; ++j)
             if (valid((int)j + 1, i)) host_accumulate(g[j], st->aggs[j]->fn, progs[j + 1]->type, hv[j + 1].data(), i);
@@ -843,6 +872,7 @@ extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, d
         HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
         st->failed = false;
         st->failure = dfmi_error{};
+        st->index.clear();
         st->groups.clear();
         st->win_width = -1;
         st->dirty = false;
