@@ -122,14 +122,43 @@ def profiled(kernel, run="main"):
     return max(hits, key=lambda e: e["grid"]) if hits else None
 
 
-def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
+LINE_BYTES = 128  # one memory request per touched 128-B line (profiles/r06/calib_masked/summary.txt)
+
+
+def lines_touched(mask, rows_per_line=LINE_BYTES // 8):
+    """128-B lines of an 8-B column (256-B aligned, row 0 at a line start)
+    that hold at least one selected row: what a lane-masked load of that
+    column fetches (tools/membw_masked.hip: FETCH_SIZE x 2 = 128 B x these
+    lines, exactly)."""
+    n = mask.numel()
+    full = n // rows_per_line * rows_per_line
+    c = int(mask[:full].view(-1, rows_per_line).any(1).sum().item())
+    if full < n:
+        c += int(mask[full:].any().item())
+    return c
+
+
+def moved_bytes(n, streamed_bpr, masked_cols, mask, written):
+    """The HBM bytes a filter kernel over n rows must move, counted from its
+    real selection mask: every streamed (predicate) column once, each
+    lane-masked 8-B column's 128-B lines that hold a selected row once, and
+    the writes. Re-reads (the sub-tile output pass re-loads the predicate's
+    columns for the selected rows) are counted as cache hits, i.e. not at
+    all: a lower bound, so the credited fraction is one too."""
+    return n * streamed_bpr + masked_cols * LINE_BYTES * lines_touched(mask) + written
+
+
+def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main", moved=None):
     """roofline object of one bench line. `frac` is the fraction the hardware
-    backs: the lower of the FORMULA fraction (SURVEY §8(d)'s algorithmic bytes
+    backs: the lowest of the FORMULA fraction (SURVEY §8(d)'s algorithmic bytes
     per launch over the kernel's average HIP-event time on the launch stream,
-    `formula_frac`) and the PMC fraction (the HBM bytes the committed profile
-    of the same kernel measured, `traffic_frac`, over this run's time) -- where
-    a kernel skips bytes the formula counts (masked loads, head-word compares)
-    only the moved bytes are credited. Without a PMC record, `frac` never
+    `formula_frac`), the MOVED fraction (`moved` bytes per launch, counted
+    from the selection mask by moved_bytes(): what a kernel that skips the
+    unselected lines of its masked columns has to move at the least,
+    `moved_frac`) and the PMC fraction (FETCH_SIZE x 2 + WRITE_SIZE of the
+    committed profile of the same kernel -- memory-side requests, calibrated
+    for streaming and lane-masked 8-B loads, Infinity-Cache hits included --
+    over this run's time, `traffic_frac`). Without a PMC record, `frac` never
     exceeds the measured copy ceiling (6.29 of 8 TB/s, MI355X_MICROARCH.md).
     `rocprof` names the committed profile (its box, its average time and
     fraction); the line's own box is the bench JSON's `box`."""
@@ -140,9 +169,15 @@ def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
          "launches_per_step": launches, "algorithmic_bytes_per_row": round(alg_bytes * launches / rows, 3),
          "traffic": None}
     p = profiled(kernel, run)
-    frac, basis = min(ffrac, COPY_CEILING_GBS / HBM_PEAK_GBS), "formula, capped at the copy ceiling (no PMC record)"
-    if ffrac <= COPY_CEILING_GBS / HBM_PEAK_GBS:
-        basis = "formula (no PMC record)"
+    cands = []  # (fraction, basis): the credited one is the lowest
+    if moved is not None:
+        mgbs = moved / (kms * 1e-3) / 1e9
+        r["moved_bytes_per_row"] = round(moved * launches / rows, 3)
+        r["moved_gbs"] = round(mgbs, 1)
+        r["moved_frac"] = round(mgbs / HBM_PEAK_GBS, 4)
+        cands.append((r["moved_frac"], "moved bytes (selection mask: streamed columns + touched 128-B lines of "
+                                       "masked columns + writes)"))
+    pmc = False
     if p:
         per_launch_alg = alg_bytes  # alg_bytes and kms are per launch
         avg_ms = p["avg_ns"] * 1e-6
@@ -151,6 +186,7 @@ def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
                         "formula_frac": round(per_launch_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "vgpr": p["vgpr"], "sgpr": p["sgpr"], "scratch": p["scratch"], "lds": p["lds"]}
         if "traffic_bytes" in p:
+            pmc = True
             r["traffic"] = round(p["traffic_bytes"])
             r["traffic_bytes_per_row"] = round(p["traffic_bytes"] * launches / rows, 3)
             # the profile's bytes per launch over THIS run's kernel time
@@ -158,10 +194,12 @@ def roofline(kernel, alg_bytes, kms, rows, launches=1, run="main"):
             r["traffic_gbs"] = round(tgbs, 1)
             r["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
             r["rocprof"]["traffic_frac"] = round(p["traffic_bytes"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-            if r["traffic_frac"] < ffrac:
-                frac, basis = r["traffic_frac"], "PMC HBM bytes (the kernel moves fewer bytes than the formula counts)"
-            else:
-                frac, basis = ffrac, "formula (PMC bytes >= formula bytes)"
+            cands.append((r["traffic_frac"], "PMC request bytes (FETCH_SIZE x 2 + WRITE_SIZE of the committed profile)"))
+    if pmc or moved is not None or ffrac <= COPY_CEILING_GBS / HBM_PEAK_GBS:
+        cands.append((ffrac, "formula (SURVEY 8(d) algorithmic bytes)"))
+    else:
+        cands.append((COPY_CEILING_GBS / HBM_PEAK_GBS, "formula, capped at the copy ceiling (no PMC record)"))
+    frac, basis = min(cands)
     r["frac"] = round(frac, 4)
     r["frac_basis"] = basis
     r["formula_exceeds_ceiling"] = ach > COPY_CEILING_GBS
@@ -747,11 +785,13 @@ def q6_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
                        pred, projs)
     s = selected / n
     bpr = 32.0 + 8.0 * s  # 4 Float64 inputs, s * 8 B output
+    # quantity, discount, shipdate streamed by the predicate; extendedprice lane-masked
+    moved = moved_bytes(n, 24, 1, q6_mask(cols), 8 * selected)
     return {"workload": "C4: TPC-H SF100 lineitem Q6-style predicate, 600037902 rows per GPU, "
                         "SELECT l_extendedprice*l_discount (Float64)",
             "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4),
             "selectivity": round(s, 5), "selected": selected, "parity_gate": gate,
-            "roofline": roofline(kname, n * bpr, kms, n)}
+            "roofline": roofline(kname, n * bpr, kms, n, moved=moved)}
 
 
 I64_RANGE = 1 << 20  # Int64 columns uniform in [0, 2^20): a*b+c never wraps
@@ -789,11 +829,12 @@ def c2_i64_line(eng, dev, rank, world, steps, warmup, dist, rows, sel=0.5):
                        projs, flags)
     s = selected / n
     bpr = 24.0 + 24.0 * s  # as C2: a, b, c read; s * (a, b, a*b+c) written
+    moved = moved_bytes(n, 16, 1, (cols[0] > k) & (cols[1] < m), 24 * selected)
     return {"workload": "C2 over Int64: 1e9-row Int64 a,b,c per GPU (uniform [0, 2^20)), s=%.2f "
                         "(Int64 gather: DFMI_FLAG_EXT_GATHER_ALL)" % sel,
             "rows_per_s": n * world * steps / el, "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4),
             "selectivity": round(s, 5), "selected": selected, "parity_gate": gate,
-            "roofline": roofline(kname, n * bpr, kms, n)}
+            "roofline": roofline(kname, n * bpr, kms, n, moved=moved)}
 
 
 def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
@@ -845,12 +886,13 @@ def q6_agg_line(eng, dev, rank, world, steps, warmup, dist, rows, comm=None):
     gate = {"rows": m, "sum_bits_equal": bool(dv.bits == rv.bits and dv.count == rv.count), "count": int(rv.count)}
     s = selected / (n * world)  # the merged count covers every rank's rows
     bpr = 32.0  # 4 Float64 inputs; the output is one value
+    moved = moved_bytes(n, 24, 1, q6_mask(cols), 0)  # the SUM argument's price column lane-masked
     v = res["v"]
     return {"workload": "C4 real Q6: SELECT SUM(l_extendedprice*l_discount) FROM lineitem WHERE <Q6>, 600037902 "
                         "rows per GPU, exact Float64 sum", "rows_per_s": n * world * steps / el,
             "ms_per_step": el / steps * 1e3, "kernel_ms": round(kms, 4), "selectivity": round(s, 5),
             "sum": float(np.array([v.bits], dtype=np.uint64).view(np.float64)[0]), "parity_gate": gate,
-            "roofline": roofline(kname, n * bpr, kms, n)}
+            "roofline": roofline(kname, n * bpr, kms, n, moved=moved)}
 
 
 def q6_table(dev, n, seed):
@@ -881,6 +923,13 @@ def q6_query():
                                  BinaryExpr(Column(2), Operator.LtEq, Literal(Float64(0.07)))), Operator.And,
                       lt(0, 24.0))
     return pred, [BinaryExpr(Column(1), Operator.Multiply, Column(2))]
+
+
+def q6_mask(cols):
+    """q6_query()'s predicate over q6_table()'s columns, with torch (the
+    selection mask moved_bytes() counts lines from)."""
+    qty, _, disc, ship = cols
+    return (ship >= 8766.0) & (ship < 9131.0) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24.0)
 
 
 C3_ROWS = 500_000_000
@@ -1233,7 +1282,9 @@ def main():
         s_real = selected / n
         bytes_per_row = 24.0 + 24.0 * s_real  # a,b,c read; s*(a,b,a*b+c) written
         kname = kernel_name(eng)
-        rl = roofline(kname, n * bytes_per_row, kms, n, run="main" if sel == 0.5 else "c2_s%.2f" % sel)
+        k_, m_ = 1.0 - sel ** 0.5, sel ** 0.5  # query(sel)'s literals
+        moved = moved_bytes(n, 16, 1, (cols[0] > k_) & (cols[1] < m_), 24 * selected)  # a, b streamed; c masked
+        rl = roofline(kname, n * bytes_per_row, kms, n, run="main" if sel == 0.5 else "c2_s%.2f" % sel, moved=moved)
         results[sel] = dict(el=el, kms=kms, selected=selected, s=s_real, rl=rl, bpr=bytes_per_row)
     del outs, step
     torch.cuda.empty_cache()
