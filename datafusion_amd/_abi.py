@@ -129,7 +129,7 @@ class dfmi_agg_value(C.Structure):
 
 
 # include/dfmi.h's DFMI_ABI_VERSION: lib() refuses a library built from another header
-DFMI_ABI_VERSION = 2
+DFMI_ABI_VERSION = 3
 
 # Every symbol include/dfmi.h declares (checked by the CPU test suite).
 EXPORTED = [
@@ -174,11 +174,15 @@ EXPORTED = [
     "dfmi_agg_merge_partials",
     "dfmi_agg_state_reset",
     "dfmi_agg_state_create_grouped",
+    "dfmi_agg_state_create_grouped_multi",
+    "dfmi_agg_state_num_keys",
     "dfmi_agg_state_finish_grouped",
     "dfmi_agg_state_group_keys_utf8",
+    "dfmi_agg_state_group_keys_utf8_part",
     "dfmi_agg_state_grouped_partial_bytes",
     "dfmi_agg_state_grouped_partial",
     "dfmi_agg_merge_grouped_partials",
+    "dfmi_agg_merge_grouped_partials_keys_utf8",
     "dfmi_shard_unique_id",
     "dfmi_shard_comm_init",
     "dfmi_shard_comm_destroy",
@@ -356,6 +360,18 @@ def lib() -> C.CDLL:
     L.dfmi_agg_state_group_keys_utf8.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, P(C.c_int64),
                                                  P(dfmi_error)]
     L.dfmi_agg_state_group_keys_utf8.restype = C.c_int32
+    L.dfmi_agg_state_create_grouped_multi.argtypes = [C.c_void_p, P(C.c_void_p), C.c_int32, P(C.c_void_p), C.c_int32,
+                                                      P(C.c_void_p), P(dfmi_error)]
+    L.dfmi_agg_state_create_grouped_multi.restype = C.c_int32
+    L.dfmi_agg_state_num_keys.argtypes = [C.c_void_p]
+    L.dfmi_agg_state_num_keys.restype = C.c_int32
+    L.dfmi_agg_state_group_keys_utf8_part.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                                      C.c_int64, P(C.c_int64), P(dfmi_error)]
+    L.dfmi_agg_state_group_keys_utf8_part.restype = C.c_int32
+    L.dfmi_agg_merge_grouped_partials_keys_utf8.argtypes = [P(C.c_void_p), C.c_int32, P(C.c_void_p), P(C.c_int64),
+                                                            C.c_int32, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                                            C.c_int64, P(C.c_int64), P(dfmi_error)]
+    L.dfmi_agg_merge_grouped_partials_keys_utf8.restype = C.c_int32
     L.dfmi_agg_partial_bytes.argtypes = [C.c_void_p]
     L.dfmi_agg_partial_bytes.restype = C.c_int64
     L.dfmi_agg_state_partial.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(dfmi_error)]

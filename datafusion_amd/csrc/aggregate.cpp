@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "exec_internal.h"
+#include "groupby.h"
 #include "slice.h"
 #include "jit_skeleton.hip"
 
@@ -44,6 +45,59 @@ struct dfmi_aggregate {
     dfmi_program arg;  // compile_expr's compiled argument (a copy: same uid, same kernels)
 };
 
+// GROUP BY keys on the host: one part per key expression, ordered
+// lexicographically, each part with its null last (aggregate.cpp emit order;
+// the oracle's group_key). A non-null part orders by `ord` (key_ord: integers
+// numerically, Boolean false < true, floats by IEEE 754 totalOrder), then by
+// its bytes (Utf8: bytewise, a shorter prefix first).
+struct KeyPart {
+    bool null = false;
+    __int128 ord = 0;
+    uint64_t bits = 0;  // Boolean 0/1, integers sign/zero-extended, float bits
+    std::string s;      // Utf8
+};
+struct HKey {
+    std::vector<KeyPart> p;
+    bool operator<(const HKey& o) const {
+        for (size_t i = 0; i < p.size(); ++i) {
+            const KeyPart &a = p[i], &b = o.p[i];
+            if (a.null != b.null) return !a.null;
+            if (a.null) continue;
+            if (a.ord != b.ord) return a.ord < b.ord;
+            if (a.s != b.s) return a.s < b.s;
+        }
+        return false;
+    }
+};
+using GroupMap = std::map<HKey, std::vector<Partial_>>;  // key -> partials + the group's row count
+
+// The device hash table of a grouped state (groupby.h; kernels in groupby.hip).
+struct HashDev {
+    dfmi::gb::Table t{};
+    uint64_t cap = 0;                 // slots
+    dfmi::gb::Hdr* hdr = nullptr;     // device counters
+    dfmi::gb::Hdr* hh = nullptr;      // pinned host copy
+    uint8_t* arena = nullptr;         // Utf8 key bytes
+    uint64_t arena_cap = 0;
+    unsigned long long* acc = nullptr;      // [acc_cap][words] group records
+    uint64_t acc_cap = 0;
+    unsigned long long* pattern = nullptr;  // one zero-state record (device)
+    std::vector<uint64_t> hpattern;
+    int words = 0;
+    std::vector<int> off, foff;       // per aggregate: record offset; float SUMs: digit offsets
+    int32_t* sidx = nullptr;
+    int32_t* coll = nullptr;
+    int64_t rows_cap = 0;             // sidx / coll capacity
+    uint32_t epoch = 0;
+    uint64_t ngroups = 0;             // groups the device holds
+    uint64_t rows_since_norm = 0;     // rows added since the digits were last carry-normalised
+    struct Buf {
+        void* p = nullptr;
+        size_t cap = 0;
+    };
+    std::vector<Buf> bufs;            // the fused pass's output columns (reused across batches)
+};
+
 struct dfmi_agg_state {
     int device = 0;
     std::vector<const dfmi_aggregate*> aggs;
@@ -52,41 +106,20 @@ struct dfmi_agg_state {
     bool failed = false;      // a batch raised an error: the query has failed
     dfmi_error failure{};
     std::vector<uint64_t> init;  // the zero state (MIN keys all ones)
-    // GROUP BY extension (dfmi_agg_state_create_grouped)
+    // GROUP BY extension (dfmi_agg_state_create_grouped / _multi)
     bool grouped = false;
-    dfmi_program key;           // the key (a copy: same uid, same kernels)
-    int gslots = 0;             // slots per accumulator copy: the key window + the null slot
+    std::vector<dfmi_program> keys;  // the key expressions (copies: same uid, same kernels)
+    dfmi_program key;           // keys[0] (the window kernel's key)
+    int gslots = 0;             // window slots per accumulator copy: the key window + the null slot
     uint64_t win_base = 0;      // the window the device accumulators hold ...
     int win_width = -1;         // ... (-1: none yet)
-    bool dirty = false;         // the device accumulators hold rows
-    struct HKey {
-        bool null;
-        __int128 ord;
-        std::string s;  // Utf8 keys: the bytes (ordered bytewise)
-        bool operator<(const HKey& o) const {
-            if (null != o.null) return !null;
-            if (null) return false;
-            return ord != o.ord ? ord < o.ord : s < o.s;
-        }
-    };
-    std::map<HKey, std::pair<uint64_t, std::vector<Partial_>>> groups;  // key -> (bits, partials + row count)
-    // the host merge's per-row lookup: a hash index over `groups` (views of
-    // the map's own keys; map nodes do not move), cleared with it
-    struct HKeyView {
-        bool null;
-        __int128 ord;
-        std::string_view s;
-        bool operator==(const HKeyView& o) const { return null == o.null && ord == o.ord && s == o.s; }
-    };
-    struct HKeyViewHash {
-        size_t operator()(const HKeyView& k) const {
-            const uint64_t lo = (uint64_t)k.ord, hi = (uint64_t)((unsigned __int128)k.ord >> 64);
-            uint64_t h = (lo ^ (hi * 0x9E3779B97F4A7C15ull) ^ (uint64_t)k.null) * 0xBF58476D1CE4E5B9ull;
-            if (!k.s.empty()) h ^= std::hash<std::string_view>{}(k.s) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-            return (size_t)(h ^ (h >> 31));
-        }
-    };
-    std::unordered_map<HKeyView, std::pair<uint64_t, std::vector<Partial_>>*, HKeyViewHash> index;
+    bool dirty = false;         // the device window accumulators hold rows
+    GroupMap groups;            // merged groups (window flushes, hash-table drains, host merges)
+    // the host merge's per-row lookup: encoded key -> entry of `groups` (map
+    // nodes do not move), cleared with it
+    std::unordered_map<std::string, std::vector<Partial_>*> index;
+    std::shared_ptr<GroupMap> shown;  // groups dfmi_shard_agg_finish_grouped merged (else `groups`)
+    HashDev* hd = nullptr;            // device hash table (created on first use)
     // integer keys: the per-batch key window comes from MIN / MAX of the key
     // over the batch's selected rows (a pre-pass through this same extension)
     dfmi_aggregate* mm[2] = {nullptr, nullptr};
@@ -421,8 +454,28 @@ bool is_signed_type(int t) {
     return t == DFMI_TYPE_INT8 || t == DFMI_TYPE_INT16 || t == DFMI_TYPE_INT32 || t == DFMI_TYPE_INT64;
 }
 
-// GROUP BY: the device accumulators (window win_base / win_width) merged into
-// the host's groups, and the device state reset.
+// The group entry of key `hk` (created with n + 1 empty partials).
+std::vector<Partial>& group_entry(GroupMap& groups, HKey&& hk, size_t n) {
+    auto it = groups.find(hk);
+    if (it == groups.end()) it = groups.emplace(std::move(hk), std::vector<Partial>(n + 1)).first;
+    return it->second;
+}
+
+void merge_group(std::vector<Partial>& into, const std::vector<Partial>& parts, const dfmi_aggregate* const* aggs,
+                 size_t n) {
+    for (size_t j = 0; j < n; ++j) merge_partial(into[j], parts[j], aggs[j]->fn == DFMI_AGG_MIN);
+    into[n].count += parts[n].count;  // the hidden count: the group's selected rows
+}
+
+KeyPart fixed_part(int kt, uint64_t bits) {
+    KeyPart k;
+    k.bits = bits;
+    k.ord = key_ord(kt, bits);
+    return k;
+}
+
+// GROUP BY: the device window accumulators (win_base / win_width) merged into
+// the host's groups, and the device window state reset.
 void flush_groups(dfmi_context* ctx, dfmi_agg_state* st) {
     if (!st->dirty) return;
     const std::vector<uint64_t> h = read_acc(ctx, st);
@@ -437,22 +490,21 @@ void flush_groups(dfmi_context* ctx, dfmi_agg_state* st) {
             normalize(parts[j]);
         }
         if (parts[n].count == 0) continue;  // no row of this key in the window
-        dfmi_agg_state::HKey hk{g == st->win_width, 0, {}};
-        uint64_t bits = 0;
-        if (!hk.null) {
-            bits = st->win_base + (uint64_t)g;
-            hk.ord = key_ord(kt, bits);
+        HKey hk;
+        if (g == st->win_width) {
+            hk.p.emplace_back();
+            hk.p.back().null = true;
+        } else {
+            hk.p.push_back(fixed_part(kt, st->win_base + (uint64_t)g));
         }
-        auto it = st->groups.find(hk);
-        if (it == st->groups.end()) it = st->groups.emplace(hk, std::make_pair(bits, std::vector<Partial>(na))).first;
-        for (size_t j = 0; j < n; ++j) merge_partial(it->second.second[j], parts[j], st->aggs[j]->fn == DFMI_AGG_MIN);
-        it->second.second[n].count += parts[n].count;  // the hidden count: the group's selected rows
+        merge_group(group_entry(st->groups, std::move(hk), n), parts, st->aggs.data(), n);
     }
     HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
     st->dirty = false;
 }
 
-// ---- GROUP BY over keys wider than the device window: the host merge.
+// ---- per-row rules on the host (the host merge: diagnostics A/B, and the
+// rows of a batch whose key shares its 63-bit hash with another key's).
 // One value (row i, non-null) of aggregate `a` into p -- the per-row rules
 // of the aggregate kernels (jit.cpp generate_agg / generate_agg_grouped,
 // jit_skeleton.hip agg_key / agg_sum_flags / fsum_add), restated on the host.
@@ -538,34 +590,39 @@ void host_accumulate(Partial& p, int fn, int t, const uint8_t* vals, int64_t i) 
     }
 }
 
-// A batch whose selected keys span more than the device window: the key and
-// every argument evaluated on the device as one fused Selection + Projection
-// pass (dfmi_filter_project: projections [key, args...] -- the same
-// evaluation order, ordinals and errors as the grouped kernel), the
-// compacted columns copied back, and each row merged into its group on the
-// host with the kernels' per-row rules.
-void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in,
-                         uint32_t flags) {
-    const size_t n = st->aggs.size();
-    const int no = (int)n + 1;
+// ---- the fused evaluation pass of a grouped batch: keys then arguments,
+// compacted by the predicate (dfmi_filter_project: the reference's
+// evaluation order and first error), into the hash state's reusable device
+// buffers. Returns the selected rows; `cols` describes each output (a
+// passed-through input column, or the compacted output).
+void* hd_buf(HashDev& H, size_t i, size_t bytes) {
+    if (H.bufs.size() <= i) H.bufs.resize(i + 1);
+    HashDev::Buf& b = H.bufs[i];
+    bytes = std::max<size_t>(bytes, 64);
+    if (b.cap < bytes) {
+        if (b.p) HIP_TRY(hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+        const size_t want = bytes + bytes / 4;
+        HIP_TRY(hipMalloc(&b.p, want));
+        b.cap = want;
+    }
+    return b.p;
+}
+
+HashDev& hashdev(dfmi_context* ctx, dfmi_agg_state* st);
+
+int64_t eval_grouped(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in,
+                     uint32_t flags, std::vector<dfmi::gb::Col>& cols) {
+    HashDev& H = hashdev(ctx, st);
+    const size_t nk = st->keys.size(), n = st->aggs.size();
+    const int no = (int)(nk + n);
     const int64_t rows = in->num_rows;
     std::vector<const dfmi_program*> progs(no);
-    progs[0] = &st->key;
-    for (size_t j = 0; j < n; ++j) progs[j + 1] = &st->aggs[j]->arg;
+    for (size_t p = 0; p < nk; ++p) progs[p] = &st->keys[p];
+    for (size_t j = 0; j < n; ++j) progs[nk + j] = &st->aggs[j]->arg;
     std::vector<dfmi_out_column> outs(no);
-    std::vector<void*> dev;
-    struct Free {
-        std::vector<void*>& v;
-        ~Free() {
-            for (void* p : v) (void)hipFree(p);
-        }
-    } free_{dev};
-    auto dalloc = [&](size_t b) {
-        void* p = nullptr;
-        HIP_TRY(hipMalloc(&p, std::max<size_t>(b, 64)));
-        dev.push_back(p);
-        return p;
-    };
+    size_t bi = 0;
     for (int o = 0; o < no; ++o) {
         dfmi_out_column& c = outs[o];
         memset(&c, 0, sizeof c);
@@ -574,18 +631,21 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
             const IrNode& root = progs[o]->ir[progs[o]->root];
             size_t cap = 8;
             if (root.kind == IR_COL && root.col >= 0 && root.col < in->num_columns && in->columns[root.col].offsets) {
-                int32_t last = 0;
-                HIP_TRY(hipMemcpy(&last, in->columns[root.col].offsets + rows, 4, hipMemcpyDeviceToHost));
-                cap = std::max<size_t>(cap, (size_t)std::max(0, last));
+                int32_t ends[2] = {0, 0};
+                HIP_TRY(hipMemcpyAsync(&ends[0], in->columns[root.col].offsets, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_TRY(hipMemcpyAsync(&ends[1], in->columns[root.col].offsets + rows, 4, hipMemcpyDeviceToHost,
+                                       ctx->stream));
+                HIP_TRY(hipStreamSynchronize(ctx->stream));
+                cap = std::max<size_t>(cap, (size_t)std::max(0, ends[1] - ends[0]));
             }
-            c.offsets = (int32_t*)dalloc((size_t)(rows + 1) * 4);
-            c.data = (uint8_t*)dalloc(cap);
+            c.offsets = (int32_t*)hd_buf(H, bi++, (size_t)(rows + 1) * 4);
+            c.data = (uint8_t*)hd_buf(H, bi++, cap);
             c.data_capacity = (int64_t)cap;
         } else {
             const int w = jit::type_width(t);
-            c.values = dalloc(t == DFMI_TYPE_BOOLEAN ? (size_t)(rows + 63) / 64 * 8 : (size_t)rows * std::max(w, 1));
+            c.values = hd_buf(H, bi++, t == DFMI_TYPE_BOOLEAN ? (size_t)(rows + 63) / 64 * 8 : (size_t)rows * std::max(w, 1));
         }
-        c.validity = (uint8_t*)dalloc((size_t)(rows + 63) / 64 * 8);
+        c.validity = (uint8_t*)hd_buf(H, bi++, (size_t)(rows + 63) / 64 * 8);
     }
     dfmi_error e{};
     if (dfmi_filter_project(ctx, pred, progs.data(), no, in, outs.data(), flags, &e) != DFMI_OK) {
@@ -593,111 +653,523 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
         st->failure = e;
         throw Fail{e.code, e.message};
     }
-    // a passthrough-only pass launches nothing, and a sliced batch's shifted
-    // bitmaps (slice.cpp) are written on ctx->stream: order the synchronous
-    // null-stream copies below after them
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    const int64_t m = outs[0].length;  // selected rows
-    // host copies of values (fixed width) and validity
-    std::vector<std::vector<uint8_t>> hv(no), hb(no);
+    cols.assign(no, dfmi::gb::Col{});
     for (int o = 0; o < no; ++o) {
         const dfmi_out_column& c = outs[o];
-        const int t = progs[o]->type;
-        const dfmi_column* src = c.passthrough_column >= 0 ? &in->columns[c.passthrough_column] : nullptr;
-        const int w = jit::type_width(t);
-        const size_t vb = t == DFMI_TYPE_BOOLEAN ? (size_t)(m + 7) / 8 : (size_t)m * w;
-        if (vb && t != DFMI_TYPE_UTF8) {
-            hv[o].resize(vb);
-            HIP_TRY(hipMemcpy(hv[o].data(), src ? src->values : c.values, vb, hipMemcpyDeviceToHost));
-        }
-        const uint8_t* vsrc = src ? (src->null_count > 0 ? src->validity : nullptr) : (c.null_count > 0 ? c.validity : nullptr);
-        if (vsrc && m) {
-            hb[o].resize((size_t)(m + 7) / 8);
-            HIP_TRY(hipMemcpy(hb[o].data(), vsrc, hb[o].size(), hipMemcpyDeviceToHost));
+        dfmi::gb::Col& d = cols[o];
+        d.type = progs[o]->type;
+        d.width = d.type == DFMI_TYPE_UTF8 || d.type == DFMI_TYPE_BOOLEAN ? 0 : jit::type_width(d.type);
+        if (c.passthrough_column >= 0) {
+            const dfmi_column& src = in->columns[c.passthrough_column];
+            d.values = src.values;
+            d.offsets = src.offsets;
+            d.validity = src.null_count > 0 ? src.validity : nullptr;
+        } else {
+            d.values = d.type == DFMI_TYPE_UTF8 ? (const void*)c.data : c.values;
+            d.offsets = c.offsets;
+            d.validity = c.null_count > 0 ? c.validity : nullptr;
         }
     }
-    auto valid = [&](int o, int64_t i) { return hb[o].empty() || ((hb[o][i >> 3] >> (i & 7)) & 1); };
-    const int kt = st->key.type;
-    // a Utf8 key: its offsets and bytes (the compacted output, or -- no
-    // predicate, a Column key -- the input column itself)
-    std::vector<int32_t> koff;
-    std::vector<uint8_t> kbytes;
-    if (kt == DFMI_TYPE_UTF8 && m > 0) {
-        const dfmi_out_column& c = outs[0];
-        const dfmi_column* src = c.passthrough_column >= 0 ? &in->columns[c.passthrough_column] : nullptr;
-        koff.resize((size_t)m + 1);
-        HIP_TRY(hipMemcpy(koff.data(), src ? src->offsets : c.offsets, koff.size() * 4, hipMemcpyDeviceToHost));
-        const size_t nbytes = (size_t)std::max(0, koff[m] - koff[0]);
-        kbytes.resize(std::max<size_t>(nbytes, 1));
-        if (nbytes)
-            HIP_TRY(hipMemcpy(kbytes.data(), (src ? (const uint8_t*)src->values : c.data) + koff[0], nbytes,
-                              hipMemcpyDeviceToHost));
-    }
-    for (int64_t i = 0; i < m; ++i) {
-        dfmi_agg_state::HKeyView kv{!valid(0, i), 0, {}};
-        uint64_t bits = 0;
-        if (!kv.null) {
-            if (kt == DFMI_TYPE_UTF8) {
-                kv.s = std::string_view((const char*)kbytes.data() + (koff[i] - koff[0]), (size_t)(koff[i + 1] - koff[i]));
-            } else if (kt == DFMI_TYPE_BOOLEAN) {
-                bits = (hv[0][i >> 3] >> (i & 7)) & 1;
-                kv.ord = (__int128)bits;
-            } else {
-                const int w = jit::type_width(kt);
-                uint64_t raw = 0;
-                memcpy(&raw, hv[0].data() + (size_t)i * w, w);
-                bits = is_signed_type(kt) ? (uint64_t)(int64_t)narrow_int(raw, kt) : narrow_int(raw, kt);
-                kv.ord = key_ord(kt, bits);
-            }
-        }
-        std::pair<uint64_t, std::vector<Partial>>* entry;
-        auto ix = st->index.find(kv);
-        if (ix != st->index.end()) {
-            entry = ix->second;
-        } else {  // first row of this key in this state (or since a reset): the ordered map, then the index
-            dfmi_agg_state::HKey hk{kv.null, kv.ord, std::string(kv.s)};
-            auto it = st->groups.find(hk);
-            if (it == st->groups.end())
-                it = st->groups.emplace(std::move(hk), std::make_pair(bits, std::vector<Partial>(n + 1))).first;
-            entry = &it->second;
-            st->index.emplace(dfmi_agg_state::HKeyView{it->first.null, it->first.ord, it->first.s}, entry);
-        }
-        std::vector<Partial>& g = entry->second;
-        ++g[n].count;  // the group's selected rows
-        for (size_t j = 0; j < n; ++j)
-            if (valid((int)j + 1, i)) host_accumulate(g[j], st->aggs[j]->fn, progs[j + 1]->type, hv[j + 1].data(), i);
-    }
-    for (auto& kv : st->groups)
-        for (Partial& p : kv.second.second) normalize(p);
+    return outs[0].length;
 }
 
-using GroupMap = std::map<dfmi_agg_state::HKey, std::pair<uint64_t, std::vector<Partial>>>;
+// Key encoding for the host merge's hash index.
+void encode_part(std::string& e, const KeyPart& k) {
+    e.push_back(k.null ? 1 : 0);
+    if (k.null) return;
+    e.append((const char*)&k.ord, sizeof k.ord);
+    const uint32_t l = (uint32_t)k.s.size();
+    e.append((const char*)&l, 4);
+    e.append(k.s);
+}
 
-// Groups in key order as dfmi_agg_state_finish_grouped outputs them.
-void emit_groups(const GroupMap& groups, int kt, const dfmi_aggregate* const* aggs, size_t n, int64_t cap,
-                 dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups) {
+// Rows `rows` (all m rows when null) of the evaluated columns merged into the
+// state's groups on the host, with the kernels' per-row rules.
+void host_merge_rows(dfmi_context* ctx, dfmi_agg_state* st, const std::vector<dfmi::gb::Col>& cols, int64_t m,
+                     const std::vector<int32_t>* rows) {
+    const size_t nk = st->keys.size(), n = st->aggs.size(), no = nk + n;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::vector<std::vector<uint8_t>> hv(no), hb(no);
+    std::vector<std::vector<int32_t>> ho(no);
+    for (size_t o = 0; o < no; ++o) {
+        const dfmi::gb::Col& c = cols[o];
+        if (c.type == DFMI_TYPE_UTF8) {
+            ho[o].resize((size_t)m + 1);
+            HIP_TRY(hipMemcpy(ho[o].data(), c.offsets, ho[o].size() * 4, hipMemcpyDeviceToHost));
+            const int32_t b0 = ho[o][0], b1 = ho[o][m];
+            for (int32_t& x : ho[o]) x -= b0;  // (a sliced column's offsets need not start at 0)
+            hv[o].resize((size_t)std::max(b1 - b0, 1));
+            if (b1 > b0) HIP_TRY(hipMemcpy(hv[o].data(), (const uint8_t*)c.values + b0, (size_t)(b1 - b0),
+                                           hipMemcpyDeviceToHost));
+        } else {
+            const size_t vb = c.type == DFMI_TYPE_BOOLEAN ? (size_t)(m + 7) / 8 : (size_t)m * c.width;
+            hv[o].resize(std::max<size_t>(vb, 1));
+            if (vb) HIP_TRY(hipMemcpy(hv[o].data(), c.values, vb, hipMemcpyDeviceToHost));
+        }
+        if (c.validity && m) {
+            hb[o].resize((size_t)(m + 7) / 8);
+            HIP_TRY(hipMemcpy(hb[o].data(), c.validity, hb[o].size(), hipMemcpyDeviceToHost));
+        }
+    }
+    auto valid = [&](size_t o, int64_t i) { return hb[o].empty() || ((hb[o][i >> 3] >> (i & 7)) & 1); };
+    std::vector<std::vector<Partial>*> touched;
+    std::string enc;
+    const int64_t cnt = rows ? (int64_t)rows->size() : m;
+    for (int64_t x = 0; x < cnt; ++x) {
+        const int64_t i = rows ? (int64_t)(*rows)[x] : x;
+        HKey hk;
+        hk.p.resize(nk);
+        enc.clear();
+        for (size_t p = 0; p < nk; ++p) {
+            KeyPart& k = hk.p[p];
+            const int kt = cols[p].type;
+            if (!valid(p, i)) {
+                k.null = true;
+            } else if (kt == DFMI_TYPE_UTF8) {
+                k.s.assign((const char*)hv[p].data() + ho[p][i], (size_t)(ho[p][i + 1] - ho[p][i]));
+            } else if (kt == DFMI_TYPE_BOOLEAN) {
+                k = fixed_part(kt, (hv[p][i >> 3] >> (i & 7)) & 1);
+            } else {
+                uint64_t raw = 0;
+                memcpy(&raw, hv[p].data() + (size_t)i * cols[p].width, cols[p].width);
+                k = fixed_part(kt, is_signed_type(kt) ? (uint64_t)(int64_t)narrow_int(raw, kt) : narrow_int(raw, kt));
+            }
+            encode_part(enc, k);
+        }
+        std::vector<Partial>* entry;
+        auto ix = st->index.find(enc);
+        if (ix != st->index.end()) {
+            entry = ix->second;
+        } else {  // first row of this key since the last reset / drain of the index
+            entry = &group_entry(st->groups, std::move(hk), n);
+            st->index.emplace(enc, entry);
+        }
+        std::vector<Partial>& g = *entry;
+        if (g[n].flags == 0) {  // first touch in this call: normalise it at the end
+            g[n].flags = 1;
+            touched.push_back(entry);
+        }
+        ++g[n].count;  // the group's selected rows
+        for (size_t j = 0; j < n; ++j)
+            if (valid(nk + j, i)) host_accumulate(g[j], st->aggs[j]->fn, cols[nk + j].type, hv[nk + j].data(), i);
+    }
+    for (std::vector<Partial>* e : touched) {  // only the entries this call touched
+        for (Partial& q : *e) normalize(q);
+        (*e)[n].flags = 0;
+    }
+}
+
+// A batch merged on the host, row by row (diagnostics: DFMI_DIAG=1
+// DFMI_GROUP_HOST=1, the A/B of the device hash table).
+void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in,
+                         uint32_t flags) {
+    std::vector<dfmi::gb::Col> cols;
+    const int64_t m = eval_grouped(ctx, st, pred, in, flags, cols);
+    if (m > 0) host_merge_rows(ctx, st, cols, m, nullptr);
+}
+
+// ---- the device hash table (groupby.h)
+void free_hashdev(HashDev* H) {
+    if (!H) return;
+    void* ps[] = {H->t.ctl, H->t.rep, H->t.gid, H->t.kw, H->t.klen, H->t.knull, H->hdr, H->arena,
+                  H->acc, H->pattern, H->sidx, H->coll};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    if (H->hh) (void)hipHostFree(H->hh);
+    for (auto& b : H->bufs)
+        if (b.p) (void)hipFree(b.p);
+    delete H;
+}
+
+void alloc_table(dfmi::gb::Table& t, uint64_t cap, hipStream_t stream) {
+    t = dfmi::gb::Table{};
+    HIP_TRY(hipMalloc((void**)&t.ctl, cap * 8));
+    HIP_TRY(hipMalloc((void**)&t.rep, cap * 8));
+    HIP_TRY(hipMalloc((void**)&t.gid, cap * 4));
+    HIP_TRY(hipMalloc((void**)&t.kw, cap * 8 * dfmi::gb::kMaxKeys));
+    HIP_TRY(hipMalloc((void**)&t.klen, cap * 4 * dfmi::gb::kMaxKeys));
+    HIP_TRY(hipMalloc((void**)&t.knull, cap * 4));
+    HIP_TRY(hipMemsetAsync(t.ctl, 0, cap * 8, stream));
+    t.mask = cap - 1;
+}
+
+void free_table(dfmi::gb::Table& t) {
+    void* ps[] = {t.ctl, t.rep, t.gid, t.kw, t.klen, t.knull};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    t = dfmi::gb::Table{};
+}
+
+constexpr uint64_t kTableSlots0 = 1 << 16;
+
+HashDev& hashdev(dfmi_context* ctx, dfmi_agg_state* st) {
+    if (st->hd) return *st->hd;
+    HashDev* H = new HashDev();
+    try {
+        const size_t n = st->aggs.size();
+        int w = 1;  // word 0: the group's rows
+        for (size_t j = 0; j < n; ++j) {
+            H->off.push_back(w);
+            const bool fs = st->aggs[j]->fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type);
+            if (fs) H->foff.push_back(w + 4);
+            w += 4 + (fs ? kAggLimbs : 0);
+        }
+        H->words = w;
+        H->hpattern.assign((size_t)w, 0);
+        for (size_t j = 0; j < n; ++j)
+            if (st->aggs[j]->fn == DFMI_AGG_MIN) H->hpattern[(size_t)H->off[j] + 2] = ~0ull;
+        HIP_TRY(hipMalloc((void**)&H->pattern, (size_t)w * 8));
+        HIP_TRY(hipMemcpyAsync(H->pattern, H->hpattern.data(), (size_t)w * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMalloc((void**)&H->hdr, sizeof(dfmi::gb::Hdr)));
+        HIP_TRY(hipMemsetAsync(H->hdr, 0, sizeof(dfmi::gb::Hdr), ctx->stream));
+        HIP_TRY(hipHostMalloc((void**)&H->hh, sizeof(dfmi::gb::Hdr), hipHostMallocDefault));
+        H->cap = kTableSlots0;
+        alloc_table(H->t, H->cap, ctx->stream);
+        H->acc_cap = 1024;
+        HIP_TRY(hipMalloc((void**)&H->acc, H->acc_cap * (size_t)w * 8));
+        HIP_TRY(dfmi::gb::launch_init(H->acc, H->pattern, w, 0, H->acc_cap, ctx->stream));
+        H->arena_cap = 1 << 16;
+        HIP_TRY(hipMalloc((void**)&H->arena, H->arena_cap));
+    } catch (...) {
+        free_hashdev(H);
+        throw;
+    }
+    st->hd = H;
+    return *H;
+}
+
+void read_hdr(dfmi_context* ctx, HashDev& H) {
+    HIP_TRY(hipMemcpyAsync(H.hh, H.hdr, sizeof(dfmi::gb::Hdr), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+}
+
+// A bigger table (cap x 4), every used slot moved (k_group_rehash).
+void grow_table(dfmi_context* ctx, HashDev& H) {
+    dfmi::gb::Table nt;
+    const uint64_t ncap = H.cap * 4;
+    alloc_table(nt, ncap, ctx->stream);
+    HIP_TRY(dfmi::gb::launch_rehash(H.t, nt, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    free_table(H.t);
+    H.t = nt;
+    H.cap = ncap;
+}
+
+// Device buffer `p` of `have` bytes replaced by one of `want`, the first
+// `keep` bytes copied.
+template <typename T>
+void regrow(dfmi_context* ctx, T*& p, size_t keep, size_t want) {
+    T* q = nullptr;
+    HIP_TRY(hipMalloc((void**)&q, want));
+    if (keep) HIP_TRY(hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (p) HIP_TRY(hipFree(p));
+    p = q;
+}
+
+// One batch through the device hash table: the fused evaluation pass, the
+// claim pass (the table grown and the pass run again while a row finds no
+// slot), the accumulate pass; rows whose key shares its hash with another
+// key's are merged on the host.
+void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_program* pred, const dfmi_batch* in,
+                        uint32_t flags) {
+    HashDev& H = hashdev(ctx, st);
+    std::vector<dfmi::gb::Col> cols;
+    const int64_t m = eval_grouped(ctx, st, pred, in, flags, cols);
+    if (m <= 0) return;
+    if (m > 0x7fffffffll) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "GROUP BY batch of 2^31 selected rows or more"};
+    const size_t nk = st->keys.size(), n = st->aggs.size();
+    hipStream_t stream = ctx->stream;
+    if (H.rows_cap < m) {
+        if (H.sidx) HIP_TRY(hipFree(H.sidx));
+        if (H.coll) HIP_TRY(hipFree(H.coll));
+        H.sidx = H.coll = nullptr;
+        H.rows_cap = 0;
+        const int64_t want = m + m / 4;
+        HIP_TRY(hipMalloc((void**)&H.sidx, (size_t)want * 4));
+        HIP_TRY(hipMalloc((void**)&H.coll, (size_t)want * 4));
+        H.rows_cap = want;
+    }
+    uint64_t hash_mask = ~0ull;
+    if (getenv("DFMI_DIAG"))  // diagnostics: a hash of so few bits that many keys share one (the host merge path)
+        if (const char* e = getenv("DFMI_GROUP_HASH_BITS")) hash_mask = (1ull << std::max(1, std::min(63, atoi(e)))) - 1;
+    dfmi::gb::ClaimArgs ca{};
+    for (size_t p = 0; p < nk; ++p) ca.k[p] = cols[p];
+    ca.nkeys = (int)nk;
+    ca.epoch = ++H.epoch;
+    ca.m = m;
+    ca.hash_mask = hash_mask;
+    ca.hdr = H.hdr;
+    ca.sidx = H.sidx;
+    for (int attempt = 0;; ++attempt) {
+        ca.t = H.t;
+        ca.limit = H.cap / 2;
+        HIP_TRY(hipMemsetAsync(&H.hdr->overflow, 0, 8, stream));
+        HIP_TRY(dfmi::gb::launch_claim(ca, stream));
+        read_hdr(ctx, H);
+        if (!H.hh->overflow) break;
+        if (H.cap >= (1ull << 31) || attempt > 16)
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "GROUP BY: more than 2^30 groups on one device"};
+        grow_table(ctx, H);
+    }
+    const uint64_t ng = H.hh->ngroups, aend = H.hh->arena_end;
+    if (ng > H.acc_cap) {
+        uint64_t want = H.acc_cap;
+        while (want < ng) want *= 2;
+        regrow(ctx, H.acc, H.acc_cap * (size_t)H.words * 8, want * (size_t)H.words * 8);
+        HIP_TRY(dfmi::gb::launch_init(H.acc, H.pattern, H.words, H.acc_cap, want, stream));
+        H.acc_cap = want;
+    }
+    if (aend > H.arena_cap) {
+        uint64_t want = H.arena_cap;
+        while (want < aend) want *= 2;
+        regrow(ctx, H.arena, H.arena_cap, want);
+        H.arena_cap = want;
+    }
+    // exact-sum digits absorb 2^31 rows between carry normalisations
+    if (!H.foff.empty() && H.rows_since_norm + (uint64_t)m > (1ull << 30)) {
+        HIP_TRY(dfmi::gb::launch_normalize(H.acc, H.words, H.foff.data(), (int)H.foff.size(), H.ngroups, stream));
+        H.rows_since_norm = 0;
+    }
+    dfmi::gb::AccArgs aa{};
+    for (size_t p = 0; p < nk; ++p) aa.k[p] = cols[p];
+    aa.nkeys = (int)nk;
+    aa.epoch = ca.epoch;
+    aa.m = m;
+    aa.t = H.t;
+    aa.arena = H.arena;
+    aa.sidx = H.sidx;
+    for (size_t j = 0; j < n; ++j) {
+        aa.a[j].c = cols[nk + j];
+        aa.a[j].fn = st->aggs[j]->fn;
+        aa.a[j].off = H.off[j];
+    }
+    aa.naggs = (int)n;
+    aa.words = H.words;
+    aa.acc = H.acc;
+    aa.hdr = H.hdr;
+    aa.coll_rows = H.coll;
+    HIP_TRY(hipMemsetAsync(&H.hdr->collided, 0, 8, stream));
+    HIP_TRY(dfmi::gb::launch_accumulate(aa, stream));
+    read_hdr(ctx, H);
+    H.ngroups = ng;
+    H.rows_since_norm += (uint64_t)m;
+    const uint64_t nc = H.hh->collided;
+    if (nc) {  // rows whose key shares its 63-bit hash with another group's key
+        std::vector<int32_t> rows((size_t)nc);
+        HIP_TRY(hipMemcpy(rows.data(), H.coll, (size_t)nc * 4, hipMemcpyDeviceToHost));
+        std::sort(rows.begin(), rows.end());
+        host_merge_rows(ctx, st, cols, m, &rows);
+    }
+}
+
+// The groups the device hash table holds merged into st->groups, and the
+// table emptied (the next batch starts a new one of the same size).
+void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
+    HashDev* Hp = st->hd;
+    if (!Hp || !Hp->ngroups) return;
+    HashDev& H = *Hp;
+    const size_t nk = st->keys.size(), n = st->aggs.size(), K = dfmi::gb::kMaxKeys;
+    const uint64_t cap = H.cap, ng = H.ngroups;
+    std::vector<uint64_t> ctl(cap), kw(cap * K), acc(ng * (size_t)H.words);
+    std::vector<unsigned> gid(cap), klen(cap * K), knull(cap);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(ctl.data(), H.t.ctl, cap * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(gid.data(), H.t.gid, cap * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(kw.data(), H.t.kw, cap * 8 * K, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(klen.data(), H.t.klen, cap * 4 * K, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(knull.data(), H.t.knull, cap * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(acc.data(), H.acc, acc.size() * 8, hipMemcpyDeviceToHost));
+    read_hdr(ctx, H);
+    std::vector<uint8_t> arena((size_t)std::max<uint64_t>(H.hh->arena_end, 1));
+    if (H.hh->arena_end) HIP_TRY(hipMemcpy(arena.data(), H.arena, H.hh->arena_end, hipMemcpyDeviceToHost));
+    for (uint64_t s = 0; s < cap; ++s) {
+        if (!ctl[s]) continue;
+        HKey hk;
+        hk.p.resize(nk);
+        for (size_t p = 0; p < nk; ++p) {
+            KeyPart& k = hk.p[p];
+            const int kt = st->keys[p].type;
+            if ((knull[s] >> p) & 1) {
+                k.null = true;
+            } else if (kt == DFMI_TYPE_UTF8) {
+                k.s.assign((const char*)arena.data() + kw[s * K + p], klen[s * K + p]);
+            } else {
+                k = fixed_part(kt, kw[s * K + p]);
+            }
+        }
+        const uint64_t* rec = &acc[(size_t)gid[s] * H.words];
+        std::vector<Partial> parts(n + 1);
+        parts[n].count = rec[0];
+        for (size_t j = 0; j < n; ++j) {
+            const uint64_t* w = rec + H.off[j];
+            Partial& q = parts[j];
+            const int fn = st->aggs[j]->fn;
+            q.count = w[0];
+            if (fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type)) {
+                q.flags = w[1] | (w[0] > w[3] ? AGGF_NONNEGZERO : 0);
+                for (int i = 0; i < kAggLimbs; ++i) q.limbs[i] = (int64_t)w[4 + i];
+                normalize(q);
+            } else if (fn == DFMI_AGG_SUM) {
+                q.isum = w[3];
+            } else if (fn == DFMI_AGG_MIN || fn == DFMI_AGG_MAX) {
+                q.key = w[2];
+                q.flags = (w[3] ? AGGF_NAN : 0) | (w[0] > w[3] ? AGGF_VALUE : 0);
+            }
+        }
+        merge_group(group_entry(st->groups, std::move(hk), n), parts, st->aggs.data(), n);
+    }
+    // an empty table of the same size for the next batch
+    HIP_TRY(hipMemsetAsync(H.t.ctl, 0, cap * 8, ctx->stream));
+    HIP_TRY(hipMemsetAsync(H.hdr, 0, sizeof(dfmi::gb::Hdr), ctx->stream));
+    HIP_TRY(dfmi::gb::launch_init(H.acc, H.pattern, H.words, 0, ng, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    H.ngroups = 0;
+    H.rows_since_norm = 0;
+}
+
+// Every group the state holds (window, hash table, host merges) in st->groups.
+void collect_groups(dfmi_context* ctx, dfmi_agg_state* st) {
+    flush_groups(ctx, st);
+    drain_hashed(ctx, st);
+    st->shown.reset();
+}
+
+// Groups in key order as dfmi_agg_state_finish_grouped outputs them:
+// keys[g * nkeys + p], values[g * n + j].
+void emit_groups(const GroupMap& groups, const std::vector<int>& ktypes, const dfmi_aggregate* const* aggs, size_t n,
+                 int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups) {
     *num_groups = (int64_t)groups.size();
     if (*num_groups > cap) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "group capacity too small"};
     if (*num_groups > 0 && (!keys || !values)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+    const size_t nk = ktypes.size();
     int64_t g = 0;
     for (const auto& [hk, v] : groups) {
-        keys[g].type = kt;
-        keys[g].is_null = hk.null ? 1 : 0;
-        keys[g].bits = hk.null ? 0 : (kt == DFMI_TYPE_BOOLEAN ? v.first : narrow_int(v.first, kt));
-        keys[g].count = (int64_t)v.second[n].count;  // the group's selected rows
-        for (size_t j = 0; j < n; ++j) values[g * n + j] = finish_one(*aggs[j], v.second[j]);
+        for (size_t p = 0; p < nk; ++p) {
+            dfmi_agg_value& k = keys[g * nk + p];
+            const int kt = ktypes[p];
+            const KeyPart& kp = hk.p[p];
+            k.type = kt;
+            k.is_null = kp.null ? 1 : 0;
+            k.bits = kp.null || kt == DFMI_TYPE_UTF8 ? 0 : (kt == DFMI_TYPE_BOOLEAN ? kp.bits : narrow_int(kp.bits, kt));
+            k.count = (int64_t)v[n].count;  // the group's selected rows
+        }
+        for (size_t j = 0; j < n; ++j) values[g * n + j] = finish_one(*aggs[j], v[j]);
         ++g;
     }
 }
 
+// The Utf8 bytes of key part `part` of `groups`, in order, as a BinaryArray.
+void emit_key_bytes(const GroupMap& groups, int part, int32_t* offsets, int64_t num_offsets, uint8_t* data,
+                    int64_t data_capacity, int64_t* data_length) {
+    int64_t total = 0;
+    for (const auto& kv : groups) total += (int64_t)kv.first.p[part].s.size();
+    *data_length = total;
+    if (total > 0x7fffffffll) throw Fail{DFMI_ERR_CAPACITY, "Utf8 group keys of 2^31 bytes or more"};
+    if (num_offsets < (int64_t)groups.size() + 1 || data_capacity < total)
+        throw Fail{DFMI_ERR_CAPACITY, "key offsets / bytes capacity too small"};
+    if (!offsets || (total && !data)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+    int64_t g = 0, pos = 0;
+    offsets[0] = 0;
+    for (const auto& kv : groups) {
+        const std::string& s = kv.first.p[part].s;
+        if (!s.empty()) memcpy(data + pos, s.data(), s.size());
+        pos += (int64_t)s.size();
+        offsets[++g] = (int32_t)pos;
+    }
+}
+
 // Serialised per-group partials (multi-GPU GROUP BY): a header, then per group
-// {null, key bits} and its n + 1 partials (aggregates, then the row count).
+// per key part {null, bits, Utf8 length} and the part's bytes (padded to 8),
+// then its n + 1 partials (aggregates, then the row count).
 struct GroupedHdr {
-    uint64_t magic, ngroups, naggs;
-    int64_t key_type;
+    uint64_t magic, ngroups, naggs, nkeys;
+    int64_t key_types[dfmi::gb::kMaxKeys];
 };
-constexpr uint64_t kGroupedMagic = 0x31505247494d4644ull;  // "DFMIGRP1"
-size_t grouped_bytes(size_t ngroups, size_t n) { return sizeof(GroupedHdr) + ngroups * (16 + (n + 1) * sizeof(Partial)); }
+constexpr uint64_t kGroupedMagic = 0x32505247494d4644ull;  // "DFMIGRP2"
+
+size_t grouped_bytes(const GroupMap& groups, size_t n) {
+    size_t b = sizeof(GroupedHdr);
+    for (const auto& kv : groups) {
+        b += (n + 1) * sizeof(Partial);
+        for (const KeyPart& k : kv.first.p) b += 24 + (k.s.size() + 7) / 8 * 8;
+    }
+    return b;
+}
+
+void serialize_groups(const GroupMap& groups, const std::vector<int>& ktypes, size_t n, uint8_t* p) {
+    GroupedHdr h{};
+    h.magic = kGroupedMagic;
+    h.ngroups = groups.size();
+    h.naggs = n;
+    h.nkeys = ktypes.size();
+    for (size_t i = 0; i < ktypes.size(); ++i) h.key_types[i] = ktypes[i];
+    memcpy(p, &h, sizeof h);
+    p += sizeof h;
+    for (const auto& [hk, v] : groups) {
+        for (const KeyPart& k : hk.p) {
+            const uint64_t rec[3] = {k.null ? 1ull : 0ull, k.bits, (uint64_t)k.s.size()};
+            memcpy(p, rec, 24);
+            p += 24;
+            if (!k.s.empty()) memcpy(p, k.s.data(), k.s.size());
+            const size_t pad = (k.s.size() + 7) / 8 * 8;
+            memset(p + k.s.size(), 0, pad - k.s.size());
+            p += pad;
+        }
+        memcpy(p, v.data(), (n + 1) * sizeof(Partial));
+        p += (n + 1) * sizeof(Partial);
+    }
+}
+
+// Every shard's serialised partials merged into `groups` (key types checked).
+void merge_serialized(GroupMap& groups, std::vector<int>& ktypes, const dfmi_aggregate* const* aggs, size_t n,
+                      const void* const* partials, const int64_t* sizes, int nparts) {
+    for (int r = 0; r < nparts; ++r) {
+        const uint8_t* p = (const uint8_t*)partials[r];
+        GroupedHdr h;
+        if (!p || sizes[r] < (int64_t)sizeof h) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+        memcpy(&h, p, sizeof h);
+        if (h.magic != kGroupedMagic || h.naggs != (uint64_t)n || h.nkeys < 1 || h.nkeys > (uint64_t)dfmi::gb::kMaxKeys)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+        std::vector<int> kt(h.key_types, h.key_types + h.nkeys);
+        if (!ktypes.empty() && kt != ktypes) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+        ktypes = kt;
+        const uint8_t* end = p + sizes[r];
+        p += sizeof h;
+        for (uint64_t g = 0; g < h.ngroups; ++g) {
+            HKey hk;
+            hk.p.resize(h.nkeys);
+            for (uint64_t q = 0; q < h.nkeys; ++q) {
+                uint64_t rec[3];
+                if (end - p < 24) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+                memcpy(rec, p, 24);
+                p += 24;
+                const size_t pad = (size_t)(rec[2] + 7) / 8 * 8;
+                if ((size_t)(end - p) < pad) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+                KeyPart& k = hk.p[q];
+                if (rec[0]) {
+                    k.null = true;
+                } else if (kt[q] == DFMI_TYPE_UTF8) {
+                    k.s.assign((const char*)p, (size_t)rec[2]);
+                } else {
+                    k = fixed_part(kt[q], rec[1]);
+                }
+                p += pad;
+            }
+            if ((size_t)(end - p) < (n + 1) * sizeof(Partial)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
+            std::vector<Partial> parts(n + 1);
+            memcpy(parts.data(), p, (n + 1) * sizeof(Partial));
+            p += (n + 1) * sizeof(Partial);
+            merge_group(group_entry(groups, std::move(hk), n), parts, aggs, n);
+        }
+    }
+}
+
+std::vector<int> key_types(const dfmi_agg_state* st) {
+    std::vector<int> t;
+    for (const dfmi_program& k : st->keys) t.push_back(k.type);
+    return t;
+}
 
 }  // namespace
 
@@ -767,44 +1239,56 @@ extern "C" int32_t dfmi_agg_state_create(dfmi_context* ctx, const dfmi_aggregate
     }
 }
 
-extern "C" int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key,
-                                                 const dfmi_aggregate* const* aggs, int32_t n, dfmi_agg_state** out,
-                                                 dfmi_error* err) {
+extern "C" int32_t dfmi_agg_state_create_grouped_multi(dfmi_context* ctx, const dfmi_program* const* keys,
+                                                       int32_t num_keys, const dfmi_aggregate* const* aggs, int32_t n,
+                                                       dfmi_agg_state** out, dfmi_error* err) {
     set_err(err, DFMI_OK, "");
     dfmi_agg_state* st = nullptr;
     try {
-        if (!ctx || !out || !key || n <= 0 || !aggs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
-        const int kt = key->type;
-        if (kt != DFMI_TYPE_BOOLEAN && !is_numeric_type(kt) && kt != DFMI_TYPE_UTF8)
-            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_debug(kt)};
-        if (n > 15) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 15 grouped aggregates"};
+        if (!ctx || !out || !keys || num_keys <= 0 || n <= 0 || !aggs) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        if (num_keys > dfmi::gb::kMaxKeys)
+            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 4 GROUP BY expressions"};
+        for (int p = 0; p < num_keys; ++p) {
+            if (!keys[p]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL key"};
+            const int kt = keys[p]->type;
+            if (kt != DFMI_TYPE_BOOLEAN && !is_numeric_type(kt) && kt != DFMI_TYPE_UTF8)
+                throw Fail{DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_debug(kt)};
+        }
+        if (n > dfmi::gb::kMaxAggs) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 15 grouped aggregates"};
         st = new dfmi_agg_state();
         st->device = ctx->device;
         st->grouped = true;
-        st->key = *key;
-        st->gslots = kt == DFMI_TYPE_BOOLEAN ? 3 : 17;  // false, true / 16 consecutive values; + null
+        for (int p = 0; p < num_keys; ++p) st->keys.push_back(*keys[p]);
+        st->key = *keys[0];
+        const int kt = st->key.type;
         for (int j = 0; j < n; ++j) {
             if (!aggs[j]) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL aggregate"};
             st->aggs.push_back(aggs[j]);
         }
-        const size_t na = (size_t)n + 1;
-        st->acc_words = (size_t)kAggCopies * st->gslots * na * kAggWords;
-        std::vector<uint64_t> init(st->acc_words, 0);
-        for (size_t cg = 0; cg < (size_t)kAggCopies * st->gslots; ++cg)
-            for (int j = 0; j < n; ++j)
-                if (aggs[j]->fn == DFMI_AGG_MIN) init[(cg * na + j) * kAggWords + 2] = ~0ull;
         HIP_TRY(hipSetDevice(ctx->device));
-        HIP_TRY(hipMalloc((void**)&st->acc, st->acc_words * 8));
-        HIP_TRY(hipMemcpyAsync(st->acc, init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        st->init = std::move(init);
-        if (kt != DFMI_TYPE_BOOLEAN && !host_keyed(kt)) {
-            dfmi_error e2{};
-            for (int i = 0; i < 2; ++i)
-                if (dfmi_compile_aggregate(i ? "MAX" : "MIN", key, kt, DFMI_FLAG_EXT_AGGREGATE, &st->mm[i], &e2) != DFMI_OK)
-                    throw Fail{e2.code, e2.message};
-            const dfmi_aggregate* mm[2] = {st->mm[0], st->mm[1]};
-            if (dfmi_agg_state_create(ctx, mm, 2, &st->mm_state, &e2) != DFMI_OK) throw Fail{e2.code, e2.message};
+        // one Boolean / integer key: the window kernel (16 consecutive values
+        // per batch, more through the hash table); anything else: the hash table
+        if (num_keys == 1 && (kt == DFMI_TYPE_BOOLEAN || !host_keyed(kt))) {
+            st->gslots = kt == DFMI_TYPE_BOOLEAN ? 3 : 17;  // false, true / 16 consecutive values; + null
+            const size_t na = (size_t)n + 1;
+            st->acc_words = (size_t)kAggCopies * st->gslots * na * kAggWords;
+            std::vector<uint64_t> init(st->acc_words, 0);
+            for (size_t cg = 0; cg < (size_t)kAggCopies * st->gslots; ++cg)
+                for (int j = 0; j < n; ++j)
+                    if (aggs[j]->fn == DFMI_AGG_MIN) init[(cg * na + j) * kAggWords + 2] = ~0ull;
+            HIP_TRY(hipMalloc((void**)&st->acc, st->acc_words * 8));
+            HIP_TRY(hipMemcpyAsync(st->acc, init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            st->init = std::move(init);
+            if (kt != DFMI_TYPE_BOOLEAN) {
+                dfmi_error e2{};
+                for (int i = 0; i < 2; ++i)
+                    if (dfmi_compile_aggregate(i ? "MAX" : "MIN", keys[0], kt, DFMI_FLAG_EXT_AGGREGATE, &st->mm[i], &e2) !=
+                        DFMI_OK)
+                        throw Fail{e2.code, e2.message};
+                const dfmi_aggregate* mm[2] = {st->mm[0], st->mm[1]};
+                if (dfmi_agg_state_create(ctx, mm, 2, &st->mm_state, &e2) != DFMI_OK) throw Fail{e2.code, e2.message};
+            }
         }
         *out = st;
         return DFMI_OK;
@@ -813,6 +1297,21 @@ extern "C" int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_p
         set_err(err, f.code, f.msg);
         return f.code;
     }
+}
+
+extern "C" int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key,
+                                                 const dfmi_aggregate* const* aggs, int32_t n, dfmi_agg_state** out,
+                                                 dfmi_error* err) {
+    if (!key) {
+        set_err(err, DFMI_ERR_INVALID_ARGUMENT, "bad argument");
+        return DFMI_ERR_INVALID_ARGUMENT;
+    }
+    const dfmi_program* keys[1] = {key};
+    return dfmi_agg_state_create_grouped_multi(ctx, keys, 1, aggs, n, out, err);
+}
+
+extern "C" int32_t dfmi_agg_state_num_keys(const dfmi_agg_state* st) {
+    return st && st->grouped ? (int32_t)st->keys.size() : 0;
 }
 
 extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_state* st, int64_t cap,
@@ -827,8 +1326,29 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
             return st->failure.code;
         }
         HIP_TRY(hipSetDevice(ctx->device));
-        flush_groups(ctx, st);
-        emit_groups(st->groups, st->key.type, st->aggs.data(), st->aggs.size(), cap, keys, values, num_groups);
+        collect_groups(ctx, st);
+        emit_groups(st->groups, key_types(st), st->aggs.data(), st->aggs.size(), cap, keys, values, num_groups);
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_state_group_keys_utf8_part(const dfmi_agg_state* st, int32_t part, int32_t* offsets,
+                                                       int64_t num_offsets, uint8_t* data, int64_t data_capacity,
+                                                       int64_t* data_length, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!st || !data_length) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+        if (st->failed) {
+            if (err) *err = st->failure;
+            return st->failure.code;
+        }
+        if (!st->grouped || part < 0 || part >= (int32_t)st->keys.size() || st->keys[part].type != DFMI_TYPE_UTF8)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state over a Utf8 key"};
+        emit_key_bytes(st->shown ? *st->shown : st->groups, part, offsets, num_offsets, data, data_capacity,
+                       data_length);
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -839,29 +1359,7 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
 extern "C" int32_t dfmi_agg_state_group_keys_utf8(const dfmi_agg_state* st, int32_t* offsets, int64_t num_offsets,
                                                   uint8_t* data, int64_t data_capacity, int64_t* data_length,
                                                   dfmi_error* err) {
-    set_err(err, DFMI_OK, "");
-    try {
-        if (!st || !data_length) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
-        if (!st->grouped || st->key.type != DFMI_TYPE_UTF8)
-            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state over a Utf8 key"};
-        int64_t total = 0;
-        for (const auto& kv : st->groups) total += (int64_t)kv.first.s.size();
-        *data_length = total;
-        if (num_offsets < (int64_t)st->groups.size() + 1 || data_capacity < total)
-            throw Fail{DFMI_ERR_CAPACITY, "key offsets / bytes capacity too small"};
-        if (!offsets || (total && !data)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
-        int64_t g = 0, pos = 0;
-        offsets[0] = 0;
-        for (const auto& kv : st->groups) {
-            if (!kv.first.s.empty()) memcpy(data + pos, kv.first.s.data(), kv.first.s.size());
-            pos += (int64_t)kv.first.s.size();
-            offsets[++g] = (int32_t)pos;
-        }
-        return DFMI_OK;
-    } catch (const Fail& f) {
-        set_err(err, f.code, f.msg);
-        return f.code;
-    }
+    return dfmi_agg_state_group_keys_utf8_part(st, 0, offsets, num_offsets, data, data_capacity, data_length, err);
 }
 
 extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, dfmi_error* err) {
@@ -869,11 +1367,20 @@ extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, d
     try {
         if (!ctx || !st) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
         HIP_TRY(hipSetDevice(ctx->device));
-        HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (st->acc)
+            HIP_TRY(hipMemcpyAsync(st->acc, st->init.data(), st->acc_words * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (HashDev* H = st->hd) {  // an empty table of the same size
+            HIP_TRY(hipMemsetAsync(H->t.ctl, 0, H->cap * 8, ctx->stream));
+            HIP_TRY(hipMemsetAsync(H->hdr, 0, sizeof(dfmi::gb::Hdr), ctx->stream));
+            HIP_TRY(dfmi::gb::launch_init(H->acc, H->pattern, H->words, 0, H->ngroups, ctx->stream));
+            H->ngroups = 0;
+            H->rows_since_norm = 0;
+        }
         st->failed = false;
         st->failure = dfmi_error{};
         st->index.clear();
         st->groups.clear();
+        st->shown.reset();
         st->win_width = -1;
         st->dirty = false;
         if (st->mm_state) {
@@ -892,10 +1399,9 @@ extern "C" void dfmi_agg_state_free(dfmi_agg_state* st) {
     dfmi_agg_state_free(st->mm_state);
     dfmi_aggregate_free(st->mm[0]);
     dfmi_aggregate_free(st->mm[1]);
-    if (st->acc) {
-        (void)hipSetDevice(st->device);
-        (void)hipFree(st->acc);
-    }
+    (void)hipSetDevice(st->device);
+    if (st->acc) (void)hipFree(st->acc);
+    free_hashdev(st->hd);
     delete st;
 }
 
@@ -914,11 +1420,16 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             HIP_TRY(hipSetDevice(ctx->device));
             in = unslice(in, 1, us_, true, ctx->stream);
         }
-        if (st->grouped && host_keyed(st->key.type)) {
-            // float / Utf8 keys: the key and the arguments through one fused
-            // Selection + Projection pass, each row merged on the host
+        if (st->grouped && (!st->acc || (getenv("DFMI_DIAG") && getenv("DFMI_GROUP_HOST")))) {
+            // several keys, a float or Utf8 key: the keys and the arguments
+            // through one fused Selection + Projection pass, then the device
+            // hash table (or, diagnostics, the host merge)
             HIP_TRY(hipSetDevice(ctx->device));
-            if (in->num_rows > 0) group_batch_on_host(ctx, st, pred, in, flags);
+            if (in->num_rows > 0) {
+                if (st->acc) flush_groups(ctx, st);
+                if (getenv("DFMI_DIAG") && getenv("DFMI_GROUP_HOST")) group_batch_on_host(ctx, st, pred, in, flags);
+                else group_batch_hashed(ctx, st, pred, in, flags);
+            }
             return DFMI_OK;
         }
         // the query's selectivity last time (this state, this predicate)
@@ -960,11 +1471,11 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
                 } else {
                     wbase = mm[0].count ? mm[0].bits : 0;
                     if (mm[0].count && mm[1].bits - mm[0].bits >= (uint64_t)wwidth) {
-                        // wider than the device window: the host merge (its
+                        // wider than the device window: the hash table (its
                         // fused pass raises the same first error in the same
                         // evaluation order as the grouped kernel would)
                         flush_groups(ctx, st);
-                        group_batch_on_host(ctx, st, pred, in, flags);
+                        group_batch_hashed(ctx, st, pred, in, flags);
                         return DFMI_OK;
                     }
                 }
@@ -1127,11 +1638,9 @@ extern "C" int64_t dfmi_agg_state_grouped_partial_bytes(dfmi_context* ctx, dfmi_
             if (err) *err = st->failure;
             return -(int64_t)st->failure.code;
         }
-        if (st->key.type == DFMI_TYPE_UTF8)
-            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "multi-GPU GROUP BY over Utf8"};
         HIP_TRY(hipSetDevice(ctx->device));
-        flush_groups(ctx, st);
-        return (int64_t)grouped_bytes(st->groups.size(), st->aggs.size());
+        collect_groups(ctx, st);
+        return (int64_t)grouped_bytes(st->groups, st->aggs.size());
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
         return -(int64_t)f.code;
@@ -1148,23 +1657,11 @@ extern "C" int32_t dfmi_agg_state_grouped_partial(dfmi_context* ctx, dfmi_agg_st
             if (err) *err = st->failure;
             return st->failure.code;
         }
-        if (st->key.type == DFMI_TYPE_UTF8)
-            throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "multi-GPU GROUP BY over Utf8"};
         HIP_TRY(hipSetDevice(ctx->device));
-        flush_groups(ctx, st);
-        const size_t n = st->aggs.size();
-        if ((size_t)bytes < grouped_bytes(st->groups.size(), n)) throw Fail{DFMI_ERR_CAPACITY, "partial buffer too small"};
-        uint8_t* p = (uint8_t*)host_out;
-        const GroupedHdr h{kGroupedMagic, (uint64_t)st->groups.size(), (uint64_t)n, (int64_t)st->key.type};
-        memcpy(p, &h, sizeof h);
-        p += sizeof h;
-        for (const auto& [hk, v] : st->groups) {
-            const uint64_t rec[2] = {hk.null ? 1ull : 0ull, v.first};
-            memcpy(p, rec, 16);
-            p += 16;
-            memcpy(p, v.second.data(), (n + 1) * sizeof(Partial));
-            p += (n + 1) * sizeof(Partial);
-        }
+        collect_groups(ctx, st);
+        if ((size_t)bytes < grouped_bytes(st->groups, st->aggs.size()))
+            throw Fail{DFMI_ERR_CAPACITY, "partial buffer too small"};
+        serialize_groups(st->groups, key_types(st), st->aggs.size(), (uint8_t*)host_out);
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -1181,35 +1678,53 @@ extern "C" int32_t dfmi_agg_merge_grouped_partials(const dfmi_aggregate* const* 
         if (!aggs || n <= 0 || !partials || !sizes || nparts <= 0 || !num_groups)
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
         GroupMap groups;
-        int64_t kt = -1;
-        for (int r = 0; r < nparts; ++r) {
-            const uint8_t* p = (const uint8_t*)partials[r];
-            GroupedHdr h;
-            if (!p || sizes[r] < (int64_t)sizeof h) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
-            memcpy(&h, p, sizeof h);
-            if (h.magic != kGroupedMagic || h.naggs != (uint64_t)n || (kt >= 0 && h.key_type != kt) ||
-                (size_t)sizes[r] < grouped_bytes(h.ngroups, (size_t)n))
-                throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad grouped partial"};
-            kt = h.key_type;
-            p += sizeof h;
-            for (uint64_t g = 0; g < h.ngroups; ++g) {
-                uint64_t rec[2];
-                memcpy(rec, p, 16);
-                p += 16;
-                dfmi_agg_state::HKey hk{rec[0] != 0, 0, {}};
-                if (!hk.null) hk.ord = key_ord((int)kt, rec[1]);
-                auto it = groups.find(hk);
-                if (it == groups.end()) it = groups.emplace(hk, std::make_pair(rec[1], std::vector<Partial>(n + 1))).first;
-                for (int j = 0; j <= n; ++j) {
-                    Partial q;
-                    memcpy(&q, p + (size_t)j * sizeof(Partial), sizeof q);
-                    if (j < n) merge_partial(it->second.second[j], q, aggs[j]->fn == DFMI_AGG_MIN);
-                    else it->second.second[n].count += q.count;
-                }
-                p += (size_t)(n + 1) * sizeof(Partial);
-            }
-        }
-        emit_groups(groups, (int)std::max<int64_t>(kt, 0), aggs, (size_t)n, cap, keys, values, num_groups);
+        std::vector<int> kt;
+        merge_serialized(groups, kt, aggs, (size_t)n, partials, sizes, nparts);
+        emit_groups(groups, kt, aggs, (size_t)n, cap, keys, values, num_groups);
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+extern "C" int32_t dfmi_agg_merge_grouped_partials_keys_utf8(const dfmi_aggregate* const* aggs, int32_t n,
+                                                             const void* const* partials, const int64_t* sizes,
+                                                             int32_t nparts, int32_t part, int32_t* offsets,
+                                                             int64_t num_offsets, uint8_t* data, int64_t data_capacity,
+                                                             int64_t* data_length, dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!aggs || n <= 0 || !partials || !sizes || nparts <= 0 || !data_length)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        GroupMap groups;
+        std::vector<int> kt;
+        merge_serialized(groups, kt, aggs, (size_t)n, partials, sizes, nparts);
+        if (part < 0 || part >= (int32_t)kt.size() || kt[part] != DFMI_TYPE_UTF8)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a Utf8 key part"};
+        emit_key_bytes(groups, part, offsets, num_offsets, data, data_capacity, data_length);
+        return DFMI_OK;
+    } catch (const Fail& f) {
+        set_err(err, f.code, f.msg);
+        return f.code;
+    }
+}
+
+// dfmi_shard_agg_finish_grouped's merge (shard.cpp): every rank's partials
+// merged into the state's shown groups, so the Utf8 key bytes of the merged
+// groups come from dfmi_agg_state_group_keys_utf8* afterwards.
+int32_t dfmi_agg_state_show_merged(dfmi_agg_state* st, const void* const* partials, const int64_t* sizes, int32_t nparts,
+                                   int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups,
+                                   dfmi_error* err) {
+    set_err(err, DFMI_OK, "");
+    try {
+        if (!st || !st->grouped || !partials || !sizes || nparts <= 0 || !num_groups)
+            throw Fail{DFMI_ERR_INVALID_ARGUMENT, "bad argument"};
+        auto merged = std::make_shared<GroupMap>();
+        std::vector<int> kt = key_types(st);
+        merge_serialized(*merged, kt, st->aggs.data(), st->aggs.size(), partials, sizes, nparts);
+        emit_groups(*merged, kt, st->aggs.data(), st->aggs.size(), cap, keys, values, num_groups);
+        st->shown = merged;
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -1280,6 +1795,7 @@ extern "C" int64_t dfmi_internal_agg_grouped_jit_check(const dfmi_program* pred,
         dfmi_agg_state st;
         st.grouped = true;
         st.key = *key;
+        st.keys.push_back(*key);
         st.gslots = key->type == DFMI_TYPE_BOOLEAN ? 3 : 17;
         for (int j = 0; j < n; ++j) st.aggs.push_back(aggs[j]);
         AggBuilt B;

@@ -1,0 +1,118 @@
+// Device GROUP BY by hashing (aggregate.cpp "hashed groups", kernels in
+// groupby.hip): the shapes shared by the host side and the fixed kernels.
+//
+// The key and aggregate arguments of a batch are first evaluated by the fused
+// Selection + Projection pass (dfmi_filter_project: projections [keys...,
+// args...], the reference's evaluation order and first error), so these
+// kernels only ever see compacted, offset-0 columns. Per batch:
+//   k_group_claim       every row hashes its key and finds its slot in an
+//                       open-addressing table (linear probing); a row that
+//                       finds an empty slot claims it with a CAS on `ctl`
+//                       and becomes the slot's representative row, takes the
+//                       next dense group id, and reserves arena bytes for its
+//                       Utf8 key parts. Nothing but `ctl` is read from the
+//                       table in this kernel, so no cross-XCD hand-off
+//                       depends on L2 coherence within the launch.
+//   k_group_accumulate  every row checks its key against its slot's key --
+//                       the representative row of this batch (a slot
+//                       claimed by this launch's claim pass), or the key
+//                       persisted by an earlier batch -- and adds its
+//                       values into the group's accumulators with atomics;
+//                       the representative row persists its key. A row
+//                       whose key differs from the slot's (two keys with one
+//                       63-bit hash) is listed; the host merges those rows
+//                       (exactly, aggregate.cpp).
+#ifndef DFMI_GROUPBY_H
+#define DFMI_GROUPBY_H
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace dfmi {
+namespace gb {
+
+constexpr int kMaxKeys = 4;   // GROUP BY key expressions
+constexpr int kMaxAggs = 15;  // aggregates of one grouped state
+
+// One key part or aggregate argument: a compacted output column (or a
+// passed-through input column) of the fused pass.
+struct Col {
+    int32_t type;              // dfmi_type
+    int32_t width;             // value bytes (0: Boolean bitmap / Utf8)
+    const void* values;        // fixed-width values / Boolean bitmap / Utf8 bytes
+    const int32_t* offsets;    // Utf8
+    const uint8_t* validity;   // nullptr: every value valid
+};
+
+// The table (struct of arrays, capacity cap = mask + 1 slots).
+struct Table {
+    unsigned long long* ctl;   // [cap] 0: empty; else the key's hash | 1 (written once, by CAS)
+    long long* rep;            // [cap] (epoch << 32) | representative row of the claiming batch
+    unsigned* gid;             // [cap] dense group id
+    unsigned long long* kw;    // [cap][kMaxKeys] persisted key words (Utf8: arena offset)
+    unsigned* klen;            // [cap][kMaxKeys] Utf8 key bytes
+    unsigned* knull;           // [cap] bit p: key part p is null
+    unsigned long long mask;   // cap - 1
+};
+
+// Device header (one per state): counters the host reads after a pass.
+struct Hdr {
+    unsigned long long ngroups;    // groups (claimed slots)
+    unsigned long long arena_end;  // Utf8 arena bytes reserved
+    unsigned long long overflow;   // nonzero: a row found no slot (table past its load limit)
+    unsigned long long collided;   // rows whose key differs from their slot's (listed)
+    unsigned long long pad[4];
+};
+
+struct ClaimArgs {
+    Col k[kMaxKeys];
+    int32_t nkeys;
+    uint32_t epoch;                // this batch's number (rep words)
+    long long m;                   // rows
+    Table t;
+    unsigned long long limit;      // claim no slot once ngroups >= limit (the host grows the table)
+    unsigned long long hash_mask;  // diagnostics: ~0 (DFMI_GROUP_HASH_BITS narrows it to force collisions)
+    Hdr* hdr;
+    int32_t* sidx;                 // [m] the row's slot (-1: not placed)
+};
+
+struct AggCol {
+    Col c;
+    int32_t fn;    // dfmi_agg_fn
+    int32_t off;   // word offset of this aggregate in a group's record
+};
+
+// A group's accumulator record: word 0 = the group's rows, then per
+// aggregate [count, flags, key, aux] (+ kAggLimbs exact-sum digits for a
+// floating-point SUM). aux: integer SUM the wrapping sum; MIN / MAX the NaN
+// values seen; float SUM the values that are not finite-and-not-(-0.0).
+struct AccArgs {
+    Col k[kMaxKeys];
+    int32_t nkeys;
+    uint32_t epoch;
+    long long m;
+    Table t;
+    unsigned char* arena;          // Utf8 key bytes of every group
+    const int32_t* sidx;
+    AggCol a[kMaxAggs];
+    int32_t naggs;
+    int32_t words;                 // words per group record
+    unsigned long long* acc;       // [groups][words]
+    Hdr* hdr;
+    int32_t* coll_rows;            // [m] rows whose key differs from the slot's
+};
+
+// groupby.hip: launches on `stream` (asynchronous)
+hipError_t launch_claim(const ClaimArgs& a, hipStream_t stream);
+hipError_t launch_accumulate(const AccArgs& a, hipStream_t stream);
+hipError_t launch_rehash(const Table& from, const Table& to, hipStream_t stream);
+hipError_t launch_init(unsigned long long* acc, const unsigned long long* pattern, int words, unsigned long long g0,
+                       unsigned long long g1, hipStream_t stream);
+hipError_t launch_normalize(unsigned long long* acc, int words, const int* foff, int nf, unsigned long long ngroups,
+                            hipStream_t stream);
+
+}  // namespace gb
+}  // namespace dfmi
+
+#endif

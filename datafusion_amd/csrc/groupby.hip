@@ -1,0 +1,492 @@
+// Device GROUP BY by hashing: the fixed gfx950 kernels (groupby.h has the
+// protocol; aggregate.cpp drives them). Every kernel takes compacted,
+// offset-0 columns -- the fused Selection + Projection pass has already
+// evaluated the keys and the aggregate arguments.
+//
+// Per-row rules are those of the aggregate kernels (jit_skeleton.hip agg_key
+// / agg_sum_flags / fsum_add) and of the host merge (aggregate.cpp
+// host_accumulate_t): COUNT counts non-null values, integer SUM wraps, a float
+// SUM is the exact sum of 32-bit digits in units of 2^-1074, MIN / MAX use
+// the order-preserving key (NaN never keyed, -0.0 below +0.0).
+#include <hip/hip_runtime.h>
+
+#include "../../include/dfmi.h"
+#include "groupby.h"
+#include "jit_skeleton.hip"
+
+namespace dfmi {
+namespace gb {
+
+typedef unsigned long long u64_ua __attribute__((aligned(1)));
+
+__device__ __forceinline__ u64 gmix(u64 z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ bool valid_at(const Col& c, long long i) {
+    return !c.validity || ((c.validity[i >> 3] >> (i & 7)) & 1);
+}
+
+// Fixed-width key bits: Boolean 0/1, signed integers sign-extended, unsigned
+// zero-extended, floats their raw bits (one group per bit pattern).
+__device__ __forceinline__ u64 key_bits(const Col& c, long long i) {
+    switch (c.type) {
+        case 1: return (((const u8*)c.values)[i >> 3] >> (i & 7)) & 1;  // DFMI_TYPE_BOOLEAN
+        case 2: return (u64)(i64)((const i8*)c.values)[i];
+        case 3: return (u64)(i64)((const i16*)c.values)[i];
+        case 4: return (u64)(i64)((const i32*)c.values)[i];
+        case 5: return (u64)((const i64*)c.values)[i];
+        case 6: return (u64)((const u8*)c.values)[i];
+        case 7: return (u64)((const u16*)c.values)[i];
+        case 8: return (u64)((const u32*)c.values)[i];
+        case 9: return ((const u64*)c.values)[i];
+        case 10: return (u64)((const u32*)c.values)[i];  // Float32 bits
+        case 11: return ((const u64*)c.values)[i];       // Float64 bits
+        default: return 0;
+    }
+}
+
+constexpr int kTypeUtf8 = 12;
+
+__device__ __forceinline__ u64 hash_bytes(const u8* p, unsigned len, u64 h) {
+    unsigned j = 0;
+    for (; j + 8 <= len; j += 8) h = gmix(h ^ *(const u64_ua*)(p + j)) + 0x9E3779B97F4A7C15ull;
+    u64 t = 0;
+    for (unsigned s = 0; j < len; ++j, s += 8) t |= (u64)p[j] << s;
+    return gmix(h ^ t ^ ((u64)len << 56));
+}
+
+__device__ __forceinline__ bool bytes_eq(const u8* a, const u8* b, unsigned len) {
+    unsigned j = 0;
+    for (; j + 8 <= len; j += 8)
+        if (*(const u64_ua*)(a + j) != *(const u64_ua*)(b + j)) return false;
+    for (; j < len; ++j)
+        if (a[j] != b[j]) return false;
+    return true;
+}
+
+// The row's key: null mask, fixed-width bits, Utf8 (start, length); its hash.
+struct RowKey {
+    unsigned nullm;
+    u64 w[kMaxKeys];
+    const u8* s[kMaxKeys];
+    unsigned len[kMaxKeys];
+};
+
+template <int NK>
+__device__ __forceinline__ u64 row_key(const Col* k, long long i, RowKey& r) {
+    u64 h = 0x243F6A8885A308D3ull;
+    r.nullm = 0;
+#pragma unroll
+    for (int p = 0; p < NK; ++p) {
+        const Col& c = k[p];
+        r.w[p] = 0;
+        r.s[p] = nullptr;
+        r.len[p] = 0;
+        if (!valid_at(c, i)) {
+            r.nullm |= 1u << p;
+            h = gmix(h + 0x5BD1E9955BD1E995ull * (u64)(p + 1));
+        } else if (c.type == kTypeUtf8) {
+            const int a = c.offsets[i], b = c.offsets[i + 1];
+            r.s[p] = (const u8*)c.values + a;
+            r.len[p] = (unsigned)(b - a);
+            h = hash_bytes(r.s[p], r.len[p], h + (u64)p);
+        } else {
+            r.w[p] = key_bits(c, i);
+            h = gmix(h ^ (r.w[p] * 0xD6E8FEB86659FD93ull + (u64)p));
+        }
+    }
+    return h;
+}
+
+// ------------------------------------------------------------ claim pass
+// NK: key parts (a template parameter so a row's key stays in registers)
+template <int NK>
+__global__ __launch_bounds__(256) void k_group_claim(const ClaimArgs A) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const Table& t = A.t;
+    bool overflow = false;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
+        RowKey r;
+        const u64 h = row_key<NK>(A.k, i, r);
+        const u64 c = (h & A.hash_mask) | 1ull;
+        u64 s = gmix(c) & t.mask;
+        int res = -1;
+        for (u64 probe = 0; probe <= t.mask; ++probe, s = (s + 1) & t.mask) {
+            u64 cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == 0) {
+                if (__hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit) {
+                    overflow = true;
+                    break;
+                }
+                cur = atomicCAS(&t.ctl[s], 0ull, c);
+                if (cur == 0) {  // claimed: this row represents the slot's key
+                    t.gid[s] = (unsigned)atomicAdd(&A.hdr->ngroups, 1ull);
+                    t.rep[s] = ((long long)A.epoch << 32) | (long long)(unsigned)i;
+                    t.knull[s] = r.nullm;
+#pragma unroll
+                    for (int p = 0; p < NK; ++p) {
+                        u64 w = r.w[p];
+                        if (r.s[p]) w = atomicAdd(&A.hdr->arena_end, (u64)r.len[p]);
+                        t.kw[s * kMaxKeys + p] = w;
+                        t.klen[s * kMaxKeys + p] = r.len[p];
+                    }
+                    res = (int)s;
+                    break;
+                }
+            }
+            if (cur == c) {
+                res = (int)s;
+                break;
+            }
+        }
+        if (res < 0) overflow = true;
+        A.sidx[i] = res;
+    }
+    if (overflow) atomicOr(&A.hdr->overflow, 1ull);
+}
+
+// ------------------------------------------------- exact float sum digits
+// (fsum_add's digit split, jit_skeleton.hip): a double is m * 2^(b-1074),
+// digits d = b/32 .. d+2 receive the three 32-bit pieces of m << (b % 32).
+__device__ __forceinline__ void fsum_pieces(double v, int& d, long long& c0, long long& c1, long long& c2) {
+    const u64 b = __builtin_bit_cast(u64, v);
+    const int e = (int)((b >> 52) & 0x7ff);
+    const u64 m = (b & ((1ull << 52) - 1)) | (e ? (1ull << 52) : 0ull);
+    const int pos = (e ? e : 1) - 1;
+    d = pos >> 5;
+    const int sh = pos & 31;
+    const u64 x0 = (m & 0xffffffffull) << sh, x1 = (m >> 32) << sh;
+    c0 = (long long)(x0 & 0xffffffffull);
+    c1 = (long long)((x0 >> 32) + (x1 & 0xffffffffull));
+    c2 = (long long)(x1 >> 32);
+    if (b >> 63) {
+        c0 = -c0;
+        c1 = -c1;
+        c2 = -c2;
+    }
+}
+
+__device__ __forceinline__ void lane_fsum_add(long long* limbs, double v) {
+    int d;
+    long long c0, c1, c2;
+    fsum_pieces(v, d, c0, c1, c2);
+    if (c0) atomicAdd((u64*)&limbs[d], (u64)c0);
+    if (c1) atomicAdd((u64*)&limbs[d + 1], (u64)c1);
+    if (c2) atomicAdd((u64*)&limbs[d + 2], (u64)c2);
+}
+
+// The `ok` lanes' values of one group (every lane active): summed across the
+// wave when they share a digit (the leader adds three words), else per lane.
+__device__ __forceinline__ void gb_fsum_add(long long* limbs, double v, bool ok, int lane, int leader) {
+    const u64 vm = __ballot(ok);
+    if (!vm) return;
+    int d = 0;
+    long long c0 = 0, c1 = 0, c2 = 0;
+    if (ok) fsum_pieces(v, d, c0, c1, c2);
+    const int d0 = __builtin_amdgcn_readlane(d, __builtin_ctzll(vm));
+    if (!__ballot(ok && d != d0)) {
+        const u64 s0 = wave_sum((u64)c0), s1 = wave_sum((u64)c1), s2 = wave_sum((u64)c2);
+        if (lane == leader) {
+            if (s0) atomicAdd((u64*)&limbs[d0], s0);
+            if (s1) atomicAdd((u64*)&limbs[d0 + 1], s1);
+            if (s2) atomicAdd((u64*)&limbs[d0 + 2], s2);
+        }
+    } else if (ok) {
+        if (c0) atomicAdd((u64*)&limbs[d], (u64)c0);
+        if (c1) atomicAdd((u64*)&limbs[d + 1], (u64)c1);
+        if (c2) atomicAdd((u64*)&limbs[d + 2], (u64)c2);
+    }
+}
+
+// ------------------------------------------------------- accumulate pass
+enum : unsigned { F_NAN = AGGF_NAN, F_PINF = AGGF_PINF, F_NINF = AGGF_NINF, F_NNZ = AGGF_NONNEGZERO };
+
+// One aggregate over the wave's rows of one group (peers P, the leader adds)
+// or, with P == 0, each lane with `mine` set adds its own row.
+template <typename T>
+__device__ __forceinline__ void agg_step(const AggCol& ac, u64* rec, long long i, bool mine, u64 P, int leader,
+                                         int lane) {
+    const bool act = mine && valid_at(ac.c, i);
+    T v = (T)0;
+    if constexpr (!__is_same(T, bool)) {
+        if (act) v = ((const T*)ac.c.values)[i];
+    }
+    u64* w = rec + ac.off;
+    const int fn = ac.fn;
+    if (P) {  // wave-reduced: every lane is active here
+        const u64 va = __ballot(act) & P;
+        const unsigned cnt = __builtin_popcountll(va);
+        if (cnt && lane == leader) atomicAdd(&w[0], (u64)cnt);
+        if constexpr (__is_same(T, bool)) {
+            return;
+        } else {
+            if (fn == DFMI_AGG_COUNT || !cnt) return;
+            if (fn == DFMI_AGG_SUM) {
+                if constexpr ((T)0.5 != (T)0) {
+                    const unsigned f = act ? agg_sum_flags(v) : F_NNZ;
+                    const u64 spec = __ballot(act && f != F_NNZ) & P;
+                    if (spec) {
+                        unsigned fl = 0;
+                        if (__ballot(f & F_NAN)) fl |= F_NAN;
+                        if (__ballot(f & F_PINF)) fl |= F_PINF;
+                        if (__ballot(f & F_NINF)) fl |= F_NINF;
+                        if (lane == leader) {
+                            atomicAdd(&w[3], (u64)__builtin_popcountll(spec));
+                            if (fl) atomicOr(&w[1], (u64)fl);
+                        }
+                    }
+                    const double d = (double)v;
+                    const bool ok = act && f == F_NNZ && d != 0.0;
+                    gb_fsum_add((long long*)(w + 4), d, ok, lane, leader);
+                } else {
+                    const u64 x = act ? ((T)-1 < (T)0 ? (u64)(i64)v : (u64)v) : 0ull;
+                    const u64 s = wave_sum(x);
+                    if (lane == leader && s) atomicAdd(&w[3], s);
+                }
+                return;
+            }
+            // MIN / MAX
+            const bool is_min = fn == DFMI_AGG_MIN;
+            const bool nan = act && agg_isnan(v);
+            const u64 nn = __ballot(nan) & P;
+            const bool keyed = act && !nan;
+            const u64 k = keyed ? agg_key(v) : (is_min ? ~0ull : 0ull);
+            const u64 r = is_min ? wave_minmax<true>(k) : wave_minmax<false>(k);
+            if (lane == leader) {
+                if (nn) atomicAdd(&w[3], (u64)__builtin_popcountll(nn));
+                if (__builtin_popcountll(nn) < cnt) {
+                    if (is_min) atomicMin(&w[2], r);
+                    else atomicMax(&w[2], r);
+                }
+            }
+        }
+        return;
+    }
+    if (!act) return;
+    atomicAdd(&w[0], 1ull);
+    if constexpr (!__is_same(T, bool)) {
+        if (fn == DFMI_AGG_COUNT) return;
+        if (fn == DFMI_AGG_SUM) {
+            if constexpr ((T)0.5 != (T)0) {
+                const unsigned f = agg_sum_flags(v);
+                if (f != F_NNZ) {
+                    atomicAdd(&w[3], 1ull);
+                    if (f) atomicOr(&w[1], (u64)f);
+                } else if (v != (T)0) {
+                    lane_fsum_add((long long*)(w + 4), (double)v);
+                }
+            } else {
+                const u64 x = (T)-1 < (T)0 ? (u64)(i64)v : (u64)v;
+                if (x) atomicAdd(&w[3], x);
+            }
+            return;
+        }
+        if (agg_isnan(v)) {
+            atomicAdd(&w[3], 1ull);
+        } else if (fn == DFMI_AGG_MIN) {
+            atomicMin(&w[2], agg_key(v));
+        } else {
+            atomicMax(&w[2], agg_key(v));
+        }
+    }
+}
+
+// Aggregate j of one row (or the peers' rows) by its argument's type.
+__device__ __forceinline__ void agg_dispatch(const AggCol& ac, u64* rec, long long i, bool mine, u64 P, int leader,
+                                             int lane) {
+    switch (ac.c.type) {
+        case 2: return agg_step<i8>(ac, rec, i, mine, P, leader, lane);
+        case 3: return agg_step<i16>(ac, rec, i, mine, P, leader, lane);
+        case 4: return agg_step<i32>(ac, rec, i, mine, P, leader, lane);
+        case 5: return agg_step<i64>(ac, rec, i, mine, P, leader, lane);
+        case 6: return agg_step<u8>(ac, rec, i, mine, P, leader, lane);
+        case 7: return agg_step<u16>(ac, rec, i, mine, P, leader, lane);
+        case 8: return agg_step<u32>(ac, rec, i, mine, P, leader, lane);
+        case 9: return agg_step<u64>(ac, rec, i, mine, P, leader, lane);
+        case 10: return agg_step<float>(ac, rec, i, mine, P, leader, lane);
+        case 11: return agg_step<double>(ac, rec, i, mine, P, leader, lane);
+        default: return agg_step<bool>(ac, rec, i, mine, P, leader, lane);  // COUNT of Boolean / Utf8
+    }
+}
+
+// One wave per 64 consecutive rows. A row whose slot holds its key adds into
+// the group's record; rows of one group within the wave are first reduced
+// across the wave (the group's leader lane adds once per word) as long as the
+// wave finds groups of several rows -- after the second single-row group the
+// remaining rows add their own values (many distinct keys: no reduction pays).
+template <int NK>
+__global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
+    const int lane = threadIdx.x & 63;
+    const Table& t = A.t;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long base = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < A.m; base += stride) {
+        const long long i = base + lane;
+        bool ok = false;
+        unsigned g = 0;
+        if (i < A.m) {
+            const int s = A.sidx[i];
+            if (s >= 0) {
+                RowKey r;
+                (void)row_key<NK>(A.k, i, r);
+                const long long rp = t.rep[s];
+                const bool cur = (unsigned)((unsigned long long)rp >> 32) == A.epoch;
+                const long long rr = (long long)(unsigned)rp;
+                bool same = t.knull[s] == r.nullm;
+                if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
+#pragma unroll
+                    for (int p = 0; p < NK; ++p)
+                        if (r.s[p]) {
+                            u8* dst = A.arena + t.kw[(u64)s * kMaxKeys + p];
+                            for (unsigned j = 0; j < r.len[p]; ++j) dst[j] = r.s[p][j];
+                        }
+                } else {
+#pragma unroll
+                    for (int p = 0; p < NK; ++p) {
+                        if (!same || ((r.nullm >> p) & 1)) continue;
+                        const u64 kwv = t.kw[(u64)s * kMaxKeys + p];
+                        if (r.s[p]) {
+                            const unsigned kl = t.klen[(u64)s * kMaxKeys + p];
+                            const u8* other = cur ? (const u8*)A.k[p].values + A.k[p].offsets[rr] : A.arena + kwv;
+                            same = kl == r.len[p] && bytes_eq(r.s[p], other, kl);
+                        } else {
+                            same = kwv == r.w[p];
+                        }
+                    }
+                }
+                if (same) {
+                    ok = true;
+                    g = t.gid[s];
+                } else {  // two keys, one hash: the host merges this row
+                    const u64 at = atomicAdd(&A.hdr->collided, 1ull);
+                    A.coll_rows[at] = (int)i;
+                }
+            }
+        }
+        u64 active = __ballot(ok);
+        int singles = 0;
+        while (active) {
+            const int l = __builtin_ctzll(active);
+            const unsigned gl = (unsigned)__builtin_amdgcn_readlane((int)g, l);
+            const u64 P = __ballot(ok && ((active >> lane) & 1) && g == gl);
+            if (__builtin_popcountll(P) == 1 && ++singles > 2) break;
+            u64* rec = A.acc + (u64)gl * (u64)A.words;
+            if (lane == l) atomicAdd(&rec[0], (u64)__builtin_popcountll(P));
+            const bool mine = (P >> lane) & 1;
+            for (int j = 0; j < A.naggs; ++j) agg_dispatch(A.a[j], rec, i, mine, P, l, lane);
+            active &= ~P;
+        }
+        if ((active >> lane) & 1) {
+            u64* rec = A.acc + (u64)g * (u64)A.words;
+            atomicAdd(&rec[0], 1ull);
+            for (int j = 0; j < A.naggs; ++j) agg_dispatch(A.a[j], rec, i, true, 0, 0, lane);
+        }
+    }
+}
+
+// ------------------------------------------------------------ maintenance
+// Every used slot of `o` into the (larger, empty) table `n`: same hash word,
+// same group id, representative and persisted key.
+__global__ __launch_bounds__(256) void k_group_rehash(const Table o, const Table n) {
+    const u64 cap = o.mask + 1;
+    for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (u64)gridDim.x * blockDim.x) {
+        const u64 c = o.ctl[s];
+        if (!c) continue;
+        u64 q = gmix(c) & n.mask;
+        while (atomicCAS(&n.ctl[q], 0ull, c) != 0ull) q = (q + 1) & n.mask;
+        n.rep[q] = o.rep[s];
+        n.gid[q] = o.gid[s];
+        n.knull[q] = o.knull[s];
+        for (int p = 0; p < kMaxKeys; ++p) {
+            n.kw[q * kMaxKeys + p] = o.kw[s * kMaxKeys + p];
+            n.klen[q * kMaxKeys + p] = o.klen[s * kMaxKeys + p];
+        }
+    }
+}
+
+// Records [g0, g1) set to the zero state (`pattern`: one record).
+__global__ __launch_bounds__(256) void k_group_init(u64* acc, const u64* pattern, int words, u64 g0, u64 g1) {
+    const u64 w0 = g0 * (u64)words, w1 = g1 * (u64)words;
+    for (u64 w = w0 + (u64)blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += (u64)gridDim.x * blockDim.x)
+        acc[w] = pattern[(w - w0) % (u64)words];
+}
+
+// Carry-normalise every group's exact-sum digits (each digit but the top one
+// back in [0, 2^32)), so the digits absorb another 2^31 rows.
+struct NormArgs {
+    u64* acc;
+    int words;
+    int nf;
+    int foff[kMaxAggs];  // word offsets of the float SUM digits in a record
+    u64 ngroups;
+};
+
+__global__ __launch_bounds__(256) void k_group_normalize(const NormArgs A) {
+    const u64 n = A.ngroups * (u64)A.nf;
+    for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (u64)gridDim.x * blockDim.x) {
+        long long* L = (long long*)(A.acc + (x / A.nf) * (u64)A.words + A.foff[x % A.nf]);
+        for (int i = 0; i < kAggLimbs - 1; ++i) {
+            const long long c = L[i] >> 32;  // floor division by 2^32
+            L[i] -= c * 4294967296ll;
+            L[i + 1] += c;
+        }
+    }
+}
+
+static int grid_for(long long items, int per_block = 256, int cap = 8192) {
+    long long g = (items + per_block - 1) / per_block;
+    return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+hipError_t launch_claim(const ClaimArgs& a, hipStream_t st) {
+    const dim3 g(grid_for(a.m)), b(256);
+    switch (a.nkeys) {
+        case 1: hipLaunchKernelGGL(k_group_claim<1>, g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL(k_group_claim<2>, g, b, 0, st, a); break;
+        case 3: hipLaunchKernelGGL(k_group_claim<3>, g, b, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_group_claim<4>, g, b, 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate(const AccArgs& a, hipStream_t st) {
+    const dim3 g(grid_for(a.m)), b(256);
+    switch (a.nkeys) {
+        case 1: hipLaunchKernelGGL(k_group_accumulate<1>, g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL(k_group_accumulate<2>, g, b, 0, st, a); break;
+        case 3: hipLaunchKernelGGL(k_group_accumulate<3>, g, b, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_group_accumulate<4>, g, b, 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rehash(const Table& o, const Table& n, hipStream_t st) {
+    hipLaunchKernelGGL(k_group_rehash, dim3(grid_for((long long)o.mask + 1)), dim3(256), 0, st, o, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_init(u64* acc, const u64* pattern, int words, u64 g0, u64 g1, hipStream_t st) {
+    if (g1 <= g0) return hipSuccess;
+    hipLaunchKernelGGL(k_group_init, dim3(grid_for((long long)((g1 - g0) * words))), dim3(256), 0, st, acc, pattern,
+                       words, g0, g1);
+    return hipGetLastError();
+}
+
+hipError_t launch_normalize(u64* acc, int words, const int* foff, int nf, u64 ngroups, hipStream_t st) {
+    if (!nf || !ngroups) return hipSuccess;
+    NormArgs a{};
+    a.acc = acc;
+    a.words = words;
+    a.nf = nf;
+    for (int f = 0; f < nf && f < kMaxAggs; ++f) a.foff[f] = foff[f];
+    a.ngroups = ngroups;
+    hipLaunchKernelGGL(k_group_normalize, dim3(grid_for((long long)(ngroups * nf))), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace gb
+}  // namespace dfmi

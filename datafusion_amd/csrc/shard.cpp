@@ -43,6 +43,11 @@ hipError_t launch_rebase_offsets(const int32_t* src, long long n, long long base
 hipError_t launch_place_bits(const uint8_t* src, long long n, uint8_t* dst, long long dst_bit, hipStream_t st);
 }  // namespace dfmi
 
+// aggregate.cpp: every rank's grouped partials merged into the state's shown groups
+int32_t dfmi_agg_state_show_merged(dfmi_agg_state* st, const void* const* partials, const int64_t* sizes, int32_t nparts,
+                                   int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* values, int64_t* num_groups,
+                                   dfmi_error* err);
+
 namespace {
 constexpr int kMaxOut = 16;
 // record per rank: status, error position (evaluation-order key >> 44), rows,
@@ -575,8 +580,9 @@ extern "C" int32_t dfmi_shard_agg_finish_grouped(dfmi_context* ctx, dfmi_shard_c
         c->tp->all_gather(ctx, part.data(), parts_all.data(), (size_t)maxb);
         std::vector<const void*> parts(c->world);
         for (int r = 0; r < c->world; ++r) parts[r] = &parts_all[(size_t)r * maxb];
-        return dfmi_agg_merge_grouped_partials(aggs, n, parts.data(), sizes.data(), c->world, cap, keys, values,
-                                               num_groups, err);
+        (void)aggs;  // the state's own aggregates (the binding passes the same ones)
+        return dfmi_agg_state_show_merged(state, parts.data(), sizes.data(), c->world, cap, keys, values, num_groups,
+                                          err);
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
         return f.code;

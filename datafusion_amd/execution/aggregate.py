@@ -55,14 +55,16 @@ def agg_value_py(v):
 class AggregateRelation(Relation):
     """Aggregate(input, group_expr, aggr_expr) with the input's Selection (if
     any) fused: pulls every batch of `input`, then yields one batch -- the
-    group key column (if any) followed by the aggregates."""
+    group key columns (if any, in group_expr order) followed by the
+    aggregates, one row per group in key order."""
 
     def __init__(self, input: Relation, predicate, aggs: List, schema: Schema, device=None, flags: int = 0,
                  key=None):
         self.input = input
         self.predicate = predicate
         self.aggs = aggs
-        self.key = key
+        # one RuntimeExpr (the single-key form) or a list of them
+        self.keys = None if key is None else (list(key) if isinstance(key, (list, tuple)) else [key])
         self._schema = schema
         self.device = device
         self.flags = flags
@@ -73,20 +75,26 @@ class AggregateRelation(Relation):
             return None
         self.done = True
         eng = engine(self.device)
-        state = eng.agg_state(self.aggs) if self.key is None else eng.grouped_agg_state(self.key, self.aggs)
+        state = eng.agg_state(self.aggs) if self.keys is None else eng.grouped_agg_state(self.keys, self.aggs)
         while True:
             b = self.input.next()
             if b is None:
                 break
             state.add(self.predicate, b, self.flags)
-        if self.key is None:
+        if self.keys is None:
             return RecordBatch(self._schema, [agg_value_array(v) for v in state.finish()])
         keys, vals = state.finish()
         if not keys:
             return None
-        kcol = Array.from_strings(state.key_strings()) if DataType(keys[0].type) == DataType.Utf8 \
-            else agg_values_array(keys)
-        cols = [kcol] + [agg_values_array([g[j] for g in vals]) for j in range(len(self.aggs))]
+        nk = len(self.keys)
+        per_part = [[g[p] for g in keys] for p in range(nk)] if nk > 1 else [keys]
+        cols = []
+        for p, kv in enumerate(per_part):
+            if DataType(kv[0].type) == DataType.Utf8:
+                cols.append(Array.from_strings(state.key_strings(p)))
+            else:
+                cols.append(agg_values_array(kv))
+        cols += [agg_values_array([g[j] for g in vals]) for j in range(len(self.aggs))]
         return RecordBatch(self._schema, cols)
 
     def schema(self) -> Schema:

@@ -421,8 +421,8 @@ class DeviceEngine:
         return AggState(self, aggs)
 
     def grouped_agg_state(self, key, aggs: Sequence) -> "GroupedAggState":
-        """Device accumulators for one Aggregate plan with a GROUP BY key
-        (dfmi_agg_state_create_grouped)."""
+        """Device accumulators for one Aggregate plan with a GROUP BY key, or
+        a list of 1-4 keys (dfmi_agg_state_create_grouped_multi)."""
         return GroupedAggState(self, key, aggs)
 
 
@@ -439,6 +439,10 @@ class AggState:
         err = _abi.dfmi_error()
         if key is None:
             rc = L.dfmi_agg_state_create(eng.ctx, arr, len(self.aggs), C.byref(out), C.byref(err))
+        elif isinstance(key, (list, tuple)):
+            karr = (C.c_void_p * len(key))(*[k.handle.value for k in key])
+            rc = L.dfmi_agg_state_create_grouped_multi(eng.ctx, karr, len(key), arr, len(self.aggs), C.byref(out),
+                                                       C.byref(err))
         else:
             rc = L.dfmi_agg_state_create_grouped(eng.ctx, key.handle, arr, len(self.aggs), C.byref(out), C.byref(err))
         if rc != _abi.DFMI_OK:
@@ -498,35 +502,39 @@ class AggState:
 
 
 class GroupedAggState(AggState):
-    """dfmi_agg_state with a GROUP BY key: finish() returns (keys, values)
-    -- one dfmi_agg_value key per group in key order (null last) and per group
-    the aggregate values."""
+    """dfmi_agg_state with GROUP BY keys: finish() returns (keys, values) --
+    per group in key order (null last, per key part) its key -- one
+    dfmi_agg_value for a single key expression, a list of one per key part
+    for several (`key` given as a list) -- and its aggregate values."""
 
     def __init__(self, eng: DeviceEngine, key, aggs: Sequence):
         super().__init__(eng, aggs, key)
+        self.multi = isinstance(key, (list, tuple))
+        self.nkeys = len(key) if self.multi else 1
 
     def finish(self):
         self.eng.drain()
         self._last = _grouped_call(len(self.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_state_finish_grouped(
-            self.eng.ctx, self.handle, cap, keys, vals, ng, err))
+            self.eng.ctx, self.handle, cap, keys, vals, ng, err), self.nkeys, self.multi)
         return self._last
 
-    def key_strings(self) -> List[Optional[bytes]]:
-        """The Utf8 keys of the groups of the last finish(), in its order
-        (None for the null key): dfmi_agg_state_group_keys_utf8."""
+    def key_strings(self, part: int = 0) -> List[Optional[bytes]]:
+        """The Utf8 key part `part` of the groups of the last finish(), in its
+        order (None for a null key): dfmi_agg_state_group_keys_utf8_part."""
         self.eng.drain()
         L = _abi.lib()
         err = _abi.dfmi_error()
         ln = C.c_int64()
-        L.dfmi_agg_state_group_keys_utf8(self.handle, None, 0, None, 0, C.byref(ln), C.byref(err))
+        L.dfmi_agg_state_group_keys_utf8_part(self.handle, part, None, 0, None, 0, C.byref(ln), C.byref(err))
         keys, _ = self._last
         offs = np.zeros(len(keys) + 1, np.int32)
         data = np.zeros(max(1, ln.value), np.uint8)
-        rc = L.dfmi_agg_state_group_keys_utf8(self.handle, offs.ctypes.data, offs.size, data.ctypes.data, data.size,
-                                              C.byref(ln), C.byref(err))
+        rc = L.dfmi_agg_state_group_keys_utf8_part(self.handle, part, offs.ctypes.data, offs.size, data.ctypes.data,
+                                                   data.size, C.byref(ln), C.byref(err))
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
-        return [None if k.is_null else bytes(data[offs[g]:offs[g + 1]]) for g, k in enumerate(keys)]
+        nulls = [(k[part] if self.multi else k).is_null for k in keys]
+        return [None if nulls[g] else bytes(data[offs[g]:offs[g + 1]]) for g in range(len(keys))]
 
     def partial(self) -> bytes:
         """The exact per-group partial state (dfmi_agg_state_grouped_partial)."""
@@ -543,14 +551,15 @@ class GroupedAggState(AggState):
         return buf.raw[:nb]
 
 
-def _grouped_call(n: int, fn):
+def _grouped_call(n: int, fn, nkeys: int = 1, multi: bool = False):
     """(keys, per-group values) from a grouped finish entry point, growing
-    the capacity to the group count it reports."""
+    the capacity to the group count it reports. keys: per group one
+    dfmi_agg_value, or (multi) a list of nkeys of them."""
     ng = C.c_int64()
     err = _abi.dfmi_error()
     cap = 64
     while True:
-        keys = (_abi.dfmi_agg_value * cap)()
+        keys = (_abi.dfmi_agg_value * (cap * nkeys))()
         vals = (_abi.dfmi_agg_value * (cap * n))()
         rc = fn(cap, keys, vals, C.byref(ng), C.byref(err))
         if rc == _abi.DFMI_ERR_INVALID_ARGUMENT and ng.value > cap:
@@ -559,17 +568,39 @@ def _grouped_call(n: int, fn):
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
         g = ng.value
-        return list(keys[:g]), [list(vals[i * n:(i + 1) * n]) for i in range(g)]
+        ks = [list(keys[i * nkeys:(i + 1) * nkeys]) for i in range(g)] if multi else list(keys[:g])
+        return ks, [list(vals[i * n:(i + 1) * n]) for i in range(g)]
 
 
-def merge_grouped_partials(aggs: Sequence, partials: Sequence[bytes]):
+def merge_grouped_partials(aggs: Sequence, partials: Sequence[bytes], nkeys: int = 1, multi: bool = False):
     """Every shard's per-group partial merged: (keys, per-group values)."""
     arr = (C.c_void_p * len(aggs))(*[a.handle.value for a in aggs])
     bufs = [C.create_string_buffer(p, len(p)) for p in partials]
     parr = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
     sizes = (C.c_int64 * len(bufs))(*[len(p) for p in partials])
     return _grouped_call(len(aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_agg_merge_grouped_partials(
-        arr, len(aggs), parr, sizes, len(bufs), cap, keys, vals, ng, err))
+        arr, len(aggs), parr, sizes, len(bufs), cap, keys, vals, ng, err), nkeys, multi)
+
+
+def merge_grouped_partials_key_strings(aggs: Sequence, partials: Sequence[bytes], part: int, num_groups: int):
+    """The Utf8 key part `part` of the merged groups (merge_grouped_partials'
+    order): dfmi_agg_merge_grouped_partials_keys_utf8 (null keys: b'')."""
+    L = _abi.lib()
+    arr = (C.c_void_p * len(aggs))(*[a.handle.value for a in aggs])
+    bufs = [C.create_string_buffer(p, len(p)) for p in partials]
+    parr = (C.c_void_p * len(bufs))(*[C.addressof(b) for b in bufs])
+    sizes = (C.c_int64 * len(bufs))(*[len(p) for p in partials])
+    err = _abi.dfmi_error()
+    ln = C.c_int64()
+    L.dfmi_agg_merge_grouped_partials_keys_utf8(arr, len(aggs), parr, sizes, len(bufs), part, None, 0, None, 0,
+                                                C.byref(ln), C.byref(err))
+    offs = np.zeros(num_groups + 1, np.int32)
+    data = np.zeros(max(1, ln.value), np.uint8)
+    rc = L.dfmi_agg_merge_grouped_partials_keys_utf8(arr, len(aggs), parr, sizes, len(bufs), part, offs.ctypes.data,
+                                                     offs.size, data.ctypes.data, data.size, C.byref(ln), C.byref(err))
+    if rc != _abi.DFMI_OK:
+        raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+    return [bytes(data[offs[g]:offs[g + 1]]) for g in range(num_groups)]
 
 
 def merge_agg_partials(aggs: Sequence, partials: Sequence[bytes]) -> List[_abi.dfmi_agg_value]:
@@ -679,11 +710,14 @@ class ShardComm:
         return list(out)
 
     def agg_finish_grouped(self, state: "GroupedAggState"):
-        """Every rank's per-group partials merged (collective): (keys, values)."""
+        """Every rank's per-group partials merged (collective): (keys, values);
+        state.key_strings() then reads the merged groups' Utf8 keys."""
         self.eng.drain()
         arr = (C.c_void_p * len(state.aggs))(*[a.handle.value for a in state.aggs])
-        return _grouped_call(len(state.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_shard_agg_finish_grouped(
-            self.eng.ctx, self.handle, state.handle, arr, len(state.aggs), cap, keys, vals, ng, err))
+        state._last = _grouped_call(len(state.aggs), lambda cap, keys, vals, ng, err: _abi.lib().dfmi_shard_agg_finish_grouped(
+            self.eng.ctx, self.handle, state.handle, arr, len(state.aggs), cap, keys, vals, ng, err), state.nkeys,
+            state.multi)
+        return state._last
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -354,6 +354,24 @@ class ScalarFunction(Expr):
                         str=self.name.encode()))
 
 
+@dataclass(frozen=True, eq=True)
+class SortExpr(Expr):
+    """Expr::Sort { expr, asc } (logicalplan.rs:160, Debug :272-278): an
+    ORDER BY key; compile_scalar_expr rejects it (expression.rs:446-449)."""
+    expr: Expr
+    asc: bool
+
+    def get_type(self, schema):
+        return self.expr.get_type(schema)
+
+    def __repr__(self):
+        return "%r %s" % (self.expr, "ASC" if self.asc else "DESC")
+
+    def _postfix(self, out):
+        self.expr._postfix(out)
+        out.append(dict(kind=7, op=1 if self.asc else 0))
+
+
 @dataclass(frozen=True, eq=True, repr=False)
 class AggregateFunction(ScalarFunction):
     def _postfix(self, out):

@@ -1,6 +1,9 @@
-"""Host SQL front end for the executable subset (unchanged semantics of
-src/sqlplanner.rs:45-359 + sqlparser 0.1.8 precedence): 
-``SELECT <expr>, ... FROM <table> [WHERE <expr>]`` -> Projection(Selection?(TableScan)).
+"""Host SQL front end (unchanged semantics of src/sqlplanner.rs:45-359 +
+sqlparser 0.1.8 precedence): ``SELECT <expr>, ... [FROM <table>] [WHERE
+<expr>] [GROUP BY <expr>, ...] [ORDER BY <expr> [ASC|DESC], ...] [LIMIT n]``
+-> Limit?(Sort?(Projection(Selection?(TableScan | EmptyRelation)))) or
+Aggregate(Selection?(TableScan)); the plans' Debug strings are pinned to the
+reference's planner tests (tests/test_planner_debug_cpu.py).
 
 Literal typing (sqlplanner.rs:204-212): integer -> Int64, decimal -> Float64,
 quoted -> Utf8. Binary operators cast both sides to their supertype
@@ -13,7 +16,7 @@ import re
 from typing import List
 
 from .logicalplan import (AggregateFunction, BinaryExpr, Cast, Column, DataType, Float64, Int64, IsNotNull, IsNull,
-                          Literal, Operator, PlanError, Utf8, binary_expr_coerced)
+                          Literal, Operator, PlanError, ScalarFunction, SortExpr, Utf8, binary_expr_coerced)
 
 _TOKEN = re.compile(r"""\s*(?:(?P<num>\d+\.\d*|\.\d+|\d+)|(?P<str>'(?:[^']|'')*')|(?P<op><>|!=|<=|>=|[=<>+\-*/%(),])|(?P<id>[A-Za-z_][A-Za-z0-9_]*))""")
 
@@ -57,7 +60,13 @@ class SqlToRel:
         self.ctx = ctx
 
     def sql_to_rel(self, sql: str):
-        from .execution.context import Projection, Selection, TableScan
+        """sqlplanner.rs:45-180: the input relation (FROM, else EmptyRelation),
+        Selection, then Aggregate (when the projection holds an aggregate) or
+        Projection -> Sort (ORDER BY, resolved against the projection's
+        schema) -> Limit."""
+        from .arrow import Schema
+        from .execution.context import (Aggregate, EmptyRelation, Limit, Projection, Selection, Sort, TableScan,
+                                        exprlist_to_fields)
         self.toks = tokenize(sql)
         self.i = 0
         self._expect("kw", "SELECT")
@@ -70,30 +79,59 @@ class SqlToRel:
                 self.i += 1
                 continue
             break
-        self._expect("kw", "FROM")
-        t = self._next()
-        if t[0] != "id":
-            raise PlanError("expected table name")
-        table = t[1]
-        schema = self.ctx.table_schema(table)
-        if schema is None:
-            raise PlanError("no schema found for table %s" % table)
+        if self._peek() == ("kw", "FROM"):
+            self.i += 1
+            t = self._next()
+            if t[0] != "id":
+                raise PlanError("expected table name")
+            table = t[1]
+            schema = self.ctx.table_schema(table)
+            if schema is None:
+                raise PlanError("no schema found for table %s" % table)
+            plan = TableScan(table, schema)
+        else:  # sqlplanner.rs:58-63
+            schema = Schema([])
+            plan = EmptyRelation(schema)
         where = None
         if self._peek() == ("kw", "WHERE"):
             self.i += 1
             where = self._parse_expr(0, schema)
         group_src = None
-        if self._peek()[0] == "id" and self._peek()[1].upper() == "GROUP":
+        if self._peek_id("GROUP"):
             self.i += 1
-            t = self._next()
-            if t[0] != "id" or t[1].upper() != "BY":
+            if not self._peek_id("BY"):
                 raise PlanError("expected BY")
+            self.i += 1
             group_src = []
             while True:
                 group_src.append(self._parse_expr(0, schema))
                 if self._peek() != ("op", ","):
                     break
                 self.i += 1
+        order_src = []  # (token range, asc)
+        if self._peek_id("ORDER"):
+            self.i += 1
+            if not self._peek_id("BY"):
+                raise PlanError("expected BY")
+            self.i += 1
+            while True:
+                a = self.i
+                self._skip_order_key()
+                b = self.i
+                asc = True
+                if self._peek_id("ASC") or self._peek_id("DESC"):
+                    asc = self._next()[1].upper() == "ASC"
+                order_src.append((a, b, asc))
+                if self._peek() != ("op", ","):
+                    break
+                self.i += 1
+        limit = None
+        if self._peek_id("LIMIT"):
+            self.i += 1
+            t = self._next()
+            if t[0] != "num" or "." in t[1]:
+                raise PlanError("LIMIT parameter is not a number")
+            limit = int(t[1])
         if self.i != len(self.toks):
             raise PlanError("unexpected token %r" % (self.toks[self.i],))
         end = self.i
@@ -106,14 +144,25 @@ class SqlToRel:
             if self.i != b:
                 raise PlanError("bad projection expression")
         self.i = end
-        plan = TableScan(table, schema)
         if where is not None:
             plan = Selection(where, plan)
         aggr = [e for e in exprs if isinstance(e, AggregateFunction)]
         if aggr:  # sqlplanner.rs:80-117: only the aggregate expressions are kept
-            from .execution.context import Aggregate
             return Aggregate(plan, group_src or [], aggr)
-        return Projection(exprs, plan, None)
+        proj_schema = Schema(exprlist_to_fields(exprs, schema))
+        plan = Projection(exprs, plan, proj_schema)
+        if order_src:  # sqlplanner.rs:139-161
+            keys = []
+            for a, b, asc in order_src:
+                self.i = a
+                keys.append(SortExpr(self._parse_expr(0, proj_schema), asc))
+                if self.i != b:
+                    raise PlanError("bad ORDER BY expression")
+            plan = Sort(keys, plan, proj_schema)
+        if limit is not None:  # sqlplanner.rs:163-176
+            plan = Limit(limit, plan, proj_schema)
+        self.i = end
+        return plan
 
     # -- helpers
     def _peek(self):
@@ -128,6 +177,22 @@ class SqlToRel:
         t = self._next()
         if t != (kind, val):
             raise PlanError("expected %s, got %r" % (val, t))
+
+    def _peek_id(self, word):
+        t = self._peek()
+        return t[0] == "id" and t[1].upper() == word
+
+    def _skip_order_key(self):
+        depth = 0
+        while self.i < len(self.toks):
+            t = self.toks[self.i]
+            if t == ("op", "("):
+                depth += 1
+            elif t == ("op", ")"):
+                depth -= 1
+            elif depth == 0 and (t == ("op", ",") or (t[0] == "id" and t[1].upper() in ("ASC", "DESC", "LIMIT"))):
+                return
+            self.i += 1
 
     def _skip_expr(self):
         depth = 0
@@ -223,4 +288,11 @@ class SqlToRel:
             return AggregateFunction(name, tuple(args), args[0].get_type(schema))
         if lname == "count":
             return AggregateFunction(name, tuple(args), DataType.UInt64)
-        raise PlanError("Invalid function '%s'" % name)
+        # a scalar function of the schema provider: each argument cast to the
+        # declared parameter type (sqlplanner.rs:330-350)
+        meta = getattr(self.ctx, "function_meta", None)
+        fm = meta(name) if meta is not None else None
+        if fm is None:
+            raise PlanError("Invalid function '%s'" % name)
+        arg_types, return_type = fm
+        return ScalarFunction(name, tuple(a.cast_to(t, schema) for a, t in zip(args, arg_types)), return_type)

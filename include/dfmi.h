@@ -31,7 +31,7 @@ extern "C" {
  * (arrow ArrayData::offset), dfmi_abi_version(), the caller-owned output form
  * dfmi_filter_project_host_batches_into. A binding compares the library's
  * dfmi_abi_version() with the constant it was built against. */
-#define DFMI_ABI_VERSION 2
+#define DFMI_ABI_VERSION 3
 
 /* DFMI_ABI_VERSION of the loaded library. */
 int32_t dfmi_abi_version(void);
@@ -417,18 +417,22 @@ int32_t dfmi_last_error_order(const dfmi_context* ctx, uint64_t* key);
  *   MIN/MAX(e): NaN values are skipped (a set of only NaNs gives the
  *             canonical NaN), -0.0 orders below +0.0;
  *   SUM/MIN/MAX over no non-null value is null.
- * GROUP BY (dfmi_agg_state_create_grouped): one key of any type the
- * reference's values take -- Boolean, integer, Float32 / Float64 or Utf8;
- * per group the aggregates above. Groups come out in key order (false <
- * true, integers numerically, floats by IEEE 754 totalOrder with one group
- * per bit pattern -- -NaN < -inf < ... < -0.0 < +0.0 < ... < +inf < +NaN, as
- * Rust's total_cmp --, Utf8 bytewise) with the null key last -- the order of
- * the reference's expected/csv_aggregate_by_c_bool.csv. Float and Utf8 keys
- * are merged on the host for every batch (below). A batch whose selected
- * keys lie within 16 consecutive integer values runs the grouped kernel; a
- * wider batch runs the key and the arguments through the fused Selection +
- * Projection pass and is merged into the groups on the host with the same
- * per-row rules (any number of keys per batch and overall).
+ * GROUP BY (dfmi_agg_state_create_grouped / _multi): one to four key
+ * expressions of any type the reference's values take -- Boolean, integer,
+ * Float32 / Float64 or Utf8; per group the aggregates above. Groups come out
+ * in key order, lexicographic over the key parts, each part ordered false <
+ * true, integers numerically, floats by IEEE 754 totalOrder with one group per
+ * bit pattern -- -NaN < -inf < ... < -0.0 < +0.0 < ... < +inf < +NaN, as
+ * Rust's total_cmp --, Utf8 bytewise, with that part's null last -- for one
+ * Boolean key the order of the reference's expected/csv_aggregate_by_c_bool.csv.
+ * One Boolean / integer key: a batch whose selected keys lie within 16
+ * consecutive values runs the fused grouped kernel. Every other batch (wider
+ * integer keys, float or Utf8 keys, several keys) runs the keys and the
+ * arguments through the fused Selection + Projection pass, then a device hash
+ * table (open addressing, one claim pass and one accumulate pass with the
+ * same per-row rules; rows whose key shares its 63-bit hash with another
+ * key's are merged on the host) -- any number of groups per batch and
+ * overall (up to 2^30 per device).
  * ------------------------------------------------------------------------- */
 typedef enum dfmi_agg_fn {       /* AggregateType (expression.rs:33-40) */
     DFMI_AGG_MIN = 0,
@@ -487,24 +491,41 @@ int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, int32_t num_a
  * through dfmi_aggregate_batch. */
 int32_t dfmi_agg_state_create_grouped(dfmi_context* ctx, const dfmi_program* key, const dfmi_aggregate* const* aggs,
                                       int32_t num_aggs, dfmi_agg_state** out, dfmi_error* err);
-/* The groups so far, in key order: keys[g] (type = the key's type, is_null,
- * bits: Boolean 0/1, integers sign/zero-extended; count = the group's selected
- * rows) and values[g * num_aggs + j]. *num_groups is set even when it exceeds
- * `capacity` (then DFMI_ERR_INVALID_ARGUMENT and nothing is written). */
+/* ... with group_expr = keys[0..num_keys) (1 to 4 expressions, the
+ * planner's Vec<Expr>, sqlplanner.rs:97-103), evaluated in that order before
+ * the aggregates' arguments (their errors come first, in that order). */
+int32_t dfmi_agg_state_create_grouped_multi(dfmi_context* ctx, const dfmi_program* const* keys, int32_t num_keys,
+                                            const dfmi_aggregate* const* aggs, int32_t num_aggs, dfmi_agg_state** out,
+                                            dfmi_error* err);
+/* The state's GROUP BY expressions (0: not a grouped state). */
+int32_t dfmi_agg_state_num_keys(const dfmi_agg_state* state);
+/* The groups so far, in key order: keys[g * num_keys + p] for key part p
+ * (type = the part's type, is_null, bits: Boolean 0/1, integers
+ * sign/zero-extended, float bits, Utf8 0 -- the bytes come from
+ * dfmi_agg_state_group_keys_utf8_part; count = the group's selected rows) and
+ * values[g * num_aggs + j]. *num_groups is set even when it exceeds
+ * `capacity` (groups; then DFMI_ERR_INVALID_ARGUMENT and nothing is
+ * written). */
 int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_state* state, int64_t capacity, dfmi_agg_value* keys,
                                       dfmi_agg_value* values, int64_t* num_groups, dfmi_error* err);
-/* The Utf8 keys of the groups of the last dfmi_agg_state_finish_grouped, in
- * the same order, as an arrow BinaryArray: offsets[0..num_groups] (from 0)
- * and the bytes (the null key's slot is empty; keys[g].is_null says which).
- * *data_length is set even when a capacity is too small (then
- * DFMI_ERR_CAPACITY and nothing is written). */
+/* The Utf8 key part `part` of the groups of the last
+ * dfmi_agg_state_finish_grouped (or dfmi_shard_agg_finish_grouped), in the
+ * same order, as an arrow BinaryArray: offsets[0..num_groups] (from 0) and
+ * the bytes (a null key's slot is empty; keys[g * num_keys + part].is_null
+ * says which). *data_length is set even when a capacity is too small (then
+ * DFMI_ERR_CAPACITY and nothing is written). _utf8: part 0. */
+int32_t dfmi_agg_state_group_keys_utf8_part(const dfmi_agg_state* state, int32_t part, int32_t* offsets,
+                                            int64_t num_offsets, uint8_t* data, int64_t data_capacity,
+                                            int64_t* data_length, dfmi_error* err);
 int32_t dfmi_agg_state_group_keys_utf8(const dfmi_agg_state* state, int32_t* offsets, int64_t num_offsets, uint8_t* data,
                                        int64_t data_capacity, int64_t* data_length, dfmi_error* err);
-/* Multi-GPU GROUP BY: the exact per-group partial state (key, the group's
- * selected rows, every aggregate's partial) as host bytes -- size first
- * (negative: -status) -- and the merge of every shard's bytes into the groups
- * one state over all the shards' rows would hold, in key order (output as
- * dfmi_agg_state_finish_grouped). Utf8 keys: NotImplemented. */
+/* Multi-GPU GROUP BY: the exact per-group partial state (every key part --
+ * Utf8 bytes included --, the group's selected rows, every aggregate's
+ * partial) as host bytes -- size first (negative: -status) -- and the merge
+ * of every shard's bytes into the groups one state over all the shards' rows
+ * would hold, in key order (output as dfmi_agg_state_finish_grouped; the
+ * bytes of a Utf8 key part of the merged groups from
+ * dfmi_agg_merge_grouped_partials_keys_utf8, same order). */
 int64_t dfmi_agg_state_grouped_partial_bytes(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
 int32_t dfmi_agg_state_grouped_partial(dfmi_context* ctx, dfmi_agg_state* state, void* host_out, int64_t bytes,
                                        dfmi_error* err);
@@ -512,6 +533,11 @@ int32_t dfmi_agg_merge_grouped_partials(const dfmi_aggregate* const* aggs, int32
                                         const void* const* partials, const int64_t* sizes, int32_t num_partials,
                                         int64_t capacity, dfmi_agg_value* keys, dfmi_agg_value* values,
                                         int64_t* num_groups, dfmi_error* err);
+int32_t dfmi_agg_merge_grouped_partials_keys_utf8(const dfmi_aggregate* const* aggs, int32_t num_aggs,
+                                                  const void* const* partials, const int64_t* sizes,
+                                                  int32_t num_partials, int32_t part, int32_t* offsets,
+                                                  int64_t num_offsets, uint8_t* data, int64_t data_capacity,
+                                                  int64_t* data_length, dfmi_error* err);
 /* Back to the empty state (asynchronous on the context stream): re-running the query. */
 int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* state, dfmi_error* err);
 void dfmi_agg_state_free(dfmi_agg_state* state);

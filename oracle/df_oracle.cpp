@@ -1306,25 +1306,36 @@ int32_t oracle_aggregate(const dfmi_expr_node* pred_nodes, int32_t pred_len, con
     }
 }
 
-// GROUP BY extension: LogicalPlan::Aggregate{group_expr: [key]} (the
-// planner's form, sqlplanner.rs:91-117) -- one Boolean or integer key; per
-// group the aggregates of the no-GROUP-BY form. keys[g] / out[g * n + j] in
-// group order (GroupKey); *num_groups is set even when cap is too small.
-int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_len, const dfmi_expr_node* key_nodes,
-                                 int32_t key_len, const char* const* names, const dfmi_expr_node* const* arg_nodes,
-                                 const int32_t* arg_lens, const int32_t* return_types, int32_t n,
-                                 const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
-                                 uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
-                                 int64_t* num_groups, int32_t* key_offsets, uint8_t* key_data, int64_t key_data_cap,
-                                 dfmi_error* err) {
+// GROUP BY extension: LogicalPlan::Aggregate{group_expr, aggr_expr} (the
+// planner's form, sqlplanner.rs:91-117; group_expr a Vec<Expr>, 1 to 4 keys
+// here) -- per group the aggregates of the no-GROUP-BY form. Groups are
+// ordered lexicographically over the key parts, each part by GroupKey (its
+// null last). keys[g * nkeys + p] / out[g * n + j] in group order; the Utf8
+// bytes of key part `key_part` (if key_offsets) as a BinaryArray;
+// *num_groups is set even when cap is too small. Build-defined (the
+// reference executes no Aggregate): parity unpinned beyond the one-key
+// fixture expected/csv_aggregate_by_c_bool.csv.
+int32_t oracle_aggregate_grouped_multi(const dfmi_expr_node* pred_nodes, int32_t pred_len,
+                                       const dfmi_expr_node* const* key_nodes, const int32_t* key_lens, int32_t nkeys,
+                                       const char* const* names, const dfmi_expr_node* const* arg_nodes,
+                                       const int32_t* arg_lens, const int32_t* return_types, int32_t n,
+                                       const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
+                                       uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
+                                       int64_t* num_groups, int32_t key_part, int32_t* key_offsets, uint8_t* key_data,
+                                       int64_t key_data_cap, dfmi_error* err) {
     try {
         set_err(err, DFMI_OK, "");
         if (!(flags & DFMI_FLAG_EXT_AGGREGATE)) fail(DFMI_ERR_PANIC, "not yet implemented");  // context.rs:161
+        if (nkeys < 1 || nkeys > 4) fail(DFMI_ERR_NOT_IMPLEMENTED, "device program limit: more than 4 GROUP BY expressions");
         Plan p = make_plan(pred_nodes, pred_len, nullptr, nullptr, 0, schema, flags);
-        ExprP kt = build_tree(key_nodes, key_len);
-        Runtime key = compile(*kt, *schema, flags);
-        if (key.t != DFMI_TYPE_BOOLEAN && !is_numeric(key.t) && key.t != DFMI_TYPE_UTF8)
-            fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_name(key.t));
+        std::vector<Runtime> key;
+        for (int k = 0; k < nkeys; ++k) {
+            ExprP kt = build_tree(key_nodes[k], key_lens[k]);
+            key.push_back(compile(*kt, *schema, flags));
+            const int t = key.back().t;
+            if (t != DFMI_TYPE_BOOLEAN && !is_numeric(t) && t != DFMI_TYPE_UTF8)
+                fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("GROUP BY over ") + type_name(t));
+        }
         std::vector<Runtime> args;
         std::vector<AggState> proto(n);
         for (int j = 0; j < n; ++j) {
@@ -1339,39 +1350,60 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
             if (fn != DFMI_AGG_COUNT && !is_numeric(args[j].t))
                 fail(DFMI_ERR_NOT_IMPLEMENTED, std::string("aggregate over ") + type_name(args[j].t));
         }
-        std::map<GroupKey, std::pair<uint64_t, std::vector<AggState>>> groups;
-        std::map<GroupKey, int64_t> rows_of;  // selected rows per group (keys[g].count)
+        struct KeyN {
+            std::vector<GroupKey> k;
+            bool operator<(const KeyN& o) const {
+                for (size_t i = 0; i < k.size(); ++i) {
+                    if (k[i] < o.k[i]) return true;
+                    if (o.k[i] < k[i]) return false;
+                }
+                return false;
+            }
+        };
+        struct Group {
+            std::vector<uint64_t> bits;
+            std::vector<AggState> st;
+            int64_t rows = 0;  // selected rows (keys[g].count)
+        };
+        std::map<KeyN, Group> groups;
         if (batch_rows <= 0) batch_rows = std::max<int64_t>(1, input->num_rows);
         for (int64_t r0 = 0; r0 < input->num_rows; r0 += batch_rows) {
             const int64_t rows = std::min(batch_rows, input->num_rows - r0);
             Batch in = wrap_input(input, r0, rows);
             Batch f = run_batch(p, in, flags);  // FilterRelation::next (or the batch itself)
-            ArrayRef ka = key.f(f);             // the key first, then the aggregates in order
+            std::vector<ArrayRef> ka;           // the keys first, in order, then the aggregates
+            for (int k = 0; k < nkeys; ++k) ka.push_back(key[k].f(f));
             std::vector<ArrayRef> av;
             for (int j = 0; j < n; ++j) av.push_back(args[j].f(f));
             for (int64_t i = 0; i < f.num_rows; ++i) {
-                uint64_t bits;
-                const GroupKey gk = group_key(*ka, i, &bits);
+                KeyN gk;
+                std::vector<uint64_t> bits(nkeys);
+                for (int k = 0; k < nkeys; ++k) gk.k.push_back(group_key(*ka[k], i, &bits[k]));
                 auto it = groups.find(gk);
-                if (it == groups.end()) it = groups.emplace(gk, std::make_pair(bits, proto)).first;
-                for (int j = 0; j < n; ++j) agg_accumulate_row(it->second.second[j], *av[j], i);
-                ++rows_of[gk];
+                if (it == groups.end()) it = groups.emplace(gk, Group{bits, proto, 0}).first;
+                for (int j = 0; j < n; ++j) agg_accumulate_row(it->second.st[j], *av[j], i);
+                ++it->second.rows;
             }
         }
         *num_groups = (int64_t)groups.size();
         if ((int64_t)groups.size() > cap) fail(DFMI_ERR_INVALID_ARGUMENT, "group capacity too small");
         int64_t g = 0, pos = 0;
-        if (key.t == DFMI_TYPE_UTF8 && key_offsets) key_offsets[0] = 0;
+        const bool want_bytes = key_offsets && key_part >= 0 && key_part < nkeys && key[key_part].t == DFMI_TYPE_UTF8;
+        if (want_bytes) key_offsets[0] = 0;
         for (const auto& [gk, v] : groups) {
-            keys[g].type = key.t;
-            keys[g].is_null = gk.null ? 1 : 0;
-            keys[g].bits = v.first;
-            keys[g].count = rows_of[gk];
-            for (int j = 0; j < n; ++j) out[g * n + j] = agg_result(v.second[j]);
-            if (key.t == DFMI_TYPE_UTF8 && key_offsets) {  // the key column as a BinaryArray
-                if (pos + (int64_t)gk.s.size() > key_data_cap) fail(DFMI_ERR_INVALID_ARGUMENT, "key bytes capacity");
-                memcpy(key_data + pos, gk.s.data(), gk.s.size());
-                pos += (int64_t)gk.s.size();
+            for (int k = 0; k < nkeys; ++k) {
+                dfmi_agg_value& kv = keys[g * nkeys + k];
+                kv.type = key[k].t;
+                kv.is_null = gk.k[k].null ? 1 : 0;
+                kv.bits = v.bits[k];
+                kv.count = v.rows;
+            }
+            for (int j = 0; j < n; ++j) out[g * n + j] = agg_result(v.st[j]);
+            if (want_bytes) {  // the key part's column as a BinaryArray
+                const std::string& s = gk.k[key_part].s;
+                if (pos + (int64_t)s.size() > key_data_cap) fail(DFMI_ERR_INVALID_ARGUMENT, "key bytes capacity");
+                memcpy(key_data + pos, s.data(), s.size());
+                pos += (int64_t)s.size();
                 key_offsets[g + 1] = (int32_t)pos;
             }
             ++g;
@@ -1381,6 +1413,21 @@ int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_
         set_err(err, e.code, e.msg);
         return e.code;
     }
+}
+
+// The one-key form: group_expr = [key].
+int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_len, const dfmi_expr_node* key_nodes,
+                                 int32_t key_len, const char* const* names, const dfmi_expr_node* const* arg_nodes,
+                                 const int32_t* arg_lens, const int32_t* return_types, int32_t n,
+                                 const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
+                                 uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
+                                 int64_t* num_groups, int32_t* key_offsets, uint8_t* key_data, int64_t key_data_cap,
+                                 dfmi_error* err) {
+    const dfmi_expr_node* kn[1] = {key_nodes};
+    const int32_t kl[1] = {key_len};
+    return oracle_aggregate_grouped_multi(pred_nodes, pred_len, kn, kl, 1, names, arg_nodes, arg_lens, return_types, n,
+                                          schema, input, batch_rows, flags, cap, keys, out, num_groups, 0, key_offsets,
+                                          key_data, key_data_cap, err);
 }
 
 // Counter-based generator shared with the device (datafusion_amd/csrc/gen.hip).

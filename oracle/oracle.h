@@ -66,6 +66,14 @@ int32_t oracle_aggregate(const dfmi_expr_node* pred_nodes, int32_t pred_len, con
 /* GROUP BY extension: one key (Boolean, integer, float -- totalOrder, one
  * group per bit pattern --, Utf8 -- bytewise, the keys' bytes into
  * key_offsets / key_data); groups in key order, null last. */
+int32_t oracle_aggregate_grouped_multi(const dfmi_expr_node* pred_nodes, int32_t pred_len,
+                                       const dfmi_expr_node* const* key_nodes, const int32_t* key_lens, int32_t nkeys,
+                                       const char* const* names, const dfmi_expr_node* const* arg_nodes,
+                                       const int32_t* arg_lens, const int32_t* return_types, int32_t n,
+                                       const dfmi_schema* schema, const dfmi_batch* input, int64_t batch_rows,
+                                       uint32_t flags, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* out,
+                                       int64_t* num_groups, int32_t key_part, int32_t* key_offsets, uint8_t* key_data,
+                                       int64_t key_data_cap, dfmi_error* err);
 int32_t oracle_aggregate_grouped(const dfmi_expr_node* pred_nodes, int32_t pred_len, const dfmi_expr_node* key_nodes,
                                  int32_t key_len, const char* const* names, const dfmi_expr_node* const* arg_nodes,
                                  const int32_t* arg_lens, const int32_t* return_types, int32_t n,

@@ -54,6 +54,13 @@ def oracle_lib() -> C.CDLL:
                                            C.c_int64, P(_abi.dfmi_agg_value), P(_abi.dfmi_agg_value), P(C.c_int64),
                                            C.c_void_p, C.c_void_p, C.c_int64, P(_abi.dfmi_error)]
     L.oracle_aggregate_grouped.restype = C.c_int32
+    L.oracle_aggregate_grouped_multi.argtypes = [P(_abi.dfmi_expr_node), C.c_int32, P(P(_abi.dfmi_expr_node)),
+                                                 P(C.c_int32), C.c_int32, P(C.c_char_p), P(P(_abi.dfmi_expr_node)),
+                                                 P(C.c_int32), P(C.c_int32), C.c_int32, P(_abi.dfmi_schema),
+                                                 P(_abi.dfmi_batch), C.c_int64, C.c_uint32, C.c_int64,
+                                                 P(_abi.dfmi_agg_value), P(_abi.dfmi_agg_value), P(C.c_int64),
+                                                 C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, P(_abi.dfmi_error)]
+    L.oracle_aggregate_grouped_multi.restype = C.c_int32
     L.oracle_gen_unit_f64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_void_p]
     L.oracle_gen_i64.argtypes = [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_void_p]
     _L = L
@@ -261,3 +268,56 @@ def oracle_aggregate_grouped(schema: Schema, batch: RecordBatch, pred: Optional[
         return res
     strs = [None if keys[i].is_null else bytes(kdata[koff[i]:koff[i + 1]]) for i in range(g)]
     return res + (strs,)
+
+
+def oracle_aggregate_grouped_multi(schema: Schema, batch: RecordBatch, pred: Optional[Expr], keys: Sequence[Expr],
+                                   aggs: Sequence, flags: int = None, batch_rows: int = 0, cap: int = 0):
+    """Aggregate{group_expr: keys}(Selection?(scan)) on the oracle: returns
+    (keys, values, strings) -- per group (key order: lexicographic over the
+    parts, each part's null last) the list of its key parts' dfmi_agg_values,
+    its aggregate values, and per Utf8 key part p strings[p] = the groups'
+    bytes (None for null; None for a non-Utf8 part) -- or raises ExecutionError."""
+    if flags is None:
+        flags = _abi.DFMI_FLAG_EXT_AGGREGATE
+    L = oracle_lib()
+    hb = Batched(batch)
+    sch, keep = _abi.make_schema([(f.name, f.data_type, f.nullable) for f in schema.fields])
+    pn = _abi.PostfixNodes(pred.to_postfix()) if pred is not None else None
+    kns = [_abi.PostfixNodes(k.to_postfix()) for k in keys]
+    nk = len(keys)
+    karr = (C.POINTER(_abi.dfmi_expr_node) * nk)(*[C.cast(x.array, C.POINTER(_abi.dfmi_expr_node)) for x in kns])
+    klens = (C.c_int32 * nk)(*[x.length for x in kns])
+    n = len(aggs)
+    arg_nodes = [_abi.PostfixNodes(a.args[0].to_postfix()) for a in aggs]
+    names = (C.c_char_p * max(1, n))(*[a.name.encode() for a in aggs])
+    arr = (C.POINTER(_abi.dfmi_expr_node) * max(1, n))(*[C.cast(x.array, C.POINTER(_abi.dfmi_expr_node))
+                                                          for x in arg_nodes])
+    lens = (C.c_int32 * max(1, n))(*[x.length for x in arg_nodes])
+    rts = (C.c_int32 * max(1, n))(*[int(a.return_type) for a in aggs])
+    cap = cap or batch.num_rows() + 1
+    kout = (_abi.dfmi_agg_value * (cap * nk))()
+    out = (_abi.dfmi_agg_value * (cap * max(1, n)))()
+    ng = C.c_int64()
+    err = _abi.dfmi_error()
+    koff = np.zeros(cap + 1, np.int32)
+    kcap = 1 << 12
+    for c in batch.columns:
+        if c.data_type == DataType.Utf8:
+            kcap += c.values.numel()
+    kdata = np.zeros(kcap, np.uint8)
+    strings = []
+    for part in range(nk):
+        rc = L.oracle_aggregate_grouped_multi(pn.array if pn else None, pn.length if pn else 0, karr, klens, nk, names,
+                                              arr, lens, rts, n, C.byref(sch), C.byref(hb.cb), batch_rows, flags, cap,
+                                              kout, out, C.byref(ng), part, koff.ctypes.data, kdata.ctypes.data, kcap,
+                                              C.byref(err))
+        if rc != _abi.DFMI_OK:
+            raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
+        g = ng.value
+        if kout[part].type == int(DataType.Utf8) if g else False:
+            strings.append([None if kout[i * nk + part].is_null else bytes(kdata[koff[i]:koff[i + 1]]) for i in range(g)])
+        else:
+            strings.append(None)
+    g = ng.value
+    return ([list(kout[i * nk:(i + 1) * nk]) for i in range(g)], [list(out[i * n:(i + 1) * n]) for i in range(g)],
+            strings)

@@ -10,7 +10,13 @@ include/dfmi.h, as round 4's 48-byte dfmi_column did):
   in include/*.h with the same arity, the same kind per parameter (pointer,
   i32, u32, i64, u64, usize, f64) and the same return kind;
 * every function the headers declare is in the block;
-* the binding's DFMI_ABI_VERSION is the header's and the library's.
+* the binding's DFMI_ABI_VERSION is the header's and the library's;
+* it would compile as written where the reference's own code pins the shape:
+  ExecutionContext::new() stays `-> Self` without a `?` (context.rs:37,
+  csv_sql.rs:36), every block that is a file (has `use` lines) imports the
+  ArrowError / ExecutionError it names, and the fused Projection arm prints
+  the Selection node's `Logical plan:` line the reference's execute prints
+  (context.rs:104) before executing the Selection's input.
 """
 import ctypes as C
 import os
@@ -179,3 +185,46 @@ def test_fusion_is_planned_in_context_not_over_a_trait_object():
     assert "LogicalPlan::Selection { expr: ref p, input: ref sel_input }" in DOC
     assert ".prog()" not in DOC and "get_prog()" in DOC
     assert "prog: Rc<DfmiProgram>" in DOC
+
+
+def _fn_body(text, sig):
+    """The brace-balanced body of the first function whose signature starts with `sig`."""
+    i = text.index(sig)
+    j = text.index("{", i)
+    depth = 0
+    for k in range(j, len(text)):
+        depth += {"{": 1, "}": -1}.get(text[k], 0)
+        if depth == 0:
+            return text[j:k + 1]
+    raise AssertionError("unbalanced " + sig)
+
+
+def test_execution_context_new_is_infallible():
+    """context.rs:37 `pub fn new() -> Self`, called without `?` by csv_sql.rs:36:
+    the binding's new() keeps that signature and does no fallible work."""
+    blocks = [b for b in rust_blocks() if "pub fn new() -> Self" in b]
+    assert blocks, "ExecutionContext::new() -> Self missing"
+    for b in blocks:
+        body = _fn_body(b, "pub fn new() -> Self")
+        assert "?" not in body and "DfmiContext::new" not in body, body
+    assert "ExecutionContext::new()?" not in DOC
+
+
+def test_file_blocks_import_the_error_types_they_name():
+    for b in rust_blocks():
+        if not re.search(r"^use ", b, re.M):
+            continue  # an excerpt of a reference file (context.rs imports ExecutionError itself, :26)
+        uses = " ".join(re.findall(r"^use [^;]*;", b, re.M | re.S))
+        code = re.sub(r"^use [^;]*;", "", b, flags=re.M | re.S)
+        for t in ("ArrowError", "ExecutionError"):
+            if re.search(r"\b%s\b" % t, code):
+                assert re.search(r"\b%s\b" % t, uses), "%s used without an import in:\n%s" % (t, b[:200])
+
+
+def test_fused_arm_prints_the_selection_plan_line():
+    """context.rs:104 prints every plan execute() visits; the fused arm skips
+    execute(Selection), so it prints that line itself, before the input's."""
+    arm = DOC[DOC.index("LogicalPlan::Selection { expr: ref p, input: ref sel_input } => {"):]
+    pr = arm.index('println!("Logical plan: {:?}", input);')
+    ex = arm.index("self.execute(sel_input)?")
+    assert pr < ex
