@@ -1068,6 +1068,111 @@ def c3_line(eng, dev, rank, world, steps, warmup, dist):
                         "Utf8 s (1000-word dictionary, avg %.2f B)" % (nbytes / C3_ROWS), **res}
 
 
+GROUPBY_ROWS = 100_000_000
+GROUPBY_KEYS = 10_000
+
+
+def groupby_line(eng, dev, rank, world, steps, warmup, dist, rows=GROUPBY_ROWS):
+    """GROUP BY on the device (DFMI_FLAG_EXT_AGGREGATE; the reference plans
+    Aggregate{group_expr} (sqlplanner.rs:91-117) but cannot execute it,
+    context.rs:161): SELECT k, SUM(v), COUNT(v) FROM t GROUP BY k over `rows`
+    HBM-resident rows with 10,000 distinct keys -- an Int64 key, a Float64
+    key, a Utf8 key, and the two keys (Int64, Utf8) -- each step one
+    dfmi_aggregate_batch (fused evaluation pass, hash-table claim and
+    accumulate passes) plus the finish (every group back in key order).
+    Exact Float64 SUM. Gate: a 2^20-row prefix against the oracle, keys and
+    values bit for bit. Atomic-bound (scattered 8-byte atomics into the
+    groups' records), not HBM-bound: `roofline` reports the algorithmic bytes'
+    rate only for scale."""
+    from datafusion_amd.arrow import Array, RecordBatch
+    from datafusion_amd.execution.expression import compile_expr
+    from datafusion_amd.logicalplan import AggregateFunction
+    from oracle_ffi import oracle_aggregate_grouped_multi
+    AGGF = _abi.DFMI_FLAG_EXT_AGGREGATE
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + 77 + rank)
+    n = rows
+    ki = torch.randint(0, GROUPBY_KEYS, (n,), device=dev, generator=g)
+    v = torch.rand(n, device=dev, dtype=torch.float64, generator=g)
+    words = [b"k%d_" % i + b"x" * (i % 13) for i in range(GROUPBY_KEYS)]
+    dict_bytes = torch.tensor(np.frombuffer(b"".join(words), dtype=np.uint8), device=dev)
+    dict_len = torch.tensor([len(w) for w in words], dtype=torch.int64, device=dev)
+    dict_off = torch.cumsum(dict_len, 0) - dict_len
+    lens = dict_len[ki]
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    data = torch.empty(int(offs[-1].item()), dtype=torch.uint8, device=dev)
+    for r0 in range(0, n, 1 << 24):
+        r1 = min(n, r0 + (1 << 24))
+        row = torch.repeat_interleave(torch.arange(r0, r1, device=dev), lens[r0:r1])
+        within = torch.arange(row.numel(), device=dev) - (offs[row] - offs[r0])
+        data[offs[r0]:offs[r1]] = dict_bytes[dict_off[ki[row]] + within]
+    utf8 = Array(DataType.Utf8, n, data, None, offs.to(torch.int32), 0)
+    kint = (ki * 7919 - 5000).contiguous()
+    kflt = (ki.to(torch.float64) / 7.0).contiguous()
+    vv = Array(DataType.Float64, n, v.view(torch.uint8))
+    cases = {
+        "int64": [Array(DataType.Int64, n, kint.view(torch.uint8))],
+        "float64": [Array(DataType.Float64, n, kflt.view(torch.uint8))],
+        "utf8": [utf8],
+        "int64_utf8": [Array(DataType.Int64, n, (ki % 100).contiguous().view(torch.uint8)), utf8],
+    }
+    out = {"workload": "SELECT k, SUM(v), COUNT(v) FROM t GROUP BY k: %d rows per GPU, %d distinct keys, v Float64 "
+                       "(exact SUM)" % (n, GROUPBY_KEYS)}
+    for name, kcols in cases.items():
+        nk = len(kcols)
+        schema = Schema([Field("k%d" % i, c.data_type, False) for i, c in enumerate(kcols)] +
+                        [Field("v", DataType.Float64, False)])
+        batch = RecordBatch(schema, kcols + [vv])
+        aggs_e = [AggregateFunction("SUM", (Column(nk),), DataType.Float64),
+                  AggregateFunction("COUNT", (Column(nk),), DataType.UInt64)]
+        aggs = [compile_expr(None, a, schema, AGGF) for a in aggs_e]
+        keys = [compile_scalar_expr(None, Column(i), schema, AGGF) for i in range(nk)]
+        res = {}
+
+        def step():
+            st = eng.grouped_agg_state(keys, aggs)
+            st.add(None, batch, AGGF)
+            k, vals = st.finish()
+            res["groups"] = len(k)
+            return len(k)
+
+        el, _, groups = timed_steps(step, steps, warmup, dist, eng, dev, py_exchange=False)
+        # gate: a 2^20-row prefix against the oracle
+        m = 1 << 20
+        pre = RecordBatch(schema, [_prefix(c, m) for c in kcols] + [_prefix(vv, m)])
+        st = eng.grouped_agg_state(keys, aggs)
+        st.add(None, pre, AGGF)
+        dk, dv = st.finish()
+        rk, rv, rs = oracle_aggregate_grouped_multi(schema, pre.to("cpu"), None, [Column(i) for i in range(nk)],
+                                                    aggs_e, AGGF)
+        ok = [[(x.is_null, x.bits, x.count) for x in gk] for gk in dk] == \
+             [[(x.is_null, x.bits, x.count) for x in gk] for gk in rk]
+        ok = ok and [[(x.is_null, x.bits, x.count) for x in gv] for gv in dv] == \
+            [[(x.is_null, x.bits, x.count) for x in gv] for gv in rv]
+        for p, strs in enumerate(rs):
+            if strs is not None:
+                ok = ok and st.key_strings(p) == strs
+        kb = sum(4 + float(c.values.numel()) / n if c.data_type == DataType.Utf8 else c.data_type.width for c in kcols)
+        bpr = kb + 8.0
+        ms = el / steps * 1e3
+        out[name] = {"rows_per_s": n * world * steps / el, "ms_per_step": round(ms, 3), "groups": groups,
+                     "parity_gate": {"rows": m, "groups": len(rk), "bit_identical_to_oracle": bool(ok)},
+                     "algorithmic_bytes_per_row": round(bpr, 3),
+                     "achieved_gbs": round(n * bpr / (ms * 1e-3) / 1e9, 1),
+                     "bound": "device atomics into the groups' records (not HBM)"}
+    del utf8, data, offs, cases
+    return out
+
+
+def _prefix(a, m):
+    """The first m rows of an offset-0 device Array (a view)."""
+    from datafusion_amd.arrow import Array
+    if a.data_type == DataType.Utf8:
+        return Array(a.data_type, m, a.values, None, a.offsets[: m + 1], 0)
+    return Array(a.data_type, m, a.values[: m * a.data_type.width], None, None, 0)
+
+
 HOST_ROWS = 100_000_000
 
 
@@ -1228,8 +1333,8 @@ def main():
     ap.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
     ap.add_argument("--sel", type=float, default=0.5, help="headline selectivity")
     ap.add_argument("--sweep", default="0.01,0.5,0.99", help="selectivities also reported (first=headline if set)")
-    ap.add_argument("--extra", default="c4,q6,c2i64,c3,batches",
-                    help="extra config lines (comma list: c4,q6,c2i64,c3,batches,host,csv; empty = none)")
+    ap.add_argument("--extra", default="c4,q6,c2i64,c3,groupby,batches",
+                    help="extra config lines (comma list: c4,q6,c2i64,c3,groupby,batches,host,csv; empty = none)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", choices=("abi", "torch"), default=None,
                     help="N>1 exchange: the C-ABI RCCL path (dfmi_shard_filter_project, default under nccl) or "
@@ -1319,6 +1424,8 @@ def main():
                 extra["csv"] = csv_line(eng, min(args.steps, 3), 1)
         elif name == "c3":
             extra["c3"] = c3_line(eng, dev, rank, world, args.steps, args.warmup, dist)
+        elif name == "groupby":
+            extra["groupby"] = groupby_line(eng, dev, rank, world, min(args.steps, 5), 1, dist)
         else:
             raise SystemExit("unknown extra config %r" % name)
         torch.cuda.empty_cache()

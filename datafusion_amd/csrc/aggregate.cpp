@@ -1005,16 +1005,16 @@ void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
             const uint64_t* w = rec + H.off[j];
             Partial& q = parts[j];
             const int fn = st->aggs[j]->fn;
-            q.count = w[0];
+            q.count = rec[0] - w[0];  // the group's rows minus its NULL arguments
             if (fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type)) {
-                q.flags = w[1] | (w[0] > w[3] ? AGGF_NONNEGZERO : 0);
+                q.flags = w[1] | (q.count > w[3] ? AGGF_NONNEGZERO : 0);
                 for (int i = 0; i < kAggLimbs; ++i) q.limbs[i] = (int64_t)w[4 + i];
                 normalize(q);
             } else if (fn == DFMI_AGG_SUM) {
                 q.isum = w[3];
             } else if (fn == DFMI_AGG_MIN || fn == DFMI_AGG_MAX) {
                 q.key = w[2];
-                q.flags = (w[3] ? AGGF_NAN : 0) | (w[0] > w[3] ? AGGF_VALUE : 0);
+                q.flags = (w[3] ? AGGF_NAN : 0) | (q.count > w[3] ? AGGF_VALUE : 0);
             }
         }
         merge_group(group_entry(st->groups, std::move(hk), n), parts, st->aggs.data(), n);

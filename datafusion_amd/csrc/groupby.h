@@ -84,9 +84,11 @@ struct AggCol {
 };
 
 // A group's accumulator record: word 0 = the group's rows, then per
-// aggregate [count, flags, key, aux] (+ kAggLimbs exact-sum digits for a
-// floating-point SUM). aux: integer SUM the wrapping sum; MIN / MAX the NaN
-// values seen; float SUM the values that are not finite-and-not-(-0.0).
+// aggregate [nulls, flags, key, aux] (+ kAggLimbs exact-sum digits for a
+// floating-point SUM): nulls = the group's rows whose argument is NULL (the
+// non-null count is rows - nulls: no atomic per row for it); aux: integer
+// SUM the wrapping sum; MIN / MAX the NaN values seen; float SUM the values
+// that are not finite-and-not-(-0.0).
 struct AccArgs {
     Col k[kMaxKeys];
     int32_t nkeys;

@@ -219,7 +219,9 @@ __device__ __forceinline__ void agg_step(const AggCol& ac, u64* rec, long long i
     if (P) {  // wave-reduced: every lane is active here
         const u64 va = __ballot(act) & P;
         const unsigned cnt = __builtin_popcountll(va);
-        if (cnt && lane == leader) atomicAdd(&w[0], (u64)cnt);
+        // word 0 counts the group's NULL values (non-null count = rows - nulls)
+        if (cnt != (unsigned)__builtin_popcountll(P) && lane == leader)
+            atomicAdd(&w[0], (u64)(__builtin_popcountll(P) - cnt));
         if constexpr (__is_same(T, bool)) {
             return;
         } else {
@@ -265,8 +267,10 @@ __device__ __forceinline__ void agg_step(const AggCol& ac, u64* rec, long long i
         }
         return;
     }
-    if (!act) return;
-    atomicAdd(&w[0], 1ull);
+    if (!act) {
+        if (mine) atomicAdd(&w[0], 1ull);  // a NULL value
+        return;
+    }
     if constexpr (!__is_same(T, bool)) {
         if (fn == DFMI_AGG_COUNT) return;
         if (fn == DFMI_AGG_SUM) {

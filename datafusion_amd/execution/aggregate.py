@@ -87,7 +87,7 @@ class AggregateRelation(Relation):
         if not keys:
             return None
         nk = len(self.keys)
-        per_part = [[g[p] for g in keys] for p in range(nk)] if nk > 1 else [keys]
+        per_part = [[g[p] for g in keys] for p in range(nk)]  # (the state is created with the key list)
         cols = []
         for p, kv in enumerate(per_part):
             if DataType(kv[0].type) == DataType.Utf8:

@@ -4,10 +4,13 @@
 rocprofv3 kernel trace, the kernel's resources (VGPRs, SGPRs, scratch, LDS),
 and its HBM traffic per launch from the separate FETCH_SIZE / WRITE_SIZE PMC
 passes, corrected as MI355X_MICROARCH.md "HBM" prescribes: FETCH_SIZE and
-WRITE_SIZE are KiB; on gfx950 FETCH_SIZE tallies 128-byte streaming read
-requests at 64 bytes, so it is doubled (exact for wide coalesced streams; a
-sparse gather of sub-128-byte pieces is over-stated by up to 2x -- noted per
-kernel as `read_correction`). Query kernels are named per shape
+WRITE_SIZE are KiB; on gfx950 FETCH_SIZE tallies 128-byte read requests at
+64 bytes, so it is doubled. Calibrated (tools/membw_masked.hip,
+profiles/r06/calib_masked/summary.txt) for 8-byte streaming loads and for
+lane-masked 8-byte loads: FETCH_SIZE x 2 = 128 B x the 128-byte lines that
+hold a loaded row, exactly; a line loaded again after it left the L2 counts
+again (Infinity-Cache hits included), so these are memory-side request
+bytes, an upper bound on HBM bytes. Query kernels are named per shape
 (dfmi_<filter|project|agg>_<hash>, jit.cpp), so every bench line's kernel has
 its own row. Writes <dir>/traffic.json, which bench.py reads to report
 roofline.traffic next to the formula bytes.
