@@ -325,6 +325,10 @@ void build_plan_impl(const dfmi_program* pred, const dfmi_program* const* projs,
             X.eq_dense = std::max(0, std::min(1024, atoi(e)));
             if (X.eq_dense) X.waves_per_eu = 0;  // LDS-limited occupancy: no register hint
         }
+        if (const char* e = getenv("DFMI_UTF8_EQ_REG")) {  // register-resident dense equality: G slices per round
+            const int g = atoi(e);
+            if (g == 1 || g == 2 || g == 4 || g == 8) X.eq_dense = X.K % g == 0 ? -g : 0;
+        }
         if (const char* e = getenv("DFMI_UTF8_RING"))  // 0: off; > 0: on (slot chunks) where it applies
             if (pred && X.utf8_outs.size() == 1 && !X.pred_slots.empty() && X.M == 1) {
                 X.ring = atoi(e) > 1 ? atoi(e) : (atoi(e) == 1 ? kRingSlot : 0);

@@ -616,7 +616,11 @@ static std::vector<int> emit_predicate(Gen& g, std::ostringstream& o, const Plan
     for (const auto& pe : g.pre_eq) load_offs(std::get<1>(pe));
     for (int u : extra_offs) load_offs(u);
     for (const auto& [arr, u, sl] : g.pre_eq)
-        if (X.eq_dense)
+        if (X.eq_dense < 0)
+            pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile_reg<BLOCK, K, " << -X.eq_dense << ">(A, " << u << ", "
+                << sl << ", A0.str + A0.str_off[" << sl << "], us" << offs_name(u) << ", ux" << offs_name(u) << ", lane, "
+                << arr << ");\n";
+        else if (X.eq_dense)
             pre << "  bool " << arr << "[K];\n  dfmi::utf8_eq_lit_tile_dense<BLOCK, K, " << X.eq_dense << ">(A, " << u << ", "
                 << sl << ", A0.str + A0.str_off[" << sl << "], us" << offs_name(u) << ", ux" << offs_name(u) << ", lane, "
                 << arr << ", EQA[wave]);\n";
@@ -1084,7 +1088,7 @@ std::string generate(const Plan& P, Launch& X) {
         // tile a block waits on in the look-back is running or done)
         if (X.ring)
             o << "  __shared__ dfmi::Utf8Ring<" << X.ring << "> RG;\n";
-        if (X.eq_dense) o << "  __shared__ uint4 EQA[WAVES][" << X.eq_dense << "];\n";
+        if (X.eq_dense > 0) o << "  __shared__ uint4 EQA[WAVES][" << X.eq_dense << "];\n";
         if (!X.utf8_outs.empty() && X.gather && X.gather != 3 && X.gather != 6 && !(X.ring && X.utf8_outs.size() == 1))
             o << "  constexpr int ARENA = " << X.arena << ";\n  __shared__ dfmi::Utf8Stage<ARENA, "
               << (X.gather == 1 ? 32 : X.gather == 5 ? 72 : X.gather == 2 ? 129 : X.image) << "> G[WAVES];\n";

@@ -79,7 +79,8 @@ struct Launch {
     // (jit_skeleton.hip "ring-staged Utf8 gather"); ring = chunks per slot
     int ring = 0;
     // Utf8 `col = literal` predicates: stage the wave's whole source spans into
-    // an LDS arena of eq_dense 16-byte chunks and compare from there (diagnostic A/B)
+    // an LDS arena of eq_dense 16-byte chunks and compare from there (diagnostic A/B);
+    // < 0: the register-resident dense form, -eq_dense slices' spans per load round
     int eq_dense = 0;
     // Utf8 gather: the per-lane fallback copy (a slice whose span is over the
     // stage) as register-light unaligned 16-/4-byte moves instead of

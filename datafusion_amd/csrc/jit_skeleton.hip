@@ -982,6 +982,82 @@ __device__ __forceinline__ void utf8_eq_lit_tile_dense(const Args& A, int u, int
     wave_lds_fence();  // the arena is reused by the next sub-tile
 }
 
+// Register-resident dense form of utf8_eq_lit_tile (Launch::eq_dense < 0,
+// diagnostic A/B): each 64-row slice's whole source span
+// is read with ONE coalesced 16-byte load per lane (a span of at most 64
+// chunks: ~888 B at C3's strings), G slices' loads in flight together, no
+// LDS; an equal-length candidate takes the words holding its first bytes
+// from the lanes that loaded them (ds_bpermute of the four dwords of the
+// owning lane, plus the next lane's first dword for a head that crosses it).
+// A slice whose span needs more than 64 chunks fetches its candidates' head
+// words from global memory, as utf8_eq_lit_tile does.
+template <int BLOCK, int K, int G>
+__device__ __forceinline__ void utf8_eq_lit_tile_reg(const Args& A, int u, int lit, const char* q, const int (&s)[K],
+                                                     const int (&nx)[K], int lane, bool (&res)[K]) {
+    const int len = A.str_len[lit];
+    const u8* by = A.bytes[u];
+    const int sm = (int)((u64)by & 15u);
+    const int hn = len < 4 ? len : 4;
+    const unsigned hm = hn == 4 ? ~0u : ((1u << (8 * hn)) - 1u);
+    const unsigned bmis = (unsigned)((u64)by & 3u);
+    unsigned qh = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < hn) qh |= (unsigned)(u8)q[i] << (8 * i);
+#pragma unroll
+    for (int g0 = 0; g0 < K; g0 += G) {
+        uint4 v[G];
+        int c0[G];
+        bool fits[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int k = g0 + j;
+            v[j] = make_uint4(0u, 0u, 0u, 0u);
+            const int s0 = __builtin_amdgcn_readfirstlane(s[k]), s1 = __builtin_amdgcn_readfirstlane(nx[k]);
+            c0[j] = (int)((((i64)s0 + sm) & ~15ll) - sm);
+            const int nch = s1 > s0 ? (int)(((i64)s1 - 1 - c0[j]) >> 4) + 1 : 0;
+            fits[j] = nch <= 64;
+            if (fits[j] && lane < nch) v[j] = *at<uint4>(by, (i64)c0[j] + 16 * lane);
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int k = g0 + j;
+            const int e = utf8_end(s[k], nx[k], lane);
+            const bool cand = e - s[k] == len && hn > 0;
+            unsigned w = qh;
+            if (fits[j]) {
+                const int rel = cand ? s[k] - c0[j] : 0;  // byte of the head in the span
+                const int dw = rel >> 2, src = dw >> 2, comp = dw & 3;
+                const int a0 = src << 2, a1 = (src + 1 < 64 ? src + 1 : 63) << 2;
+                const unsigned x = (unsigned)__builtin_amdgcn_ds_bpermute(a0, (int)v[j].x);
+                const unsigned y = (unsigned)__builtin_amdgcn_ds_bpermute(a0, (int)v[j].y);
+                const unsigned z = (unsigned)__builtin_amdgcn_ds_bpermute(a0, (int)v[j].z);
+                const unsigned ww = (unsigned)__builtin_amdgcn_ds_bpermute(a0, (int)v[j].w);
+                const unsigned nxw = (unsigned)__builtin_amdgcn_ds_bpermute(a1, (int)v[j].x);
+                const unsigned w0 = comp == 0 ? x : comp == 1 ? y : comp == 2 ? z : ww;
+                const unsigned w1 = comp == 0 ? y : comp == 1 ? z : comp == 2 ? ww : nxw;
+                if (cand) w = __builtin_amdgcn_alignbyte(w1, w0, (unsigned)(rel & 3));
+            } else if (cand) {  // span over 64 chunks: the head words from global memory
+                const unsigned sk = (unsigned)s[k];
+                const unsigned mis = (sk + bmis) & 3u;
+                const unsigned w0 = *at<unsigned>(by, sk - mis);
+                const unsigned w1 = *at<unsigned>(by, sk - mis + ((mis + (unsigned)hn - 1u) & ~3u));
+                w = __builtin_amdgcn_alignbyte(w1, w0, mis);
+            }
+            bool eq = cand && (w & hm) == qh;
+            if (eq) {
+                const u8* p = by + s[k];
+                for (int i = hn; i < len; ++i)
+                    if (p[i] != (u8)q[i]) {
+                        eq = false;
+                        break;
+                    }
+            }
+            res[k] = len == 0 ? e - s[k] == 0 : eq;
+        }
+    }
+}
+
 // OR v into the LDS word p (no return value). Through inline asm: the
 // compiler's wait-count pass, which does not see the explicit vmcnt wait
 // after each staging round, otherwise puts an s_waitcnt vmcnt(0) before

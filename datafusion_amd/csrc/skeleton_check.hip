@@ -27,6 +27,9 @@ extern "C" __global__ __launch_bounds__(512) void dfmi_skeleton_check(const dfmi
     bool eq[K];
     dfmi::utf8_offs_tile<BLOCK, K>(A, 0, base, lane, wave, ~0u, us, ue);
     dfmi::utf8_eq_lit_tile<BLOCK, K>(A, 0, 0, A.str + A.str_off[0], us, ue, lane, eq);
+    bool eq2[K];
+    dfmi::utf8_eq_lit_tile_reg<BLOCK, K, 4>(A, 0, 0, A.str + A.str_off[0], us, ue, lane, eq2);
+    for (int k = 0; k < K; ++k) eq[k] = eq[k] || eq2[k];
     for (int k = 0; k < K; ++k) {
         selm |= (unsigned)eq[k] << k;
         wm[k] = __ballot((selm >> k) & 1);

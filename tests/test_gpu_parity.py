@@ -429,6 +429,18 @@ def test_utf8_equality_dense_variant(monkeypatch, chunks):
     test_utf8_many_tiles()
 
 
+@pytest.mark.parametrize("group", ["4", "8", "1"])
+def test_utf8_equality_register_variant(monkeypatch, group):
+    """Utf8 `col = literal` with each slice's span in registers (one 16-byte
+    load per lane, the candidates' head words by ds_bpermute;
+    DFMI_UTF8_EQ_REG: slices per load round; long strings' slices over 64
+    chunks take the global head loads) against the oracle."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_UTF8_EQ_REG", group)
+    test_utf8_gather_and_equality()
+    test_utf8_many_tiles()
+
+
 @pytest.mark.parametrize("variant", ["3", "2", "0", "4", "1", "5", "4p", "5p", "4d", "4dp", "4q", "4w", "4wd", "6", "6g1", "6g4"])
 def test_utf8_gather_variants(monkeypatch, variant):
     """The Utf8 gather variants (DFMI_UTF8_GATHER under DFMI_DIAG: 3 = two
