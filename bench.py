@@ -250,7 +250,8 @@ def timed_steps(step, steps, warmup, dist, eng, dev, py_exchange=True):
     selected = 0
     for _ in range(steps):
         selected = step()
-        kern_ms.append(eng.last_timing()[1])
+        t = eng.last_timing()  # (None where the step's last call times no kernel)
+        kern_ms.append(t[1] if t else 0.0)
         if dist and py_exchange:  # per-GPU selected counts -> global output offsets
             exchange_counts([selected])
     torch.cuda.synchronize(dev)

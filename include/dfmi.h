@@ -181,7 +181,7 @@ typedef struct dfmi_expr_node {
                                            commented out in the reference): the operand's
                                            validity as a non-null Boolean */
 
-#define DFMI_FLAG_EXT_AGGREGATE    0x10u /* LogicalPlan::Aggregate without GROUP BY
+#define DFMI_FLAG_EXT_AGGREGATE    0x10u /* LogicalPlan::Aggregate, with or without GROUP BY
                                            (sqlplanner.rs:91-117, compile_expr
                                            expression.rs:81-116) instead of the
                                            executor's unimplemented!() (context.rs:161):
