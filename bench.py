@@ -1129,14 +1129,25 @@ def groupby_line(eng, dev, rank, world, steps, warmup, dist, rows=GROUPBY_ROWS):
                   AggregateFunction("COUNT", (Column(nk),), DataType.UInt64)]
         aggs = [compile_expr(None, a, schema, AGGF) for a in aggs_e]
         keys = [compile_scalar_expr(None, Column(i), schema, AGGF) for i in range(nk)]
-        res = {}
+        # the calls the Rust AggregateRelation makes (INTEGRATION.md "Aggregate"), on a state
+        # created once per plan: reset, one batch, the groups into caller-owned arrays
+        L = _abi.lib()
+        st = eng.grouped_agg_state(keys, aggs)
+        cb, keep = eng._batch_struct(batch)
+        cap = 2 * GROUPBY_KEYS
+        kout = (_abi.dfmi_agg_value * (cap * nk))()
+        vout = (_abi.dfmi_agg_value * (cap * len(aggs)))()
+        ngr = C.c_int64()
+        err = _abi.dfmi_error()
 
         def step():
-            st = eng.grouped_agg_state(keys, aggs)
-            st.add(None, batch, AGGF)
-            k, vals = st.finish()
-            res["groups"] = len(k)
-            return len(k)
+            rc = L.dfmi_agg_state_reset(eng.ctx, st.handle, C.byref(err))
+            rc = rc or L.dfmi_aggregate_batch(eng.ctx, st.handle, None, C.byref(cb), AGGF, C.byref(err))
+            rc = rc or L.dfmi_agg_state_finish_grouped(eng.ctx, st.handle, cap, kout, vout, C.byref(ngr),
+                                                       C.byref(err))
+            if rc != 0:
+                raise RuntimeError(err.message.decode())
+            return ngr.value
 
         el, _, groups = timed_steps(step, steps, warmup, dist, eng, dev, py_exchange=False)
         # gate: a 2^20-row prefix against the oracle

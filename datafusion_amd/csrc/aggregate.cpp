@@ -223,8 +223,14 @@ double round_exact(const Partial& p, int prec, int qmin, double overflow_limit, 
     uint64_t mant = 0;
     for (int i = msb; i >= q; --i) mant = (mant << 1) | bit(i);
     const uint64_t rb = q >= 1 ? bit(q - 1) : 0;
+    // sticky: any set bit below the round bit, bits [0, q - 2] (whole digits first)
     bool sticky = false;
-    for (int i = q - 2; i >= 0 && !sticky; --i) sticky = bit(i);
+    if (q >= 2) {
+        const int hb = q - 2, hd = hb >> 5;
+        for (int i = 0; i < hd && !sticky; ++i) sticky = d[i] != 0;
+        const uint64_t m = (hb & 31) == 31 ? 0xffffffffull : ((1ull << ((hb & 31) + 1)) - 1);
+        sticky = sticky || ((uint64_t)d[hd] & m) != 0;
+    }
     if (rb && (sticky || (mant & 1))) {
         ++mant;
         if (mant >> prec) {
