@@ -6,7 +6,8 @@ Float64 keys (10,000 values), Utf8 keys (1,000 words and 10,000 words), two
 keys Int64 x Utf8 (the device hash table: aggregate.cpp group_batch_hashed)
 -- each timed end to end (state creation excluded, finish included) after a
 warm-up, and the host-merge A/B (DFMI_DIAG=1 DFMI_GROUP_HOST=1) on the same
-batches. usage: groupby_probe.py [rows] [--no-host]"""
+batches; --sweep: Float64 keys of 4 ... 1e6 distinct values instead.
+usage: groupby_probe.py [rows] [--no-host] [--sweep]"""
 import os
 import sys
 import time
@@ -31,15 +32,19 @@ eng = engine()
 dev = eng.device
 v = Array.from_numpy(DataType.Float64, rng.random(n)).to(dev)
 words = [("w%d_" % i + "x" * (i % 17)) for i in range(10_000)]
-cases = {
-    "int64 window": [Array.from_numpy(DataType.Int64, rng.integers(0, 16, n))],
-    "int64 10k": [Array.from_numpy(DataType.Int64, rng.integers(0, 10_000, n) * 7919)],
-    "float64 10k": [Array.from_numpy(DataType.Float64, rng.integers(0, 10_000, n) / 7.0)],
-    "utf8 1k": [Array.from_strings([words[i] for i in rng.integers(0, 1000, n)])],
-    "utf8 10k": [Array.from_strings([words[i] for i in rng.integers(0, 10_000, n)])],
-    "int64 x utf8 10k": [Array.from_numpy(DataType.Int64, rng.integers(0, 100, n)),
-                         Array.from_strings([words[i] for i in rng.integers(0, 100, n)])],
-}
+if "--sweep" in sys.argv:  # the hash table across key cardinalities (Float64 keys: always the hash path)
+    cases = {"float64 %d" % c: [Array.from_numpy(DataType.Float64, rng.integers(0, c, n) / 7.0)]
+             for c in (4, 16, 100, 1000, 10_000, 100_000, 1_000_000)}
+else:
+    cases = {
+        "int64 window": [Array.from_numpy(DataType.Int64, rng.integers(0, 16, n))],
+        "int64 10k": [Array.from_numpy(DataType.Int64, rng.integers(0, 10_000, n) * 7919)],
+        "float64 10k": [Array.from_numpy(DataType.Float64, rng.integers(0, 10_000, n) / 7.0)],
+        "utf8 1k": [Array.from_strings([words[i] for i in rng.integers(0, 1000, n)])],
+        "utf8 10k": [Array.from_strings([words[i] for i in rng.integers(0, 10_000, n)])],
+        "int64 x utf8 10k": [Array.from_numpy(DataType.Int64, rng.integers(0, 100, n)),
+                             Array.from_strings([words[i] for i in rng.integers(0, 100, n)])],
+    }
 AGG = _abi.DFMI_FLAG_EXT_AGGREGATE
 
 
