@@ -220,8 +220,13 @@ double round_exact(const Partial& p, int prec, int qmin, double overflow_limit, 
             break;
         }
     int q = std::max(msb - (prec - 1), qmin);
-    uint64_t mant = 0;
-    for (int i = msb; i >= q; --i) mant = (mant << 1) | bit(i);
+    uint64_t mant = 0;  // bits [q, msb] (at most prec <= 53 of them), from the top three digits
+    if (q <= msb) {
+        const int b0 = std::max(top - 2, 0);
+        unsigned __int128 w = 0;
+        for (int i = top; i >= b0; --i) w = (w << 32) | (uint64_t)d[i];
+        mant = (uint64_t)(w >> (q - 32 * b0)) & ((1ull << (msb - q + 1)) - 1);
+    }
     const uint64_t rb = q >= 1 ? bit(q - 1) : 0;
     // sticky: any set bit below the round bit, bits [0, q - 2] (whole digits first)
     bool sticky = false;
@@ -975,36 +980,58 @@ void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
     HashDev* Hp = st->hd;
     if (!Hp || !Hp->ngroups) return;
     HashDev& H = *Hp;
-    const size_t nk = st->keys.size(), n = st->aggs.size(), K = dfmi::gb::kMaxKeys;
-    const uint64_t cap = H.cap, ng = H.ngroups;
-    std::vector<uint64_t> ctl(cap), kw(cap * K), acc(ng * (size_t)H.words);
-    std::vector<unsigned> gid(cap), klen(cap * K), knull(cap);
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipMemcpy(ctl.data(), H.t.ctl, cap * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(gid.data(), H.t.gid, cap * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(kw.data(), H.t.kw, cap * 8 * K, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(klen.data(), H.t.klen, cap * 4 * K, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(knull.data(), H.t.knull, cap * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(acc.data(), H.acc, acc.size() * 8, hipMemcpyDeviceToHost));
-    read_hdr(ctx, H);
+    const size_t nk = st->keys.size(), n = st->aggs.size();
+    const uint64_t ng = H.ngroups;
+    // the keys by group id (k_group_compact), then the records
+    unsigned* dnull = nullptr;
+    unsigned long long* dkw = nullptr;
+    unsigned* dklen = nullptr;
+    struct Free {
+        void* p[3];
+        ~Free() {
+            for (void* q : p)
+                if (q) (void)hipFree(q);
+        }
+    } fr{{nullptr, nullptr, nullptr}};
+    HIP_TRY(hipMalloc((void**)&dnull, ng * 4));
+    fr.p[0] = dnull;
+    HIP_TRY(hipMalloc((void**)&dkw, ng * nk * 8));
+    fr.p[1] = dkw;
+    HIP_TRY(hipMalloc((void**)&dklen, ng * nk * 4));
+    fr.p[2] = dklen;
+    HIP_TRY(dfmi::gb::launch_compact(H.t, (int)nk, dnull, dkw, dklen, ctx->stream));
+    std::vector<unsigned> knull(ng), klen(ng * nk);
+    std::vector<uint64_t> kw(ng * nk), acc(ng * (size_t)H.words);
+    HIP_TRY(hipMemcpyAsync(knull.data(), dnull, ng * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(kw.data(), dkw, ng * nk * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(klen.data(), dklen, ng * nk * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(acc.data(), H.acc, acc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    read_hdr(ctx, H);  // (synchronises the stream)
     std::vector<uint8_t> arena((size_t)std::max<uint64_t>(H.hh->arena_end, 1));
     if (H.hh->arena_end) HIP_TRY(hipMemcpy(arena.data(), H.arena, H.hh->arena_end, hipMemcpyDeviceToHost));
-    for (uint64_t s = 0; s < cap; ++s) {
-        if (!ctl[s]) continue;
-        HKey hk;
+    std::vector<HKey> keys(ng);
+    for (uint64_t g = 0; g < ng; ++g) {
+        HKey& hk = keys[g];
         hk.p.resize(nk);
         for (size_t p = 0; p < nk; ++p) {
             KeyPart& k = hk.p[p];
             const int kt = st->keys[p].type;
-            if ((knull[s] >> p) & 1) {
+            if ((knull[g] >> p) & 1) {
                 k.null = true;
             } else if (kt == DFMI_TYPE_UTF8) {
-                k.s.assign((const char*)arena.data() + kw[s * K + p], klen[s * K + p]);
+                k.s.assign((const char*)arena.data() + kw[g * nk + p], klen[g * nk + p]);
             } else {
-                k = fixed_part(kt, kw[s * K + p]);
+                k = fixed_part(kt, kw[g * nk + p]);
             }
         }
-        const uint64_t* rec = &acc[(size_t)gid[s] * H.words];
+    }
+    // groups in key order: into an empty map each insertion is O(1) at its end
+    std::vector<uint32_t> order(ng);
+    for (uint64_t g = 0; g < ng; ++g) order[g] = (uint32_t)g;
+    const bool fresh = st->groups.empty();
+    if (fresh) std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+    for (uint32_t g : order) {
+        const uint64_t* rec = &acc[(size_t)g * H.words];
         std::vector<Partial> parts(n + 1);
         parts[n].count = rec[0];
         for (size_t j = 0; j < n; ++j) {
@@ -1023,10 +1050,11 @@ void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
                 q.flags = (w[3] ? AGGF_NAN : 0) | (q.count > w[3] ? AGGF_VALUE : 0);
             }
         }
-        merge_group(group_entry(st->groups, std::move(hk), n), parts, st->aggs.data(), n);
+        if (fresh) st->groups.emplace_hint(st->groups.end(), std::move(keys[g]), std::move(parts));
+        else merge_group(group_entry(st->groups, std::move(keys[g]), n), parts, st->aggs.data(), n);
     }
     // an empty table of the same size for the next batch
-    HIP_TRY(hipMemsetAsync(H.t.ctl, 0, cap * 8, ctx->stream));
+    HIP_TRY(hipMemsetAsync(H.t.ctl, 0, H.cap * 8, ctx->stream));
     HIP_TRY(hipMemsetAsync(H.hdr, 0, sizeof(dfmi::gb::Hdr), ctx->stream));
     HIP_TRY(dfmi::gb::launch_init(H.acc, H.pattern, H.words, 0, ng, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -109,6 +109,8 @@ struct AccArgs {
 hipError_t launch_claim(const ClaimArgs& a, hipStream_t stream);
 hipError_t launch_accumulate(const AccArgs& a, hipStream_t stream);
 hipError_t launch_rehash(const Table& from, const Table& to, hipStream_t stream);
+hipError_t launch_compact(const Table& t, int nkeys, unsigned* knull, unsigned long long* kw, unsigned* klen,
+                          hipStream_t stream);
 hipError_t launch_init(unsigned long long* acc, const unsigned long long* pattern, int words, unsigned long long g0,
                        unsigned long long g1, hipStream_t stream);
 hipError_t launch_normalize(unsigned long long* acc, int words, const int* foff, int nf, unsigned long long ngroups,

@@ -410,6 +410,22 @@ __global__ __launch_bounds__(256) void k_group_rehash(const Table o, const Table
     }
 }
 
+// The persisted key of every used slot, by group id (the host's drain reads
+// ngroups-sized arrays instead of the whole table).
+__global__ __launch_bounds__(256) void k_group_compact(const Table t, int nkeys, unsigned* knull, u64* kw,
+                                                       unsigned* klen) {
+    const u64 cap = t.mask + 1;
+    for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (u64)gridDim.x * blockDim.x) {
+        if (!t.ctl[s]) continue;
+        const u64 g = t.gid[s];
+        knull[g] = t.knull[s];
+        for (int p = 0; p < nkeys; ++p) {
+            kw[g * nkeys + p] = t.kw[s * kMaxKeys + p];
+            klen[g * nkeys + p] = t.klen[s * kMaxKeys + p];
+        }
+    }
+}
+
 // Records [g0, g1) set to the zero state (`pattern`: one record).
 __global__ __launch_bounds__(256) void k_group_init(u64* acc, const u64* pattern, int words, u64 g0, u64 g1) {
     const u64 w0 = g0 * (u64)words, w1 = g1 * (u64)words;
@@ -470,6 +486,13 @@ hipError_t launch_accumulate(const AccArgs& a, hipStream_t st) {
 
 hipError_t launch_rehash(const Table& o, const Table& n, hipStream_t st) {
     hipLaunchKernelGGL(k_group_rehash, dim3(grid_for((long long)o.mask + 1)), dim3(256), 0, st, o, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const Table& t, int nkeys, unsigned* knull, unsigned long long* kw, unsigned* klen,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_group_compact, dim3(grid_for((long long)t.mask + 1)), dim3(256), 0, st, t, nkeys, knull, kw,
+                       klen);
     return hipGetLastError();
 }
 

@@ -551,25 +551,31 @@ class GroupedAggState(AggState):
         return buf.raw[:nb]
 
 
+_AGG_VALUE = np.dtype([("type", "<i4"), ("is_null", "<i4"), ("count", "<i8"), ("bits", "<u8")])
+
+
 def _grouped_call(n: int, fn, nkeys: int = 1, multi: bool = False):
     """(keys, per-group values) from a grouped finish entry point, growing
-    the capacity to the group count it reports. keys: per group one
-    dfmi_agg_value, or (multi) a list of nkeys of them."""
+    the capacity to the group count it reports. Numpy record arrays over the
+    dfmi_agg_value layout (`k.bits`, `k.is_null`, ... per element): keys one
+    record per group, or (multi) a row of nkeys records; values a row of n
+    records per group."""
     ng = C.c_int64()
     err = _abi.dfmi_error()
     cap = 64
+    PV = C.POINTER(_abi.dfmi_agg_value)
     while True:
-        keys = (_abi.dfmi_agg_value * (cap * nkeys))()
-        vals = (_abi.dfmi_agg_value * (cap * n))()
-        rc = fn(cap, keys, vals, C.byref(ng), C.byref(err))
+        keys = np.zeros(max(cap * nkeys, 1), _AGG_VALUE)
+        vals = np.zeros(max(cap * n, 1), _AGG_VALUE)
+        rc = fn(cap, keys.ctypes.data_as(PV), vals.ctypes.data_as(PV), C.byref(ng), C.byref(err))
         if rc == _abi.DFMI_ERR_INVALID_ARGUMENT and ng.value > cap:
             cap = ng.value
             continue
         if rc != _abi.DFMI_OK:
             raise ExecutionError.from_status(rc, err.message.decode("utf-8", errors="replace"))
         g = ng.value
-        ks = [list(keys[i * nkeys:(i + 1) * nkeys]) for i in range(g)] if multi else list(keys[:g])
-        return ks, [list(vals[i * n:(i + 1) * n]) for i in range(g)]
+        kr = keys[: g * nkeys].view(np.recarray)
+        return (kr.reshape(g, nkeys) if multi else kr), vals[: g * n].view(np.recarray).reshape(g, n)
 
 
 def merge_grouped_partials(aggs: Sequence, partials: Sequence[bytes], nkeys: int = 1, multi: bool = False):
