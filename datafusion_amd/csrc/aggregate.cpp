@@ -1029,7 +1029,17 @@ void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
     std::vector<uint32_t> order(ng);
     for (uint64_t g = 0; g < ng; ++g) order[g] = (uint32_t)g;
     const bool fresh = st->groups.empty();
-    if (fresh) std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+    if (fresh) {
+        if (nk == 1 && st->keys[0].type != DFMI_TYPE_UTF8) {  // one fixed-width part: sort on (null, ord) values
+            std::vector<std::pair<__int128, uint32_t>> ko(ng);
+            const __int128 last = ~((__int128)1 << 126);  // the null key after every value (ord < 2^64)
+            for (uint64_t g = 0; g < ng; ++g) ko[g] = {keys[g].p[0].null ? last : keys[g].p[0].ord, (uint32_t)g};
+            std::sort(ko.begin(), ko.end());
+            for (uint64_t g = 0; g < ng; ++g) order[g] = ko[g].second;
+        } else {
+            std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+        }
+    }
     for (uint32_t g : order) {
         const uint64_t* rec = &acc[(size_t)g * H.words];
         std::vector<Partial> parts(n + 1);

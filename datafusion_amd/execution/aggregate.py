@@ -84,7 +84,7 @@ class AggregateRelation(Relation):
         if self.keys is None:
             return RecordBatch(self._schema, [agg_value_array(v) for v in state.finish()])
         keys, vals = state.finish()
-        if not keys:
+        if len(keys) == 0:
             return None
         nk = len(self.keys)
         per_part = [[g[p] for g in keys] for p in range(nk)]  # (the state is created with the key list)
