@@ -101,7 +101,7 @@ class FusedStep:
         return self.outs[0].length
 
 
-PROFILE_TAG = "profiles/r05"
+PROFILE_TAG = "profiles/r06"
 PROFILE_DIR = os.path.join(ROOT, PROFILE_TAG)
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Every bench line of a profile (profiles/<round>/<run>/bench.json) with
 bench.py's roofline() recomputed against the same profile's traffic.json:
-HIP-event ms, rocprof ms, formula and PMC fractions, `frac` -- the lower of the two
+HIP-event ms, rocprof ms, formula, moved-bytes and PMC fractions, `frac` -- the lowest
 (DESIGN.md §6). usage: tools/credited_table.py [runs...]"""
 import json
 import os
@@ -37,12 +37,15 @@ def main(runs):
             L = r.get("launches_per_step", 1)
             alg = r["achieved"] * 1e9 * r["kernel_ms"] * 1e-3
             rows = alg * L / r["algorithmic_bytes_per_row"]
-            n = bench.roofline(r["kernel"], alg, r["kernel_ms"], rows, launches=L, run=run)
+            moved = r["moved_bytes_per_row"] * rows / L if "moved_bytes_per_row" in r else None
+            n = bench.roofline(r["kernel"], alg, r["kernel_ms"], rows, launches=L, run=run, moved=moved)
             rp = n.get("rocprof", {}).get("avg_ms", float("nan"))
-            print("%-9s %-14s %-22s hip %.4f rocprof %.4f (%+.1f%%) | formula %.2f B/row -> %.3f | PMC %.2f B/row %.0f GB/s"
-                  " -> %.3f | frac %.3f (%s)%s" % (
+            print("%-9s %-14s %-22s hip %.4f rocprof %.4f (%+.1f%%) | formula %.2f B/row -> %.3f | moved %s | PMC %.2f B/row"
+                  " %.0f GB/s -> %.3f | frac %.3f (%s)%s" % (
                       run, path or "/", r["kernel"], r["kernel_ms"], rp, (r["kernel_ms"] / rp - 1) * 100,
-                      n["algorithmic_bytes_per_row"], n["formula_frac"], n.get("traffic_bytes_per_row", 0), n.get("traffic_gbs", 0),
+                      n["algorithmic_bytes_per_row"], n["formula_frac"],
+                      "%.2f B/row -> %.3f" % (n["moved_bytes_per_row"], n["moved_frac"]) if moved is not None else "-",
+                      n.get("traffic_bytes_per_row", 0), n.get("traffic_gbs", 0),
                       n.get("traffic_frac", 0), n["frac"], n["frac_basis"].split(" ")[0], " (formula exceeds ceiling)" if n["formula_exceeds_ceiling"] else ""))
 
 
