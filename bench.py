@@ -1120,6 +1120,10 @@ def groupby_line(eng, dev, rank, world, steps, warmup, dist, rows=GROUPBY_ROWS):
     }
     out = {"workload": "SELECT k, SUM(v), COUNT(v) FROM t GROUP BY k: %d rows per GPU, %d distinct keys, v Float64 "
                        "(exact SUM)" % (n, GROUPBY_KEYS)}
+    if world > 1:  # each rank's groups of its own shard; the merge across ranks is a separate entry point
+        out["note"] = ("per-rank groups (rows/s counts every rank's rows); merging them across ranks is "
+                       "dfmi_shard_agg_finish_grouped (RCCL all_gather of the exact per-group partials), tested "
+                       "at world 2 / 3 over the loopback transport (tests/test_shard_abi_gpu.py), not timed here")
     for name, kcols in cases.items():
         nk = len(kcols)
         schema = Schema([Field("k%d" % i, c.data_type, False) for i, c in enumerate(kcols)] +
