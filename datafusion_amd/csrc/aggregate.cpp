@@ -19,6 +19,7 @@
 #include <new>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <type_traits>
 #include <unordered_map>
 #include <vector>
@@ -98,6 +99,20 @@ struct HashDev {
     std::vector<Buf> bufs;            // the fused pass's output columns (reused across batches)
 };
 
+// The device hash table's groups as flat host arrays by group id (read_table):
+// keys (null bits, words: the value bits or the Utf8 arena offset, lengths),
+// the records, the Utf8 arena, and `order` -- the group ids in key order.
+struct FlatGroups {
+    uint64_t ng = 0;
+    size_t nk = 0;
+    int words = 0;
+    std::vector<int> off;
+    std::vector<uint32_t> order;
+    std::vector<unsigned> knull, klen;
+    std::vector<uint64_t> kw, acc;
+    std::vector<uint8_t> arena;
+};
+
 struct dfmi_agg_state {
     int device = 0;
     std::vector<const dfmi_aggregate*> aggs;
@@ -120,6 +135,7 @@ struct dfmi_agg_state {
     std::unordered_map<std::string, std::vector<Partial_>*> index;
     std::shared_ptr<GroupMap> shown;  // groups dfmi_shard_agg_finish_grouped merged (else `groups`)
     HashDev* hd = nullptr;            // device hash table (created on first use)
+    std::unique_ptr<FlatGroups> flat; // a finish's groups, not yet in `groups` (finish_flat)
     // integer keys: the per-batch key window comes from MIN / MAX of the key
     // over the batch's selected rows (a pre-pass through this same extension)
     dfmi_aggregate* mm[2] = {nullptr, nullptr};
@@ -273,8 +289,14 @@ uint64_t narrow_int(uint64_t v, int t) {
     }
 }
 
+dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p);
 dfmi_agg_value finish_one(const dfmi_aggregate& a, Partial p) {
     normalize(p);
+    return finish_normalized(a, p);
+}
+
+// finish_one of a partial whose digits are already carry-normalised.
+dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p) {
     dfmi_agg_value r;
     r.type = a.ret_type;
     r.count = (int64_t)p.count;
@@ -606,6 +628,7 @@ void host_accumulate(Partial& p, int fn, int t, const uint8_t* vals, int64_t i) 
 // evaluation order and first error), into the hash state's reusable device
 // buffers. Returns the selected rows; `cols` describes each output (a
 // passed-through input column, or the compacted output).
+constexpr size_t kDrainBuf = 3 * (dfmi::gb::kMaxKeys + dfmi::gb::kMaxAggs);  // read_table's buffers after the pass's
 void* hd_buf(HashDev& H, size_t i, size_t bytes) {
     if (H.bufs.size() <= i) H.bufs.resize(i + 1);
     HashDev::Buf& b = H.bufs[i];
@@ -974,95 +997,50 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
     }
 }
 
-// The groups the device hash table holds merged into st->groups, and the
-// table emptied (the next batch starts a new one of the same size).
-void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
-    HashDev* Hp = st->hd;
-    if (!Hp || !Hp->ngroups) return;
-    HashDev& H = *Hp;
-    const size_t nk = st->keys.size(), n = st->aggs.size();
+// fn(i0, i1) over [0, n) in contiguous ranges of at least `grain`, on up to
+// DFMI_HOST_THREADS (default min(cores, 8)) threads.
+template <typename F>
+void parallel_ranges(uint64_t n, uint64_t grain, const F& fn) {
+    int hw = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("DFMI_HOST_THREADS")) hw = atoi(e);
+    const uint64_t ways = std::min<uint64_t>((uint64_t)std::max(1, std::min(hw, 8)), std::max<uint64_t>(1, n / grain));
+    if (ways <= 1) {
+        fn((uint64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const uint64_t piece = (n + ways - 1) / ways;
+    for (uint64_t w = 1; w < ways; ++w) th.emplace_back([&, w] { fn(std::min(n, w * piece), std::min(n, (w + 1) * piece)); });
+    fn(0, std::min(n, piece));
+    for (auto& t : th) t.join();
+}
+
+// The groups the device hash table holds, copied out as flat arrays by group
+// id (keys compacted on the device: k_group_compact), and the table emptied
+// (the next batch starts a new one of the same size).
+void read_table(dfmi_context* ctx, dfmi_agg_state* st, FlatGroups& f) {
+    HashDev& H = *st->hd;
+    const size_t nk = st->keys.size();
     const uint64_t ng = H.ngroups;
-    // the keys by group id (k_group_compact), then the records
-    unsigned* dnull = nullptr;
-    unsigned long long* dkw = nullptr;
-    unsigned* dklen = nullptr;
-    struct Free {
-        void* p[3];
-        ~Free() {
-            for (void* q : p)
-                if (q) (void)hipFree(q);
-        }
-    } fr{{nullptr, nullptr, nullptr}};
-    HIP_TRY(hipMalloc((void**)&dnull, ng * 4));
-    fr.p[0] = dnull;
-    HIP_TRY(hipMalloc((void**)&dkw, ng * nk * 8));
-    fr.p[1] = dkw;
-    HIP_TRY(hipMalloc((void**)&dklen, ng * nk * 4));
-    fr.p[2] = dklen;
+    f.ng = ng;
+    f.nk = nk;
+    f.words = H.words;
+    f.off = H.off;
+    unsigned* dnull = (unsigned*)hd_buf(H, kDrainBuf, ng * 4);
+    unsigned long long* dkw = (unsigned long long*)hd_buf(H, kDrainBuf + 1, ng * nk * 8);
+    unsigned* dklen = (unsigned*)hd_buf(H, kDrainBuf + 2, ng * nk * 4);
     HIP_TRY(dfmi::gb::launch_compact(H.t, (int)nk, dnull, dkw, dklen, ctx->stream));
-    std::vector<unsigned> knull(ng), klen(ng * nk);
-    std::vector<uint64_t> kw(ng * nk), acc(ng * (size_t)H.words);
-    HIP_TRY(hipMemcpyAsync(knull.data(), dnull, ng * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(kw.data(), dkw, ng * nk * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(klen.data(), dklen, ng * nk * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(acc.data(), H.acc, acc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    f.knull.resize(ng);
+    f.klen.resize(ng * nk);
+    f.kw.resize(ng * nk);
+    f.acc.resize(ng * (size_t)H.words);
+    HIP_TRY(hipMemcpyAsync(f.knull.data(), dnull, ng * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(f.kw.data(), dkw, ng * nk * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(f.klen.data(), dklen, ng * nk * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(f.acc.data(), H.acc, f.acc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     read_hdr(ctx, H);  // (synchronises the stream)
-    std::vector<uint8_t> arena((size_t)std::max<uint64_t>(H.hh->arena_end, 1));
-    if (H.hh->arena_end) HIP_TRY(hipMemcpy(arena.data(), H.arena, H.hh->arena_end, hipMemcpyDeviceToHost));
-    std::vector<HKey> keys(ng);
-    for (uint64_t g = 0; g < ng; ++g) {
-        HKey& hk = keys[g];
-        hk.p.resize(nk);
-        for (size_t p = 0; p < nk; ++p) {
-            KeyPart& k = hk.p[p];
-            const int kt = st->keys[p].type;
-            if ((knull[g] >> p) & 1) {
-                k.null = true;
-            } else if (kt == DFMI_TYPE_UTF8) {
-                k.s.assign((const char*)arena.data() + kw[g * nk + p], klen[g * nk + p]);
-            } else {
-                k = fixed_part(kt, kw[g * nk + p]);
-            }
-        }
-    }
-    // groups in key order: into an empty map each insertion is O(1) at its end
-    std::vector<uint32_t> order(ng);
-    for (uint64_t g = 0; g < ng; ++g) order[g] = (uint32_t)g;
-    const bool fresh = st->groups.empty();
-    if (fresh) {
-        if (nk == 1 && st->keys[0].type != DFMI_TYPE_UTF8) {  // one fixed-width part: sort on (null, ord) values
-            std::vector<std::pair<__int128, uint32_t>> ko(ng);
-            const __int128 last = ~((__int128)1 << 126);  // the null key after every value (ord < 2^64)
-            for (uint64_t g = 0; g < ng; ++g) ko[g] = {keys[g].p[0].null ? last : keys[g].p[0].ord, (uint32_t)g};
-            std::sort(ko.begin(), ko.end());
-            for (uint64_t g = 0; g < ng; ++g) order[g] = ko[g].second;
-        } else {
-            std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
-        }
-    }
-    for (uint32_t g : order) {
-        const uint64_t* rec = &acc[(size_t)g * H.words];
-        std::vector<Partial> parts(n + 1);
-        parts[n].count = rec[0];
-        for (size_t j = 0; j < n; ++j) {
-            const uint64_t* w = rec + H.off[j];
-            Partial& q = parts[j];
-            const int fn = st->aggs[j]->fn;
-            q.count = rec[0] - w[0];  // the group's rows minus its NULL arguments
-            if (fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type)) {
-                q.flags = w[1] | (q.count > w[3] ? AGGF_NONNEGZERO : 0);
-                for (int i = 0; i < kAggLimbs; ++i) q.limbs[i] = (int64_t)w[4 + i];
-                normalize(q);
-            } else if (fn == DFMI_AGG_SUM) {
-                q.isum = w[3];
-            } else if (fn == DFMI_AGG_MIN || fn == DFMI_AGG_MAX) {
-                q.key = w[2];
-                q.flags = (w[3] ? AGGF_NAN : 0) | (q.count > w[3] ? AGGF_VALUE : 0);
-            }
-        }
-        if (fresh) st->groups.emplace_hint(st->groups.end(), std::move(keys[g]), std::move(parts));
-        else merge_group(group_entry(st->groups, std::move(keys[g]), n), parts, st->aggs.data(), n);
-    }
+    f.arena.resize((size_t)H.hh->arena_end);
+    if (H.hh->arena_end) HIP_TRY(hipMemcpy(f.arena.data(), H.arena, H.hh->arena_end, hipMemcpyDeviceToHost));
     // an empty table of the same size for the next batch
     HIP_TRY(hipMemsetAsync(H.t.ctl, 0, H.cap * 8, ctx->stream));
     HIP_TRY(hipMemsetAsync(H.hdr, 0, sizeof(dfmi::gb::Hdr), ctx->stream));
@@ -1070,6 +1048,224 @@ void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     H.ngroups = 0;
     H.rows_since_norm = 0;
+}
+
+// f.order: the group ids in key order (HKey's order restated on the flat
+// arrays: per part, null last; integers / floats by key_ord; Utf8 bytewise,
+// a shorter prefix first).
+void sort_flat(const dfmi_agg_state* st, FlatGroups& f) {
+    const uint64_t ng = f.ng;
+    const size_t nk = f.nk;
+    f.order.resize(ng);
+    if (nk == 1 && st->keys[0].type != DFMI_TYPE_UTF8) {  // one fixed-width part: sort on (null, ord) values
+        // LSD radix sort (16-bit digits) of the order values mapped onto
+        // unsigned 64 bits (signed integers offset by 2^63); the null group last
+        const int kt = st->keys[0].type;
+        const bool sgn = is_signed_type(kt);
+        std::vector<uint64_t> kv, kv2;
+        std::vector<uint32_t> id, id2;
+        kv.reserve(ng);
+        id.reserve(ng);
+        int64_t null_g = -1;
+        for (uint64_t g = 0; g < ng; ++g) {
+            if (f.knull[g] & 1) {
+                null_g = (int64_t)g;
+                continue;
+            }
+            const __int128 o = key_ord(kt, f.kw[g]);
+            kv.push_back(sgn ? (uint64_t)(int64_t)o ^ (1ull << 63) : (uint64_t)o);
+            id.push_back((uint32_t)g);
+        }
+        const size_t m = kv.size();
+        if (m < 65536) {
+            std::vector<std::pair<uint64_t, uint32_t>> ko(m);
+            for (size_t i = 0; i < m; ++i) ko[i] = {kv[i], id[i]};
+            std::sort(ko.begin(), ko.end());
+            for (size_t i = 0; i < m; ++i) f.order[i] = ko[i].second;
+        } else {
+            kv2.resize(m);
+            id2.resize(m);
+            std::vector<size_t> cnt(65536);
+            for (int pass = 0; pass < 4; ++pass) {
+                const int sh = 16 * pass;
+                std::fill(cnt.begin(), cnt.end(), 0);
+                for (size_t i = 0; i < m; ++i) ++cnt[(kv[i] >> sh) & 0xffff];
+                if (cnt[kv[0] >> sh & 0xffff] == m) continue;  // one digit value: this pass moves nothing
+                size_t sum = 0;
+                for (auto& c : cnt) {
+                    const size_t t = c;
+                    c = sum;
+                    sum += t;
+                }
+                for (size_t i = 0; i < m; ++i) {
+                    const size_t d = cnt[(kv[i] >> sh) & 0xffff]++;
+                    kv2[d] = kv[i];
+                    id2[d] = id[i];
+                }
+                kv.swap(kv2);
+                id.swap(id2);
+            }
+            std::copy(id.begin(), id.end(), f.order.begin());
+        }
+        if (null_g >= 0) f.order[m] = (uint32_t)null_g;
+        return;
+    }
+    for (uint64_t g = 0; g < ng; ++g) f.order[g] = (uint32_t)g;
+    std::vector<int> kt(nk);
+    for (size_t p = 0; p < nk; ++p) kt[p] = st->keys[p].type;
+    std::sort(f.order.begin(), f.order.end(), [&](uint32_t a, uint32_t b) {
+        for (size_t p = 0; p < nk; ++p) {
+            const bool na = (f.knull[a] >> p) & 1, nb = (f.knull[b] >> p) & 1;
+            if (na != nb) return !na;
+            if (na) continue;
+            const uint64_t wa = f.kw[a * nk + p], wb = f.kw[b * nk + p];
+            if (kt[p] == DFMI_TYPE_UTF8) {
+                const unsigned la = f.klen[a * nk + p], lb = f.klen[b * nk + p];
+                const int c = memcmp(f.arena.data() + wa, f.arena.data() + wb, std::min(la, lb));
+                if (c) return c < 0;
+                if (la != lb) return la < lb;
+            } else if (wa != wb) {
+                return key_ord(kt[p], wa) < key_ord(kt[p], wb);
+            }
+        }
+        return false;
+    });
+}
+
+// Aggregate j's partial of group record `rec` (the device record layout:
+// groupby.h; word 0 the group's rows).
+void rec_partial(const dfmi_agg_state* st, const FlatGroups& f, const uint64_t* rec, size_t j, Partial& q) {
+    const uint64_t* w = rec + f.off[j];
+    const int fn = st->aggs[j]->fn;
+    q.count = rec[0] - w[0];  // the group's rows minus its NULL arguments
+    if (fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type)) {
+        q.flags = w[1] | (q.count > w[3] ? AGGF_NONNEGZERO : 0);
+        for (int i = 0; i < kAggLimbs; ++i) q.limbs[i] = (int64_t)w[4 + i];
+        normalize(q);
+    } else if (fn == DFMI_AGG_SUM) {
+        q.isum = w[3];
+    } else if (fn == DFMI_AGG_MIN || fn == DFMI_AGG_MAX) {
+        q.key = w[2];
+        q.flags = (w[3] ? AGGF_NAN : 0) | (q.count > w[3] ? AGGF_VALUE : 0);
+    }
+}
+
+// The flat groups merged into st->groups (into an empty map in key order:
+// each insertion O(1) at its end).
+void materialize_flat(dfmi_agg_state* st, FlatGroups& f) {
+    const size_t nk = f.nk, n = st->aggs.size();
+    const bool fresh = st->groups.empty();
+    if (fresh && f.order.size() != f.ng) sort_flat(st, f);
+    for (uint64_t i = 0; i < f.ng; ++i) {
+        const uint32_t g = fresh ? f.order[i] : (uint32_t)i;
+        HKey hk;
+        hk.p.resize(nk);
+        for (size_t p = 0; p < nk; ++p) {
+            KeyPart& k = hk.p[p];
+            const int kt = st->keys[p].type;
+            if ((f.knull[g] >> p) & 1) k.null = true;
+            else if (kt == DFMI_TYPE_UTF8) k.s.assign((const char*)f.arena.data() + f.kw[g * nk + p], f.klen[g * nk + p]);
+            else k = fixed_part(kt, f.kw[g * nk + p]);
+        }
+        const uint64_t* rec = &f.acc[(size_t)g * f.words];
+        std::vector<Partial> parts(n + 1);
+        parts[n].count = rec[0];
+        for (size_t j = 0; j < n; ++j) rec_partial(st, f, rec, j, parts[j]);
+        if (fresh) st->groups.emplace_hint(st->groups.end(), std::move(hk), std::move(parts));
+        else merge_group(group_entry(st->groups, std::move(hk), n), parts, st->aggs.data(), n);
+    }
+}
+
+// A finish's flat groups (st->flat) moved into st->groups before anything
+// else merges into or reads the map.
+void unflatten(dfmi_agg_state* st) {
+    if (!st->flat) return;
+    std::unique_ptr<FlatGroups> f = std::move(st->flat);
+    materialize_flat(st, *f);
+}
+
+// The groups the device hash table holds merged into st->groups, and the
+// table emptied.
+void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
+    unflatten(st);
+    if (!st->hd || !st->hd->ngroups) return;
+    FlatGroups f;
+    read_table(ctx, st, f);
+    materialize_flat(st, f);
+}
+
+// The finish of a state whose groups all sit in the device hash table (no
+// window flush, no host merge: the common case): the groups stay flat
+// (st->flat, sorted by key) and are emitted from there -- no per-group map
+// node, key string or partial copy.
+bool finish_flat(dfmi_context* ctx, dfmi_agg_state* st) {
+    flush_groups(ctx, st);
+    if (!st->groups.empty()) return false;
+    if (st->flat && st->hd && st->hd->ngroups) return false;  // (a batch unflattens first: not reached)
+    if (!st->flat) {
+        if (!st->hd || !st->hd->ngroups) return false;
+        auto f = std::make_unique<FlatGroups>();
+        read_table(ctx, st, *f);
+        sort_flat(st, *f);
+        st->flat = std::move(f);
+    }
+    st->shown.reset();
+    return true;
+}
+
+void emit_flat(const dfmi_agg_state* st, const FlatGroups& f, int64_t cap, dfmi_agg_value* keys,
+               dfmi_agg_value* values, int64_t* num_groups) {
+    *num_groups = (int64_t)f.ng;
+    if (*num_groups > cap) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "group capacity too small"};
+    if (*num_groups > 0 && (!keys || !values)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+    const size_t nk = f.nk, n = st->aggs.size();
+    auto emit_range = [&](uint64_t i0, uint64_t i1) {
+        Partial q;
+        for (uint64_t i = i0; i < i1; ++i) {
+            const uint32_t g = f.order[i];
+            const uint64_t* rec = &f.acc[(size_t)g * f.words];
+            for (size_t p = 0; p < nk; ++p) {
+                dfmi_agg_value& k = keys[i * nk + p];
+                const int kt = st->keys[p].type;
+                const bool null = (f.knull[g] >> p) & 1;
+                k.type = kt;
+                k.is_null = null ? 1 : 0;
+                k.bits = null || kt == DFMI_TYPE_UTF8 ? 0
+                                                      : (kt == DFMI_TYPE_BOOLEAN ? f.kw[g * nk + p] : narrow_int(f.kw[g * nk + p], kt));
+                k.count = (int64_t)rec[0];
+            }
+            for (size_t j = 0; j < n; ++j) {
+                q.flags = q.key = q.isum = 0;  // (rec_partial sets count and, for a float SUM, every digit)
+                rec_partial(st, f, rec, j, q);
+                values[i * n + j] = finish_normalized(*st->aggs[j], q);
+            }
+        }
+    };
+    parallel_ranges(f.ng, 4096, emit_range);
+}
+
+void emit_key_bytes_flat(const FlatGroups& f, int part, int32_t* offsets, int64_t num_offsets, uint8_t* data,
+                         int64_t data_capacity, int64_t* data_length) {
+    const size_t nk = f.nk;
+    int64_t total = 0;
+    for (uint64_t g = 0; g < f.ng; ++g)
+        if (!((f.knull[g] >> part) & 1)) total += f.klen[g * nk + part];
+    *data_length = total;
+    if (total > 0x7fffffffll) throw Fail{DFMI_ERR_CAPACITY, "Utf8 group keys of 2^31 bytes or more"};
+    if (num_offsets < (int64_t)f.ng + 1 || data_capacity < total)
+        throw Fail{DFMI_ERR_CAPACITY, "key offsets / bytes capacity too small"};
+    if (!offsets || (total && !data)) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+    int64_t pos = 0;
+    offsets[0] = 0;
+    for (uint64_t i = 0; i < f.ng; ++i) {
+        const uint32_t g = f.order[i];
+        if (!((f.knull[g] >> part) & 1)) {
+            const unsigned len = f.klen[g * nk + part];
+            if (len) memcpy(data + pos, f.arena.data() + f.kw[g * nk + part], len);
+            pos += len;
+        }
+        offsets[i + 1] = (int32_t)pos;
+    }
 }
 
 // Every group the state holds (window, hash table, host merges) in st->groups.
@@ -1370,6 +1566,10 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
             return st->failure.code;
         }
         HIP_TRY(hipSetDevice(ctx->device));
+        if (finish_flat(ctx, st)) {
+            emit_flat(st, *st->flat, cap, keys, values, num_groups);
+            return DFMI_OK;
+        }
         collect_groups(ctx, st);
         emit_groups(st->groups, key_types(st), st->aggs.data(), st->aggs.size(), cap, keys, values, num_groups);
         return DFMI_OK;
@@ -1391,8 +1591,11 @@ extern "C" int32_t dfmi_agg_state_group_keys_utf8_part(const dfmi_agg_state* st,
         }
         if (!st->grouped || part < 0 || part >= (int32_t)st->keys.size() || st->keys[part].type != DFMI_TYPE_UTF8)
             throw Fail{DFMI_ERR_INVALID_ARGUMENT, "not a GROUP BY state over a Utf8 key"};
-        emit_key_bytes(st->shown ? *st->shown : st->groups, part, offsets, num_offsets, data, data_capacity,
-                       data_length);
+        if (!st->shown && st->flat)
+            emit_key_bytes_flat(*st->flat, part, offsets, num_offsets, data, data_capacity, data_length);
+        else
+            emit_key_bytes(st->shown ? *st->shown : st->groups, part, offsets, num_offsets, data, data_capacity,
+                           data_length);
         return DFMI_OK;
     } catch (const Fail& f) {
         set_err(err, f.code, f.msg);
@@ -1424,6 +1627,7 @@ extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, d
         st->failure = dfmi_error{};
         st->index.clear();
         st->groups.clear();
+        st->flat.reset();
         st->shown.reset();
         st->win_width = -1;
         st->dirty = false;
@@ -1459,6 +1663,7 @@ extern "C" int32_t dfmi_aggregate_batch(dfmi_context* ctx, dfmi_agg_state* st, c
             if (err) *err = st->failure;
             return st->failure.code;
         }
+        if (st->grouped) unflatten(st);  // a finish's flat groups back in the map before more rows merge
         Unsliced us_;  // sliced arrays (arrow offsets): offset-0 views / shifted bitmaps (slice.cpp)
         if (any_offset(in, 1)) {
             HIP_TRY(hipSetDevice(ctx->device));

@@ -221,3 +221,44 @@ def test_grouped_partials_utf8_and_multi_key_merge():
             if strs is not None:
                 got = merge_grouped_partials_key_strings(cs, parts, p, len(mk))
                 assert [None if mk[g][p].is_null else got[g] for g in range(len(mk))] == strs
+
+
+def test_finish_then_more_rows_partial_and_reset():
+    """The finish's flat groups (aggregate.cpp finish_flat: emitted from the
+    drained table without the host map): a second finish gives the same
+    groups; rows added after a finish merge with the finished groups; the
+    grouped partial after a finish holds every group; reset empties."""
+    rng = np.random.default_rng(68)
+    s, b = _table(rng, 24_000)
+    aggs_e = AGGS(s)
+    db = b.to(engine().device)
+    for keys_e in ([Column(2)], [Column(1)], [Column(0), Column(1)]):
+        cs = [compile_expr(None, a, s, FL) for a in aggs_e]
+        st = engine().grouped_agg_state([compile_scalar_expr(None, k, s, FL) for k in keys_e], cs)
+        rk1, rv1, rs1 = oracle_aggregate_grouped_multi(s, slice_batch(b, 0, 10_000), None, keys_e, aggs_e, FL)
+        rk, rv, rs = oracle_aggregate_grouped_multi(s, b, None, keys_e, aggs_e, FL)
+
+        def check(out, rk_, rv_, rs_):
+            dk, dv = out
+            assert [[(k.is_null, k.bits, k.count) for k in g] for g in dk] == \
+                [[(k.is_null, k.bits, k.count) for k in g] for g in rk_]
+            assert [_vals(v) for v in dv] == [_vals(v) for v in rv_]
+            for p, strs in enumerate(rs_):
+                if strs is not None:
+                    assert st.key_strings(p) == strs
+
+        st.add(None, slice_batch(db, 0, 10_000), FL)
+        check(st.finish(), rk1, rv1, rs1)
+        check(st.finish(), rk1, rv1, rs1)
+        st.add(None, slice_batch(db, 10_000, 14_000), FL)
+        check(st.finish(), rk, rv, rs)
+        part = st.partial()
+        mk, mv = merge_grouped_partials(cs, [part], len(keys_e), True)
+        assert [[(k.is_null, k.bits, k.count) for k in g] for g in mk] == \
+            [[(k.is_null, k.bits, k.count) for k in g] for g in rk]
+        assert [_vals(v) for v in mv] == [_vals(v) for v in rv]
+        check(st.finish(), rk, rv, rs)
+        st.reset()
+        assert len(st.finish()[0]) == 0
+        st.add(None, slice_batch(db, 0, 10_000), FL)
+        check(st.finish(), rk1, rv1, rs1)
