@@ -7,7 +7,9 @@ keys Int64 x Utf8 (the device hash table: aggregate.cpp group_batch_hashed)
 -- each timed end to end (state creation excluded, finish included) after a
 warm-up, and the host-merge A/B (DFMI_DIAG=1 DFMI_GROUP_HOST=1) on the same
 batches; --sweep: Float64 keys of 4 ... 1e6 distinct values instead.
-usage: groupby_probe.py [rows] [--no-host] [--sweep]"""
+--card=C1,C2: the sweep at those cardinalities only; --phases: add and
+finish timed apart (add synchronised).
+usage: groupby_probe.py [rows] [--no-host] [--sweep] [--card=...] [--phases]"""
 import os
 import sys
 import time
@@ -32,9 +34,14 @@ eng = engine()
 dev = eng.device
 v = Array.from_numpy(DataType.Float64, rng.random(n)).to(dev)
 words = [("w%d_" % i + "x" * (i % 17)) for i in range(10_000)]
+CARDS = (4, 16, 100, 1000, 10_000, 100_000, 1_000_000)
+PHASES = "--phases" in sys.argv
+for a in sys.argv:
+    if a.startswith("--card="):
+        CARDS = tuple(int(float(c)) for c in a[7:].split(","))
 if "--sweep" in sys.argv:  # the hash table across key cardinalities (Float64 keys: always the hash path)
     cases = {"float64 %d" % c: [Array.from_numpy(DataType.Float64, rng.integers(0, c, n) / 7.0)]
-             for c in (4, 16, 100, 1000, 10_000, 100_000, 1_000_000)}
+             for c in CARDS}
 else:
     cases = {
         "int64 window": [Array.from_numpy(DataType.Int64, rng.integers(0, 16, n))],
@@ -57,17 +64,22 @@ def run(name, kcols, reps=3):
             AggregateFunction("COUNT", (Column(nk),), DataType.UInt64)]
     cs = [compile_expr(None, a, s, AGG) for a in aggs]
     kp = [compile_scalar_expr(None, Column(i), s, AGG) for i in range(nk)]
-    best, groups = None, 0
+    best, groups, split = None, 0, None
     for rep in range(reps + 1):  # rep 0 warms up (code objects, allocations, clocks)
         st = eng.grouped_agg_state(kp if nk > 1 else kp[0], cs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st.add(None, b, AGG)
+        if PHASES:
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
         keys_out, vals = st.finish()
         el = time.perf_counter() - t0
         if rep and (best is None or el < best):
-            best = el
+            best, split = el, (t1 - t0, el - (t1 - t0))
         groups = len(keys_out)
+    if PHASES:
+        print("  %s: add %.2f ms, finish %.2f ms" % (name, split[0] * 1e3, split[1] * 1e3), flush=True)
     return best, groups
 
 
