@@ -99,10 +99,13 @@ struct HashDev {
     std::vector<Buf> bufs;            // the fused pass's output columns (reused across batches)
 };
 
-// The device hash table's groups as flat host arrays by group id (read_table):
+// The device hash table's groups as flat host arrays by group id (read_table;
+// for a finish, `rounded`: the records finished on the device and the table
+// left as it is):
 // keys (null bits, words: the value bits or the Utf8 arena offset, lengths),
 // the records, the Utf8 arena, and `order` -- the group ids in key order.
 struct FlatGroups {
+    bool rounded = false;  // acc: the device finish's compact records (groupby.h RoundArgs), the table kept
     uint64_t ng = 0;
     size_t nk = 0;
     int words = 0;
@@ -289,14 +292,21 @@ uint64_t narrow_int(uint64_t v, int t) {
     }
 }
 
-dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p);
+// A floating-point SUM already rounded (the device finish, k_group_round).
+struct Rounded {
+    double v;
+    bool zero;
+};
+
+dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p, const Rounded* pre = nullptr);
 dfmi_agg_value finish_one(const dfmi_aggregate& a, Partial p) {
     normalize(p);
     return finish_normalized(a, p);
 }
 
-// finish_one of a partial whose digits are already carry-normalised.
-dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p) {
+// finish_one of a partial whose digits are already carry-normalised (or, with
+// `pre`, of a floating-point SUM whose digits the device has rounded).
+dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p, const Rounded* pre) {
     dfmi_agg_value r;
     r.type = a.ret_type;
     r.count = (int64_t)p.count;
@@ -323,7 +333,13 @@ dfmi_agg_value finish_normalized(const dfmi_aggregate& a, const Partial& p) {
             r.bits = f32 ? (pos ? 0x7F800000ull : 0xFF800000ull) : (pos ? 0x7FF0000000000000ull : 0xFFF0000000000000ull);
         } else {
             bool zero = false;
-            double v = f32 ? round_exact(p, 24, 925, 0x1p128, &zero) : round_exact(p, 53, 0, HUGE_VAL, &zero);
+            double v;
+            if (pre) {
+                v = pre->v;
+                zero = pre->zero;
+            } else {
+                v = f32 ? round_exact(p, 24, 925, 0x1p128, &zero) : round_exact(p, 53, 0, HUGE_VAL, &zero);
+            }
             if (zero) v = (p.flags & AGGF_NONNEGZERO) ? 0.0 : -0.0;
             if (f32) {
                 const float fv = (float)v;
@@ -1017,15 +1033,37 @@ void parallel_ranges(uint64_t n, uint64_t grain, const F& fn) {
 
 // The groups the device hash table holds, copied out as flat arrays by group
 // id (keys compacted on the device: k_group_compact), and the table emptied
-// (the next batch starts a new one of the same size).
-void read_table(dfmi_context* ctx, dfmi_agg_state* st, FlatGroups& f) {
+// (the next batch starts a new one of the same size) -- or, `rounded` (a
+// finish), every record finished on the device first (k_group_round: the
+// compact records without their exact-sum digits cross PCIe) and the table
+// kept as it is, so that more batches can still merge into it.
+void read_table(dfmi_context* ctx, dfmi_agg_state* st, FlatGroups& f, bool rounded = false) {
     HashDev& H = *st->hd;
-    const size_t nk = st->keys.size();
+    const size_t nk = st->keys.size(), n = st->aggs.size();
     const uint64_t ng = H.ngroups;
+    f.rounded = rounded;
     f.ng = ng;
     f.nk = nk;
     f.words = H.words;
     f.off = H.off;
+    const unsigned long long* src = H.acc;
+    if (rounded) {
+        dfmi::gb::RoundArgs ra{};
+        ra.acc = H.acc;
+        ra.words = H.words;
+        ra.naggs = (int)n;
+        for (size_t j = 0; j < n; ++j) {
+            ra.off[j] = H.off[j];
+            const int t = st->aggs[j]->arg.type;
+            ra.kind[j] = st->aggs[j]->fn == DFMI_AGG_SUM && is_float_type(t) ? (t == DFMI_TYPE_FLOAT32 ? 2 : 1) : 0;
+            f.off[j] = 1 + 4 * (int)j;
+        }
+        f.words = 1 + 4 * (int)n;
+        ra.ngroups = ng;
+        ra.out = (unsigned long long*)hd_buf(H, kDrainBuf + 3, ng * (size_t)f.words * 8);
+        HIP_TRY(dfmi::gb::launch_round(ra, ctx->stream));
+        src = ra.out;
+    }
     unsigned* dnull = (unsigned*)hd_buf(H, kDrainBuf, ng * 4);
     unsigned long long* dkw = (unsigned long long*)hd_buf(H, kDrainBuf + 1, ng * nk * 8);
     unsigned* dklen = (unsigned*)hd_buf(H, kDrainBuf + 2, ng * nk * 4);
@@ -1033,14 +1071,15 @@ void read_table(dfmi_context* ctx, dfmi_agg_state* st, FlatGroups& f) {
     f.knull.resize(ng);
     f.klen.resize(ng * nk);
     f.kw.resize(ng * nk);
-    f.acc.resize(ng * (size_t)H.words);
+    f.acc.resize(ng * (size_t)f.words);
     HIP_TRY(hipMemcpyAsync(f.knull.data(), dnull, ng * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(f.kw.data(), dkw, ng * nk * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(f.klen.data(), dklen, ng * nk * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(f.acc.data(), H.acc, f.acc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(f.acc.data(), src, f.acc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     read_hdr(ctx, H);  // (synchronises the stream)
     f.arena.resize((size_t)H.hh->arena_end);
     if (H.hh->arena_end) HIP_TRY(hipMemcpy(f.arena.data(), H.arena, H.hh->arena_end, hipMemcpyDeviceToHost));
+    if (rounded) return;
     // an empty table of the same size for the next batch
     HIP_TRY(hipMemsetAsync(H.t.ctl, 0, H.cap * 8, ctx->stream));
     HIP_TRY(hipMemsetAsync(H.hdr, 0, sizeof(dfmi::gb::Hdr), ctx->stream));
@@ -1139,7 +1178,8 @@ void rec_partial(const dfmi_agg_state* st, const FlatGroups& f, const uint64_t* 
     const int fn = st->aggs[j]->fn;
     q.count = rec[0] - w[0];  // the group's rows minus its NULL arguments
     if (fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type)) {
-        q.flags = w[1] | (q.count > w[3] ? AGGF_NONNEGZERO : 0);
+        q.flags = (w[1] & 0xffffffffull) | (q.count > w[3] ? AGGF_NONNEGZERO : 0);
+        if (f.rounded) return;  // (the digits were rounded on the device: w[2])
         for (int i = 0; i < kAggLimbs; ++i) q.limbs[i] = (int64_t)w[4 + i];
         normalize(q);
     } else if (fn == DFMI_AGG_SUM) {
@@ -1177,11 +1217,12 @@ void materialize_flat(dfmi_agg_state* st, FlatGroups& f) {
 }
 
 // A finish's flat groups (st->flat) moved into st->groups before anything
-// else merges into or reads the map.
+// else merges into or reads the map (a device-finished snapshot is dropped:
+// the device table still holds its groups).
 void unflatten(dfmi_agg_state* st) {
     if (!st->flat) return;
     std::unique_ptr<FlatGroups> f = std::move(st->flat);
-    materialize_flat(st, *f);
+    if (!f->rounded) materialize_flat(st, *f);
 }
 
 // The groups the device hash table holds merged into st->groups, and the
@@ -1195,17 +1236,18 @@ void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
 }
 
 // The finish of a state whose groups all sit in the device hash table (no
-// window flush, no host merge: the common case): the groups stay flat
-// (st->flat, sorted by key) and are emitted from there -- no per-group map
-// node, key string or partial copy.
+// window flush, no host merge: the common case): every group finished on the
+// device, the results kept flat (st->flat, sorted by key) and emitted from
+// there -- no per-group map node, key string, partial copy or exact-sum
+// digits on the host; the table keeps the groups for later batches.
 bool finish_flat(dfmi_context* ctx, dfmi_agg_state* st) {
     flush_groups(ctx, st);
     if (!st->groups.empty()) return false;
-    if (st->flat && st->hd && st->hd->ngroups) return false;  // (a batch unflattens first: not reached)
+    if (st->flat && !st->flat->rounded && st->hd && st->hd->ngroups) return false;  // (a batch unflattens first)
     if (!st->flat) {
         if (!st->hd || !st->hd->ngroups) return false;
         auto f = std::make_unique<FlatGroups>();
-        read_table(ctx, st, *f);
+        read_table(ctx, st, *f, !(getenv("DFMI_DIAG") && getenv("DFMI_GROUP_HOST_FINISH")));
         sort_flat(st, *f);
         st->flat = std::move(f);
     }
@@ -1237,7 +1279,15 @@ void emit_flat(const dfmi_agg_state* st, const FlatGroups& f, int64_t cap, dfmi_
             for (size_t j = 0; j < n; ++j) {
                 q.flags = q.key = q.isum = 0;  // (rec_partial sets count and, for a float SUM, every digit)
                 rec_partial(st, f, rec, j, q);
-                values[i * n + j] = finish_normalized(*st->aggs[j], q);
+                if (f.rounded && st->aggs[j]->fn == DFMI_AGG_SUM && is_float_type(st->aggs[j]->arg.type)) {
+                    const uint64_t* w = rec + f.off[j];
+                    Rounded r;
+                    memcpy(&r.v, &w[2], 8);
+                    r.zero = (w[1] & dfmi::gb::kRoundZero) != 0;
+                    values[i * n + j] = finish_normalized(*st->aggs[j], q, &r);
+                } else {
+                    values[i * n + j] = finish_normalized(*st->aggs[j], q);
+                }
             }
         }
     };

@@ -105,6 +105,95 @@ struct AccArgs {
     int32_t* coll_rows;            // [m] rows whose key differs from the slot's
 };
 
+// Bucketed accumulation (many rows per group: aggregate.cpp use_buckets). The
+// accumulate pass's scattered record atomics -- one request per lane, the
+// chip's slowest atomic shape (MI355X_MICROARCH.md "Global float atomics") --
+// replaced by a partition of the rows by group and a per-bucket sum in LDS:
+//   k_group_rank     the accumulate pass's key check per row (the same
+//                    representative / persisted-key rules, colliding rows
+//                    listed); the row's group id into rg, and per block the
+//                    rows of each bucket (gpb consecutive group ids) into bh
+//   k_group_scan     exclusive scan of bh, bucket-major: every (bucket,
+//                    block) its first position
+//   k_group_scatter  the same rows per block as the rank pass: each placed
+//                    row's group id, NULL mask and argument bits written at
+//                    its bucket's next position (LDS counters)
+//   k_group_bucket   per (bucket, split) block: the bucket's records in LDS,
+//                    every row of its share added with LDS atomics, then
+//                    each record word that moved added once into the
+//                    group's global record (atomics over contiguous words)
+// Integer digit sums are order-free: the records equal the accumulate pass's.
+constexpr int kBucketMax = 256;   // buckets per pass
+constexpr int kBucketBlocks = 1024;  // blocks of the rank and scatter passes
+
+struct RankArgs {
+    Col k[kMaxKeys];
+    int32_t nkeys;
+    uint32_t epoch;
+    long long m;
+    Table t;
+    unsigned char* arena;
+    const int32_t* sidx;
+    Hdr* hdr;
+    int32_t* coll_rows;
+    unsigned* rg;      // [m] the row's group id, ~0u: not added here (listed)
+    uint32_t gpb;      // groups per bucket
+    int32_t nbuckets;
+    unsigned* bh;      // [nbuckets][kBucketBlocks] rows per (bucket, block); [nbuckets * kBucketBlocks]: total
+};
+
+struct ScatterArgs {
+    long long m;
+    const unsigned* rg;
+    uint32_t gpb;
+    int32_t nbuckets;
+    const unsigned* base;        // k_group_scan's output
+    int32_t naggs;
+    Col arg[kMaxAggs];           // aggregate j's argument column (its NULLs)
+    Col pay[kMaxAggs];           // payload column c's source (the arguments whose values are needed, once each)
+    int32_t npay;
+    unsigned* pg;                // [placed] group ids in bucket order
+    unsigned* pn;                // [placed] NULL mask (bit j: argument j NULL); nullptr: no nullable argument
+    unsigned long long* pv;      // [npay][m] argument bits (integers sign/zero-extended, float raw bits)
+};
+
+struct BucketArgs {
+    long long m;                 // pv's column stride
+    const unsigned* base;
+    uint32_t gpb;
+    int32_t nbuckets;
+    int32_t splits;              // blocks per bucket
+    unsigned long long ngroups;
+    const unsigned* pg;
+    const unsigned* pn;
+    const unsigned long long* pv;
+    AggCol a[kMaxAggs];          // type, fn, record offset (a[j].c.values unused)
+    int32_t pcol[kMaxAggs];
+    int32_t naggs;
+    int32_t words;
+    unsigned long long* acc;
+    const unsigned long long* pattern;  // one zero-state record
+};
+
+hipError_t launch_buckets(const RankArgs& r, ScatterArgs s, BucketArgs b, hipStream_t stream);
+
+// The finish of every group on the device (k_group_round): per group a
+// compact record [rows, then per aggregate nulls, flags, key, aux] -- the
+// record without its exact-sum digits; a floating-point SUM's key word holds
+// its digits rounded once, half to even (aggregate.cpp round_exact restated:
+// kind 1 to a Float64, kind 2 to a Float32's value as a double), and its
+// flags word kRoundZero when the exact sum is 0.
+struct RoundArgs {
+    const unsigned long long* acc;  // [ngroups][words]
+    int32_t words;
+    int32_t naggs;
+    int32_t off[kMaxAggs];          // word offset of aggregate j in a record
+    int32_t kind[kMaxAggs];         // 0: copied; 1: Float64 SUM; 2: Float32 SUM
+    unsigned long long ngroups;
+    unsigned long long* out;        // [ngroups][1 + 4 * naggs]
+};
+constexpr unsigned long long kRoundZero = 1ull << 32;
+
 // groupby.hip: launches on `stream` (asynchronous)
 hipError_t launch_claim(const ClaimArgs& a, hipStream_t stream);
 hipError_t launch_accumulate(const AccArgs& a, hipStream_t stream);
@@ -113,6 +202,7 @@ hipError_t launch_compact(const Table& t, int nkeys, unsigned* knull, unsigned l
                           hipStream_t stream);
 hipError_t launch_init(unsigned long long* acc, const unsigned long long* pattern, int words, unsigned long long g0,
                        unsigned long long g1, hipStream_t stream);
+hipError_t launch_round(const RoundArgs& a, hipStream_t stream);
 hipError_t launch_normalize(unsigned long long* acc, int words, const int* foff, int nf, unsigned long long ngroups,
                             hipStream_t stream);
 

@@ -316,6 +316,52 @@ __device__ __forceinline__ void agg_dispatch(const AggCol& ac, u64* rec, long lo
     }
 }
 
+// Row i's group: its slot's group id when the slot holds the row's key -- the
+// representative row of this batch (a slot claimed by this launch's claim
+// pass; that row persists its Utf8 key bytes here) or the key persisted by an
+// earlier batch; a row whose key differs (two keys, one hash) is listed for
+// the host merge. False: not added on the device.
+template <int NK>
+__device__ __forceinline__ bool row_group(const Col* k, uint32_t epoch, const Table& t, unsigned char* arena, Hdr* hdr,
+                                          int32_t* coll_rows, const int32_t* sidx, long long i, unsigned& g) {
+    const int s = sidx[i];
+    if (s < 0) return false;
+    RowKey r;
+    (void)row_key<NK>(k, i, r);
+    const long long rp = t.rep[s];
+    const bool cur = (unsigned)((unsigned long long)rp >> 32) == epoch;
+    const long long rr = (long long)(unsigned)rp;
+    bool same = t.knull[s] == r.nullm;
+    if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
+#pragma unroll
+        for (int p = 0; p < NK; ++p)
+            if (r.s[p]) {
+                u8* dst = arena + t.kw[(u64)s * kMaxKeys + p];
+                for (unsigned j = 0; j < r.len[p]; ++j) dst[j] = r.s[p][j];
+            }
+    } else {
+#pragma unroll
+        for (int p = 0; p < NK; ++p) {
+            if (!same || ((r.nullm >> p) & 1)) continue;
+            const u64 kwv = t.kw[(u64)s * kMaxKeys + p];
+            if (r.s[p]) {
+                const unsigned kl = t.klen[(u64)s * kMaxKeys + p];
+                const u8* other = cur ? (const u8*)k[p].values + k[p].offsets[rr] : arena + kwv;
+                same = kl == r.len[p] && bytes_eq(r.s[p], other, kl);
+            } else {
+                same = kwv == r.w[p];
+            }
+        }
+    }
+    if (same) {
+        g = t.gid[s];
+        return true;
+    }
+    const u64 at = atomicAdd(&hdr->collided, 1ull);  // two keys, one hash: the host merges this row
+    coll_rows[at] = (int)i;
+    return false;
+}
+
 // One wave per 64 consecutive rows. A row whose slot holds its key adds into
 // the group's record; rows of one group within the wave are first reduced
 // across the wave (the group's leader lane adds once per word) as long as the
@@ -324,51 +370,11 @@ __device__ __forceinline__ void agg_dispatch(const AggCol& ac, u64* rec, long lo
 template <int NK>
 __global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
     const int lane = threadIdx.x & 63;
-    const Table& t = A.t;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long base = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < A.m; base += stride) {
         const long long i = base + lane;
-        bool ok = false;
         unsigned g = 0;
-        if (i < A.m) {
-            const int s = A.sidx[i];
-            if (s >= 0) {
-                RowKey r;
-                (void)row_key<NK>(A.k, i, r);
-                const long long rp = t.rep[s];
-                const bool cur = (unsigned)((unsigned long long)rp >> 32) == A.epoch;
-                const long long rr = (long long)(unsigned)rp;
-                bool same = t.knull[s] == r.nullm;
-                if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
-#pragma unroll
-                    for (int p = 0; p < NK; ++p)
-                        if (r.s[p]) {
-                            u8* dst = A.arena + t.kw[(u64)s * kMaxKeys + p];
-                            for (unsigned j = 0; j < r.len[p]; ++j) dst[j] = r.s[p][j];
-                        }
-                } else {
-#pragma unroll
-                    for (int p = 0; p < NK; ++p) {
-                        if (!same || ((r.nullm >> p) & 1)) continue;
-                        const u64 kwv = t.kw[(u64)s * kMaxKeys + p];
-                        if (r.s[p]) {
-                            const unsigned kl = t.klen[(u64)s * kMaxKeys + p];
-                            const u8* other = cur ? (const u8*)A.k[p].values + A.k[p].offsets[rr] : A.arena + kwv;
-                            same = kl == r.len[p] && bytes_eq(r.s[p], other, kl);
-                        } else {
-                            same = kwv == r.w[p];
-                        }
-                    }
-                }
-                if (same) {
-                    ok = true;
-                    g = t.gid[s];
-                } else {  // two keys, one hash: the host merges this row
-                    const u64 at = atomicAdd(&A.hdr->collided, 1ull);
-                    A.coll_rows[at] = (int)i;
-                }
-            }
-        }
+        const bool ok = i < A.m && row_group<NK>(A.k, A.epoch, A.t, A.arena, A.hdr, A.coll_rows, A.sidx, i, g);
         u64 active = __ballot(ok);
         int singles = 0;
         while (active) {
@@ -387,6 +393,178 @@ __global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
             atomicAdd(&rec[0], 1ull);
             for (int j = 0; j < A.naggs; ++j) agg_dispatch(A.a[j], rec, i, true, 0, 0, lane);
         }
+    }
+}
+
+// --------------------------------------------------- bucketed accumulation
+// (groupby.h "Bucketed accumulation"). The rank and scatter passes run
+// kBucketBlocks blocks of 256 threads over the same rows per block (the same
+// grid-stride), so a block's rows of a bucket fill exactly its positions.
+template <int NK>
+__global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
+    __shared__ unsigned cnt[kBucketMax];
+    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
+        unsigned g = 0;
+        const bool ok = row_group<NK>(A.k, A.epoch, A.t, A.arena, A.hdr, A.coll_rows, A.sidx, i, g);
+        A.rg[i] = ok ? g : ~0u;
+        if (ok) atomicAdd(&cnt[g / A.gpb], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) A.bh[b * kBucketBlocks + blockIdx.x] = cnt[b];
+}
+
+// Exclusive scan of n counts (one block): base[i] = sum of cnt[0 .. i), base[n] the total.
+__global__ __launch_bounds__(1024) void k_group_scan(const unsigned* cnt, unsigned* base, int n) {
+    __shared__ unsigned part[1024];
+    const int t = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int i0 = t * per < n ? t * per : n, i1 = i0 + per < n ? i0 + per : n;
+    unsigned s = 0;
+    for (int i = i0; i < i1; ++i) s += cnt[i];
+    part[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const unsigned v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    unsigned run = t ? part[t - 1] : 0u;
+    for (int i = i0; i < i1; ++i) {
+        base[i] = run;
+        run += cnt[i];
+    }
+    if (t == 1023) base[n] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_group_scatter(const ScatterArgs A) {
+    __shared__ unsigned cur[kBucketMax];
+    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cur[b] = A.base[b * kBucketBlocks + blockIdx.x];
+    __syncthreads();
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
+        const unsigned g = A.rg[i];
+        if (g == ~0u) continue;
+        const unsigned pos = atomicAdd(&cur[g / A.gpb], 1u);
+        A.pg[pos] = g;
+        if (A.pn) {
+            unsigned nm = 0;
+            for (int j = 0; j < A.naggs; ++j)
+                if (!valid_at(A.arg[j], i)) nm |= 1u << j;
+            A.pn[pos] = nm;
+        }
+        for (int c = 0; c < A.npay; ++c) A.pv[(u64)c * (u64)A.m + pos] = key_bits(A.pay[c], i);
+    }
+}
+
+// agg_step's per-lane rules on an LDS record (ds atomics).
+__device__ __forceinline__ void lds_fsum_add(u64* limbs, double v) {
+    int d;
+    long long c0, c1, c2;
+    fsum_pieces(v, d, c0, c1, c2);
+    if (c0) atomicAdd(&limbs[d], (u64)c0);
+    if (c1) atomicAdd(&limbs[d + 1], (u64)c1);
+    if (c2) atomicAdd(&limbs[d + 2], (u64)c2);
+}
+
+template <typename T>
+__device__ __forceinline__ void lds_agg_step(const AggCol& ac, u64* rec, bool null, u64 bits) {
+    u64* w = rec + ac.off;
+    if (null) {
+        atomicAdd(&w[0], 1ull);  // a NULL value
+        return;
+    }
+    if constexpr (!__is_same(T, bool)) {
+        const int fn = ac.fn;
+        if (fn == DFMI_AGG_COUNT) return;
+        T v;
+        if constexpr (__is_same(T, float)) v = __builtin_bit_cast(float, (unsigned)bits);
+        else if constexpr (__is_same(T, double)) v = __builtin_bit_cast(double, bits);
+        else v = (T)bits;  // (integers sign- or zero-extended by key_bits)
+        if (fn == DFMI_AGG_SUM) {
+            if constexpr ((T)0.5 != (T)0) {
+                const unsigned f = agg_sum_flags(v);
+                if (f != F_NNZ) {
+                    atomicAdd(&w[3], 1ull);
+                    if (f) atomicOr(&w[1], (u64)f);
+                } else if (v != (T)0) {
+                    lds_fsum_add(w + 4, (double)v);
+                }
+            } else {
+                const u64 x = (T)-1 < (T)0 ? (u64)(i64)v : (u64)v;
+                if (x) atomicAdd(&w[3], x);
+            }
+            return;
+        }
+        if (agg_isnan(v)) {
+            atomicAdd(&w[3], 1ull);
+        } else if (fn == DFMI_AGG_MIN) {
+            atomicMin(&w[2], agg_key(v));
+        } else {
+            atomicMax(&w[2], agg_key(v));
+        }
+    }
+}
+
+__device__ __forceinline__ void lds_agg_dispatch(const AggCol& ac, u64* rec, bool null, u64 bits) {
+    switch (ac.c.type) {
+        case 2: return lds_agg_step<i8>(ac, rec, null, bits);
+        case 3: return lds_agg_step<i16>(ac, rec, null, bits);
+        case 4: return lds_agg_step<i32>(ac, rec, null, bits);
+        case 5: return lds_agg_step<i64>(ac, rec, null, bits);
+        case 6: return lds_agg_step<u8>(ac, rec, null, bits);
+        case 7: return lds_agg_step<u16>(ac, rec, null, bits);
+        case 8: return lds_agg_step<u32>(ac, rec, null, bits);
+        case 9: return lds_agg_step<u64>(ac, rec, null, bits);
+        case 10: return lds_agg_step<float>(ac, rec, null, bits);
+        case 11: return lds_agg_step<double>(ac, rec, null, bits);
+        default: return lds_agg_step<bool>(ac, rec, null, bits);
+    }
+}
+
+// One block per (bucket, split): the bucket's gpb records in LDS (the zero
+// state), the split's share of the bucket's rows added, then every record word
+// that moved added into the global record (rows / NULLs / sums / digits:
+// add; flags: or; MIN / MAX keys: min / max) -- lanes over consecutive words.
+__global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
+    extern __shared__ u64 lrec[];
+    const int b = blockIdx.x / A.splits, sp = blockIdx.x % A.splits;
+    const u64 g0 = (u64)b * A.gpb;
+    const u64 left = A.ngroups - g0;
+    const unsigned nb = (unsigned)(left < (u64)A.gpb ? left : (u64)A.gpb);
+    const int W = A.words;
+    for (unsigned x = threadIdx.x; x < nb * (unsigned)W; x += blockDim.x) lrec[x] = A.pattern[x % (unsigned)W];
+    __syncthreads();
+    const unsigned r0 = A.base[b * kBucketBlocks], r1 = A.base[(b + 1) * kBucketBlocks];
+    const unsigned len = r1 - r0;
+    const unsigned q0 = r0 + (unsigned)((u64)len * (u64)sp / (u64)A.splits);
+    const unsigned q1 = r0 + (unsigned)((u64)len * (u64)(sp + 1) / (u64)A.splits);
+    for (unsigned pos = q0 + threadIdx.x; pos < q1; pos += blockDim.x) {
+        u64* rec = lrec + (u64)(A.pg[pos] - (unsigned)g0) * (u64)W;
+        atomicAdd(&rec[0], 1ull);
+        const unsigned nm = A.pn ? A.pn[pos] : 0u;
+        for (int j = 0; j < A.naggs; ++j) {
+            const u64 bits = A.pcol[j] >= 0 ? A.pv[(u64)A.pcol[j] * (u64)A.m + pos] : 0ull;
+            lds_agg_dispatch(A.a[j], rec, (nm >> j) & 1, bits);
+        }
+    }
+    __syncthreads();
+    for (unsigned x = threadIdx.x; x < nb * (unsigned)W; x += blockDim.x) {
+        const int w = (int)(x % (unsigned)W);
+        const u64 v = lrec[x];
+        if (v == A.pattern[w]) continue;
+        u64* dst = A.acc + (g0 + x / (unsigned)W) * (u64)W + (u64)w;
+        int j = -1;  // the aggregate owning word w (w = 0: the group's rows)
+        for (int q = 0; q < A.naggs; ++q)
+            if (A.a[q].off <= w) j = q;
+        const int r = j < 0 ? -1 : w - A.a[j].off;
+        if (r == 1) atomicOr(dst, v);
+        else if (r == 2 && A.a[j].fn == DFMI_AGG_MIN) atomicMin(dst, v);
+        else if (r == 2 && A.a[j].fn == DFMI_AGG_MAX) atomicMax(dst, v);
+        else atomicAdd(dst, v);
     }
 }
 
@@ -455,6 +633,107 @@ __global__ __launch_bounds__(256) void k_group_normalize(const NormArgs A) {
     }
 }
 
+// ------------------------------------------------------------ device finish
+// One exact sum (kAggLimbs int64 digits in units of 2^-1074, not necessarily
+// carry-normalised) rounded half to even to `prec` significand bits with a
+// quantum of at least 2^(qmin-1074): aggregate.cpp normalize + round_exact,
+// step for step. The thread's digits 0 .. kAggLimbs-2 live in LDS (`d`, with a
+// stride of kRoundBlock words: consecutive threads, consecutive banks), the top
+// (sign) digit in a register.
+constexpr int kRoundBlock = 128;
+
+__device__ double round_digits(const u64* L, unsigned* d, int prec, int qmin, double overflow_limit, bool& zero) {
+    constexpr int K = kAggLimbs;
+    long long c = 0;
+    for (int i = 0; i < K - 1; ++i) {  // carry-normalise: digits in [0, 2^32), floor carries upward
+        const long long v = (long long)L[i] + c;
+        c = v >> 32;
+        d[i * kRoundBlock] = (unsigned)v;
+    }
+    long long t = (long long)L[K - 1] + c;
+    const bool neg = t < 0;
+    if (neg) {  // the magnitude: two's complement negation of the digit string
+        long long borrow = 0;
+        for (int i = 0; i < K - 1; ++i) {
+            long long v = -(long long)d[i * kRoundBlock] - borrow;
+            borrow = 0;
+            if (v < 0) {
+                v += 4294967296ll;
+                borrow = 1;
+            }
+            d[i * kRoundBlock] = (unsigned)v;
+        }
+        t = -t - borrow;
+    }
+    auto D = [&](int i) -> u64 { return i == K - 1 ? (u64)t : (u64)d[i * kRoundBlock]; };
+    int top = -1;
+    if (t) top = K - 1;
+    else
+        for (int i = K - 2; i >= 0; --i)
+            if (d[i * kRoundBlock]) {
+                top = i;
+                break;
+            }
+    zero = top < 0;
+    if (top < 0) return 0.0;
+    const unsigned lo = (unsigned)D(top);
+    const int msb = 32 * top + (lo ? 31 - __builtin_clz(lo) : 0);
+    int q = msb - (prec - 1) > qmin ? msb - (prec - 1) : qmin;
+    u64 mant = 0;  // bits [q, msb] from the top three digits
+    if (q <= msb) {
+        const int b0 = top - 2 > 0 ? top - 2 : 0;
+        unsigned __int128 w = 0;
+        for (int i = top; i >= b0; --i) w = (w << 32) | (unsigned __int128)D(i);
+        mant = (u64)(w >> (q - 32 * b0)) & ((1ull << (msb - q + 1)) - 1);
+    }
+    auto bit = [&](int i) -> u64 { return i < 0 ? 0 : (D(i >> 5) >> (i & 31)) & 1; };
+    const u64 rb = q >= 1 ? bit(q - 1) : 0;
+    bool sticky = false;  // any set bit in [0, q - 2]
+    if (q >= 2) {
+        const int hb = q - 2, hd = hb >> 5;
+        for (int i = 0; i < hd && !sticky; ++i) sticky = D(i) != 0;
+        const u64 m = (hb & 31) == 31 ? 0xffffffffull : ((1ull << ((hb & 31) + 1)) - 1);
+        sticky = sticky || (D(hd) & m) != 0;
+    }
+    if (rb && (sticky || (mant & 1))) {
+        ++mant;
+        if (mant >> prec) {
+            mant >>= 1;
+            ++q;
+        }
+    }
+    double v = ldexp((double)mant, q - 1074);
+    if (v >= overflow_limit) v = __builtin_inf();
+    return neg ? -v : v;
+}
+
+__global__ __launch_bounds__(kRoundBlock) void k_group_round(const RoundArgs A) {
+    __shared__ unsigned dg[(kAggLimbs - 1) * kRoundBlock];
+    const u64 n = A.ngroups * (u64)A.naggs;
+    const int cw = 1 + 4 * A.naggs;
+    for (u64 x = (u64)blockIdx.x * kRoundBlock + threadIdx.x; x < n; x += (u64)gridDim.x * kRoundBlock) {
+        const u64 g = x / (u64)A.naggs;
+        const int j = (int)(x % (u64)A.naggs);
+        const u64* rec = A.acc + g * (u64)A.words;
+        u64* o = A.out + g * (u64)cw;
+        if (j == 0) o[0] = rec[0];
+        const u64* w = rec + A.off[j];
+        u64* ow = o + 1 + 4 * j;
+        u64 flags = w[1], key = w[2];
+        if (A.kind[j]) {
+            bool zero = false;
+            const double v = A.kind[j] == 2 ? round_digits(w + 4, dg + threadIdx.x, 24, 925, 0x1p128, zero)
+                                            : round_digits(w + 4, dg + threadIdx.x, 53, 0, __builtin_inf(), zero);
+            key = __builtin_bit_cast(u64, v);
+            if (zero) flags |= kRoundZero;
+        }
+        ow[0] = w[0];
+        ow[1] = flags;
+        ow[2] = key;
+        ow[3] = w[3];
+    }
+}
+
 static int grid_for(long long items, int per_block = 256, int cap = 8192) {
     long long g = (items + per_block - 1) / per_block;
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -500,6 +779,13 @@ hipError_t launch_init(u64* acc, const u64* pattern, int words, u64 g0, u64 g1, 
     if (g1 <= g0) return hipSuccess;
     hipLaunchKernelGGL(k_group_init, dim3(grid_for((long long)((g1 - g0) * words))), dim3(256), 0, st, acc, pattern,
                        words, g0, g1);
+    return hipGetLastError();
+}
+
+hipError_t launch_round(const RoundArgs& a, hipStream_t st) {
+    if (!a.ngroups || !a.naggs) return hipSuccess;
+    hipLaunchKernelGGL(k_group_round, dim3(grid_for((long long)(a.ngroups * a.naggs), kRoundBlock)),
+                       dim3(kRoundBlock), 0, st, a);
     return hipGetLastError();
 }
 

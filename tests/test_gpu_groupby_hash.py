@@ -262,3 +262,51 @@ def test_finish_then_more_rows_partial_and_reset():
         assert len(st.finish()[0]) == 0
         st.add(None, slice_batch(db, 0, 10_000), FL)
         check(st.finish(), rk1, rv1, rs1)
+
+
+def _rounding_table(rng, n):
+    """Per group (a Float64 key, hashed) SUMs that exercise every step of the
+    exact rounding: overflow to +-inf, exact cancellation (+0.0) and sums of
+    -0.0 (-0.0), subnormal sums, ties to even at 2^-53 and at Float32's
+    2^-24, Float32 sums past 2^128, and wild doubles over the whole exponent
+    range; a Float32 column of the same values narrowed."""
+    g = rng.integers(0, 64, n).astype(np.float64)
+    x = wild_doubles(rng, n)
+    grp = rng.integers(0, 8, n)
+    x[grp == 0] = 1.7e308 * np.where(rng.random(int((grp == 0).sum())) < 0.7, 1.0, -1.0)
+    x[grp == 1] = -0.0
+    x[grp == 2] = np.ldexp(rng.integers(-9, 10, int((grp == 2).sum())).astype(np.float64), -1074)
+    x[grp == 3] = np.where(rng.random(int((grp == 3).sum())) < 0.5, 1.0, np.ldexp(1.0, -53))
+    x[grp == 4] = np.where(rng.random(int((grp == 4).sum())) < 0.5, 3.0e38, np.ldexp(1.0, -24))
+    g[grp <= 4] = 100 + grp[grp <= 4] * 1000 + rng.integers(0, 3, int((grp <= 4).sum()))
+    f32 = np.clip(x, -3.4e38, 3.4e38).astype(np.float32)
+    s = Schema([Field("g", DataType.Float64, True), Field("x", DataType.Float64, True),
+                Field("y", DataType.Float32, True)])
+    return s, RecordBatch(s, [Array.from_numpy(DataType.Float64, g, rng.random(n) >= 0.02),
+                              Array.from_numpy(DataType.Float64, x, rng.random(n) >= 0.05),
+                              Array.from_numpy(DataType.Float32, f32, rng.random(n) >= 0.05)])
+
+
+def test_group_by_device_finish_rounding(monkeypatch):
+    """The finish rounds every group's exact sum on the device (groupby.hip
+    k_group_round): bit-identical to the oracle and to the host's rounding of
+    the same table (DFMI_GROUP_HOST_FINISH=1, the A/B), for Float64 and
+    Float32 SUMs, one batch and several, and for two keys."""
+    rng = np.random.default_rng(69)
+    s, b = _rounding_table(rng, 60_000)
+    aggs_e = [agg("SUM", Column(1), s), agg("SUM", Column(2), s), agg("COUNT", Column(1), s),
+              agg("MIN", Column(2), s), agg("MAX", Column(1), s)]
+    for keys in ([Column(0)], [Column(0), Column(2)]):
+        for br in (0, 17_000):
+            dev = run_multi(s, b, None, keys, aggs_e, batch_rows=br)
+            assert dev is not None and len(dev[0]) > 60
+            monkeypatch.setenv("DFMI_DIAG", "1")
+            monkeypatch.setenv("DFMI_GROUP_HOST_FINISH", "1")
+            host = run_multi(s, b, None, keys, aggs_e, batch_rows=br)
+            monkeypatch.delenv("DFMI_DIAG")
+            monkeypatch.delenv("DFMI_GROUP_HOST_FINISH")
+            assert [_vals(v) for v in dev[1]] == [_vals(v) for v in host[1]]
+    # the specials really occur among the device's results
+    f64 = {int(v[0].bits) for v in run_multi(s, b, None, [Column(0)], aggs_e)[1] if not v[0].is_null}
+    assert 0x7FF0000000000000 in f64 or 0xFFF0000000000000 in f64
+    assert 0x8000000000000000 in f64
