@@ -1082,9 +1082,13 @@ def groupby_line(eng, dev, rank, world, steps, warmup, dist, rows=GROUPBY_ROWS):
     dfmi_aggregate_batch (fused evaluation pass, hash-table claim and
     accumulate passes) plus the finish (every group back in key order).
     Exact Float64 SUM. Gate: a 2^20-row prefix against the oracle, keys and
-    values bit for bit. Atomic-bound (scattered 8-byte atomics into the
-    groups' records), not HBM-bound: `roofline` reports the algorithmic bytes'
-    rate only for scale."""
+    values bit for bit. The batch has 1e4 rows per group, so the bucketed
+    passes run (groupby.h: claim, rank, scatter by bucket, per-bucket LDS
+    sums): `pass_bytes_per_row` counts what those passes move per row (the
+    claim reads the key and writes the slot index, the rank reads both and
+    writes the group id, the scatter reads it and v and writes both, the
+    bucket pass reads them back), `frac` the algorithmic bytes' rate over
+    the HBM peak."""
     from datafusion_amd.arrow import Array, RecordBatch
     from datafusion_amd.execution.expression import compile_expr
     from datafusion_amd.logicalplan import AggregateFunction
@@ -1172,11 +1176,16 @@ def groupby_line(eng, dev, rank, world, steps, warmup, dist, rows=GROUPBY_ROWS):
         kb = sum(4 + float(c.values.numel()) / n if c.data_type == DataType.Utf8 else c.data_type.width for c in kcols)
         bpr = kb + 8.0
         ms = el / steps * 1e3
+        pbr = 2 * kb + 48.0  # claim kb + 4, rank 4 + kb + 4, scatter 4 + 8 + 4 + 8, bucket 4 + 8
         out[name] = {"rows_per_s": n * world * steps / el, "ms_per_step": round(ms, 3), "groups": groups,
                      "parity_gate": {"rows": m, "groups": len(rk), "bit_identical_to_oracle": bool(ok)},
                      "algorithmic_bytes_per_row": round(bpr, 3),
                      "achieved_gbs": round(n * bpr / (ms * 1e-3) / 1e9, 1),
-                     "bound": "device atomics into the groups' records (not HBM)"}
+                     "frac": round(n * bpr / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "pass_bytes_per_row": round(pbr, 3),
+                     "pass_gbs": round(n * pbr / (ms * 1e-3) / 1e9, 1),
+                     "bound": "the passes' dependent table reads (claim, rank), the scatter's LDS position "
+                              "atomics and the bucket pass's LDS atomics; the whole step incl. finish"}
     del utf8, data, offs, cases
     return out
 

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -821,7 +822,7 @@ void group_batch_on_host(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progr
 // ---- the device hash table (groupby.h)
 void free_hashdev(HashDev* H) {
     if (!H) return;
-    void* ps[] = {H->t.ctl, H->t.rep, H->t.gid, H->t.kw, H->t.klen, H->t.knull, H->hdr, H->arena,
+    void* ps[] = {H->t.ctl, H->t.slot, H->hdr, H->arena,
                   H->acc, H->pattern, H->sidx, H->coll};
     for (void* p : ps)
         if (p) (void)hipFree(p);
@@ -834,17 +835,13 @@ void free_hashdev(HashDev* H) {
 void alloc_table(dfmi::gb::Table& t, uint64_t cap, hipStream_t stream) {
     t = dfmi::gb::Table{};
     HIP_TRY(hipMalloc((void**)&t.ctl, cap * 8));
-    HIP_TRY(hipMalloc((void**)&t.rep, cap * 8));
-    HIP_TRY(hipMalloc((void**)&t.gid, cap * 4));
-    HIP_TRY(hipMalloc((void**)&t.kw, cap * 8 * dfmi::gb::kMaxKeys));
-    HIP_TRY(hipMalloc((void**)&t.klen, cap * 4 * dfmi::gb::kMaxKeys));
-    HIP_TRY(hipMalloc((void**)&t.knull, cap * 4));
+    HIP_TRY(hipMalloc((void**)&t.slot, cap * sizeof(dfmi::gb::Slot)));
     HIP_TRY(hipMemsetAsync(t.ctl, 0, cap * 8, stream));
     t.mask = cap - 1;
 }
 
 void free_table(dfmi::gb::Table& t) {
-    void* ps[] = {t.ctl, t.rep, t.gid, t.kw, t.klen, t.knull};
+    void* ps[] = {t.ctl, t.slot};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     t = dfmi::gb::Table{};
@@ -917,6 +914,111 @@ void regrow(dfmi_context* ctx, T*& p, size_t keep, size_t want) {
     p = q;
 }
 
+// Bucketed accumulation (groupby.h): worth it when the batch has many rows per
+// group -- the per-bucket sums then replace ~(2 + 3 per float SUM) scattered
+// record atomics per row by LDS atomics, and each (bucket, split) block adds
+// a group's moved words once. Needs the bucket's records in 56 KiB of LDS
+// and at most kBucketMax buckets. DFMI_DIAG=1 DFMI_GROUP_BUCKETS=0 / 1
+// forces the choice (tests run small batches through both).
+constexpr size_t kBucketBuf = kDrainBuf + 8;
+
+struct BucketShape {
+    uint32_t gpb = 0;  // a power of two: 1 << gshift
+    int gshift = 0;
+    int nbuckets = 0, splits = 0;
+};
+
+BucketShape bucket_shape(const HashDev& H, uint64_t ng) {
+    BucketShape b;
+    const size_t fit = 57344 / ((size_t)H.words * 8);  // records in 56 KiB of LDS (+ the block's bucket starts)
+    if (!fit || !ng) return b;
+    while ((2ull << b.gshift) <= fit) ++b.gshift;
+    b.gpb = 1u << b.gshift;
+    b.nbuckets = (int)((ng + b.gpb - 1) / b.gpb);
+    b.splits = std::max(1, std::min(1024, 2048 / std::max(1, b.nbuckets)));
+    return b;
+}
+
+bool use_buckets(const dfmi_agg_state* st, const HashDev& H, int64_t m, uint64_t ng) {
+    const BucketShape b = bucket_shape(H, ng);
+    if (!b.gpb || b.nbuckets > dfmi::gb::kBucketMax || st->aggs.size() > 32) return false;
+    if (getenv("DFMI_DIAG"))
+        if (const char* e = getenv("DFMI_GROUP_BUCKETS")) return atoi(e) != 0;
+    // ~4 record atomics per row against each block adding a touched group's
+    // ~10 moved words once: many rows per group and split
+    return (uint64_t)m >= 4ull * ng * (uint64_t)b.splits && m >= (1 << 20);
+}
+
+std::atomic<long> g_bucketed_batches{0};  // diagnostics: dfmi_internal_group_bucketed_batches
+
+void accumulate_bucketed(dfmi_context* ctx, dfmi_agg_state* st, HashDev& H, const std::vector<dfmi::gb::Col>& cols,
+                         int64_t m, uint64_t ng, uint32_t epoch) {
+    g_bucketed_batches.fetch_add(1);
+    const size_t nk = st->keys.size(), n = st->aggs.size();
+    const BucketShape sh = bucket_shape(H, ng);
+    const size_t nbh = (size_t)sh.nbuckets * dfmi::gb::kBucketBlocks;
+    dfmi::gb::RankArgs ra{};
+    for (size_t p = 0; p < nk; ++p) ra.k[p] = cols[p];
+    ra.nkeys = (int)nk;
+    ra.epoch = epoch;
+    ra.m = m;
+    ra.t = H.t;
+    ra.arena = H.arena;
+    ra.sidx = H.sidx;
+    ra.hdr = H.hdr;
+    ra.coll_rows = H.coll;
+    ra.rg = (unsigned*)hd_buf(H, kBucketBuf, (size_t)m * 4);
+    ra.gshift = sh.gshift;
+    ra.nbuckets = sh.nbuckets;
+    ra.bh = (unsigned*)hd_buf(H, kBucketBuf + 1, nbh * 4);
+    dfmi::gb::ScatterArgs sa{};
+    sa.m = m;
+    sa.rg = ra.rg;
+    sa.gshift = sh.gshift;
+    sa.nbuckets = sh.nbuckets;
+    sa.base = ra.bh;
+    sa.tot = (const unsigned*)hd_buf(H, kBucketBuf + 2, (size_t)sh.nbuckets * 4);
+    sa.naggs = (int)n;
+    dfmi::gb::BucketArgs ba{};
+    bool nullable = false;
+    int npay = 0;
+    for (size_t j = 0; j < n; ++j) {
+        const dfmi::gb::Col& c = cols[nk + j];
+        sa.arg[j] = c;
+        nullable = nullable || c.validity;
+        ba.a[j].c = c;
+        ba.a[j].fn = st->aggs[j]->fn;
+        ba.a[j].off = H.off[j];
+        ba.pcol[j] = -1;
+        const bool needs = st->aggs[j]->fn != DFMI_AGG_COUNT && c.type != DFMI_TYPE_UTF8 && c.type != DFMI_TYPE_BOOLEAN;
+        if (!needs) continue;
+        for (int q = 0; q < npay && ba.pcol[j] < 0; ++q)  // one payload column per distinct argument column
+            if (sa.pay[q].values == c.values && sa.pay[q].type == c.type) ba.pcol[j] = q;
+        if (ba.pcol[j] < 0) {
+            sa.pay[npay] = c;
+            ba.pcol[j] = npay++;
+        }
+    }
+    sa.npay = npay;
+    sa.pg = (unsigned*)hd_buf(H, kBucketBuf + 3, (size_t)m * 4);
+    sa.pn = nullable ? (unsigned*)hd_buf(H, kBucketBuf + 4, (size_t)m * 4) : nullptr;
+    sa.pv = (unsigned long long*)hd_buf(H, kBucketBuf + 5, (size_t)std::max(npay, 1) * (size_t)m * 8);
+    ba.m = m;
+    ba.tot = sa.tot;
+    ba.gpb = sh.gpb;
+    ba.nbuckets = sh.nbuckets;
+    ba.splits = sh.splits;
+    ba.ngroups = ng;
+    ba.pg = sa.pg;
+    ba.pn = sa.pn;
+    ba.pv = sa.pv;
+    ba.naggs = (int)n;
+    ba.words = H.words;
+    ba.acc = H.acc;
+    ba.pattern = H.pattern;
+    HIP_TRY(dfmi::gb::launch_buckets(ra, sa, ba, ctx->stream));
+}
+
 // One batch through the device hash table: the fused evaluation pass, the
 // claim pass (the table grown and the pass run again while a row finds no
 // slot), the accumulate pass; rows whose key shares its hash with another
@@ -981,6 +1083,10 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
         HIP_TRY(dfmi::gb::launch_normalize(H.acc, H.words, H.foff.data(), (int)H.foff.size(), H.ngroups, stream));
         H.rows_since_norm = 0;
     }
+    HIP_TRY(hipMemsetAsync(&H.hdr->collided, 0, 8, stream));
+    if (use_buckets(st, H, m, ng)) {
+        accumulate_bucketed(ctx, st, H, cols, m, ng, ca.epoch);
+    } else {
     dfmi::gb::AccArgs aa{};
     for (size_t p = 0; p < nk; ++p) aa.k[p] = cols[p];
     aa.nkeys = (int)nk;
@@ -999,8 +1105,8 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
     aa.acc = H.acc;
     aa.hdr = H.hdr;
     aa.coll_rows = H.coll;
-    HIP_TRY(hipMemsetAsync(&H.hdr->collided, 0, 8, stream));
     HIP_TRY(dfmi::gb::launch_accumulate(aa, stream));
+    }
     read_hdr(ctx, H);
     H.ngroups = ng;
     H.rows_since_norm += (uint64_t)m;
@@ -2062,6 +2168,9 @@ extern "C" int32_t dfmi_agg_merge_partials(const dfmi_aggregate* const* aggs, in
 // Internal test hook (not part of the C ABI, not declared in include/): the
 // aggregate kernel a dfmi_aggregate_batch call would launch, generated and
 // (compile != 0) compiled with hipRTC -- no device needed (tests/test_aggregate_cpu.py).
+// Diagnostics: grouped batches accumulated by the bucketed passes (groupby.h) in this process.
+extern "C" long dfmi_internal_group_bucketed_batches() { return g_bucketed_batches.load(); }
+
 extern "C" int64_t dfmi_internal_agg_jit_check(const dfmi_program* pred, const dfmi_aggregate* const* aggs, int32_t n,
                                                const dfmi_batch* in, uint32_t flags, int32_t compile, char* buf,
                                                int64_t cap, dfmi_error* err) {

@@ -45,14 +45,21 @@ struct Col {
     const uint8_t* validity;   // nullptr: every value valid
 };
 
-// The table (struct of arrays, capacity cap = mask + 1 slots).
+// A slot's record: one 64-byte line piece, so a row's check of its slot
+// (k_group_rank / row_group) is one random access, not one per field.
+struct alignas(64) Slot {
+    long long rep;                    // (epoch << 32) | representative row of the claiming batch
+    unsigned gid;                     // dense group id
+    unsigned knull;                   // bit p: key part p is null
+    unsigned long long kw[kMaxKeys];  // persisted key words (Utf8: arena offset)
+    unsigned klen[kMaxKeys];          // Utf8 key bytes
+};
+
+// The table (capacity cap = mask + 1 slots): the probe words apart (dense for
+// the claim's linear probing), the slots' records beside them.
 struct Table {
     unsigned long long* ctl;   // [cap] 0: empty; else the key's hash | 1 (written once, by CAS)
-    long long* rep;            // [cap] (epoch << 32) | representative row of the claiming batch
-    unsigned* gid;             // [cap] dense group id
-    unsigned long long* kw;    // [cap][kMaxKeys] persisted key words (Utf8: arena offset)
-    unsigned* klen;            // [cap][kMaxKeys] Utf8 key bytes
-    unsigned* knull;           // [cap] bit p: key part p is null
+    Slot* slot;                // [cap]
     unsigned long long mask;   // cap - 1
 };
 
@@ -112,9 +119,11 @@ struct AccArgs {
 //   k_group_rank     the accumulate pass's key check per row (the same
 //                    representative / persisted-key rules, colliding rows
 //                    listed); the row's group id into rg, and per block the
-//                    rows of each bucket (gpb consecutive group ids) into bh
-//   k_group_scan     exclusive scan of bh, bucket-major: every (bucket,
-//                    block) its first position
+//                    rows of each bucket (gpb = 2^gshift consecutive group
+//                    ids) into bh
+//   k_group_scan     per bucket, the exclusive prefix of its per-block
+//                    counts (in place) and its total; a bucket starts at the
+//                    sum of the totals before it
 //   k_group_scatter  the same rows per block as the rank pass: each placed
 //                    row's group id, NULL mask and argument bits written at
 //                    its bucket's next position (LDS counters)
@@ -123,8 +132,8 @@ struct AccArgs {
 //                    each record word that moved added once into the
 //                    group's global record (atomics over contiguous words)
 // Integer digit sums are order-free: the records equal the accumulate pass's.
-constexpr int kBucketMax = 256;   // buckets per pass
-constexpr int kBucketBlocks = 1024;  // blocks of the rank and scatter passes
+constexpr int kBucketMax = 1024;  // buckets per pass
+constexpr int kBucketBlocks = 1024;  // blocks of the rank and scatter passes (= k_group_scan's block size)
 
 struct RankArgs {
     Col k[kMaxKeys];
@@ -137,17 +146,18 @@ struct RankArgs {
     Hdr* hdr;
     int32_t* coll_rows;
     unsigned* rg;      // [m] the row's group id, ~0u: not added here (listed)
-    uint32_t gpb;      // groups per bucket
+    int32_t gshift;    // groups per bucket: 1 << gshift
     int32_t nbuckets;
-    unsigned* bh;      // [nbuckets][kBucketBlocks] rows per (bucket, block); [nbuckets * kBucketBlocks]: total
+    unsigned* bh;      // [nbuckets][kBucketBlocks] rows per (bucket, block) (k_group_scan: their exclusive prefixes)
 };
 
 struct ScatterArgs {
     long long m;
     const unsigned* rg;
-    uint32_t gpb;
+    int32_t gshift;
     int32_t nbuckets;
-    const unsigned* base;        // k_group_scan's output
+    const unsigned* base;        // k_group_scan's output: per (bucket, block) its first position in the bucket
+    const unsigned* tot;         // [nbuckets] rows per bucket
     int32_t naggs;
     Col arg[kMaxAggs];           // aggregate j's argument column (its NULLs)
     Col pay[kMaxAggs];           // payload column c's source (the arguments whose values are needed, once each)
@@ -159,7 +169,7 @@ struct ScatterArgs {
 
 struct BucketArgs {
     long long m;                 // pv's column stride
-    const unsigned* base;
+    const unsigned* tot;
     uint32_t gpb;
     int32_t nbuckets;
     int32_t splits;              // blocks per bucket

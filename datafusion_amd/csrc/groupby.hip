@@ -75,7 +75,7 @@ struct RowKey {
     unsigned len[kMaxKeys];
 };
 
-template <int NK>
+template <int NK, bool HASH = true>
 __device__ __forceinline__ u64 row_key(const Col* k, long long i, RowKey& r) {
     u64 h = 0x243F6A8885A308D3ull;
     r.nullm = 0;
@@ -92,7 +92,7 @@ __device__ __forceinline__ u64 row_key(const Col* k, long long i, RowKey& r) {
             const int a = c.offsets[i], b = c.offsets[i + 1];
             r.s[p] = (const u8*)c.values + a;
             r.len[p] = (unsigned)(b - a);
-            h = hash_bytes(r.s[p], r.len[p], h + (u64)p);
+            if (HASH) h = hash_bytes(r.s[p], r.len[p], h + (u64)p);
         } else {
             r.w[p] = key_bits(c, i);
             h = gmix(h ^ (r.w[p] * 0xD6E8FEB86659FD93ull + (u64)p));
@@ -102,7 +102,56 @@ __device__ __forceinline__ u64 row_key(const Col* k, long long i, RowKey& r) {
 }
 
 // ------------------------------------------------------------ claim pass
-// NK: key parts (a template parameter so a row's key stays in registers)
+// One row's slot: linear probing from slot s, whose probe word the caller has
+// already loaded (`cur`); an empty slot is claimed with a CAS. -1: no slot
+// (the table is at its load limit, or the probe ran past kProbeMax slots: the
+// host grows the table and runs the pass again -- every row again, so a row
+// given up here is placed then).
+constexpr u64 kProbeMax = 4096;
+
+template <int NK>
+__device__ __forceinline__ int claim_row(const ClaimArgs& A, const RowKey& r, u64 c, u64 s, u64 cur, long long i) {
+    const Table& t = A.t;
+    if (__hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit) return -1;
+    for (u64 probe = 0; probe <= t.mask && probe < kProbeMax; ++probe) {
+        if (probe) {
+            s = (s + 1) & t.mask;
+            cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (cur == 0) {
+            if (__hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit) return -1;
+            cur = atomicCAS(&t.ctl[s], 0ull, c);
+            if (cur == 0) {  // claimed: this row represents the slot's key
+                Slot& sr = t.slot[s];
+                // the next dense group id: one counter add per wave for the lanes claiming together
+                // (a single counter takes ~88 adds per us: MI355X_MICROARCH.md "dequeue")
+                const u64 cl = __ballot(1);
+                const int lead = __builtin_ctzll(cl);
+                const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(cl >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)cl, 0u));
+                u64 g0 = 0;
+                if (below == 0) g0 = atomicAdd(&A.hdr->ngroups, (u64)__builtin_popcountll(cl));
+                g0 = readlane_u64(g0, lead);
+                sr.gid = (unsigned)(g0 + below);
+                sr.rep = ((long long)A.epoch << 32) | (long long)(unsigned)i;
+                sr.knull = r.nullm;
+#pragma unroll
+                for (int p = 0; p < NK; ++p) {
+                    u64 w = r.w[p];
+                    if (r.s[p]) w = atomicAdd(&A.hdr->arena_end, (u64)r.len[p]);
+                    sr.kw[p] = w;
+                    sr.klen[p] = r.len[p];
+                }
+                return (int)s;
+            }
+        }
+        if (cur == c) return (int)s;
+    }
+    return -1;
+}
+
+// NK: key parts (a template parameter so a row's key stays in registers).
+// One row per thread (4 rows per thread with their first probes loaded
+// together measured slower: 0.90 -> 1.13 ms per 1e8 rows).
 template <int NK>
 __global__ __launch_bounds__(256) void k_group_claim(const ClaimArgs A) {
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -110,38 +159,10 @@ __global__ __launch_bounds__(256) void k_group_claim(const ClaimArgs A) {
     bool overflow = false;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
         RowKey r;
-        const u64 h = row_key<NK>(A.k, i, r);
-        const u64 c = (h & A.hash_mask) | 1ull;
-        u64 s = gmix(c) & t.mask;
-        int res = -1;
-        for (u64 probe = 0; probe <= t.mask; ++probe, s = (s + 1) & t.mask) {
-            u64 cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cur == 0) {
-                if (__hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit) {
-                    overflow = true;
-                    break;
-                }
-                cur = atomicCAS(&t.ctl[s], 0ull, c);
-                if (cur == 0) {  // claimed: this row represents the slot's key
-                    t.gid[s] = (unsigned)atomicAdd(&A.hdr->ngroups, 1ull);
-                    t.rep[s] = ((long long)A.epoch << 32) | (long long)(unsigned)i;
-                    t.knull[s] = r.nullm;
-#pragma unroll
-                    for (int p = 0; p < NK; ++p) {
-                        u64 w = r.w[p];
-                        if (r.s[p]) w = atomicAdd(&A.hdr->arena_end, (u64)r.len[p]);
-                        t.kw[s * kMaxKeys + p] = w;
-                        t.klen[s * kMaxKeys + p] = r.len[p];
-                    }
-                    res = (int)s;
-                    break;
-                }
-            }
-            if (cur == c) {
-                res = (int)s;
-                break;
-            }
-        }
+        const u64 c = (row_key<NK>(A.k, i, r) & A.hash_mask) | 1ull;
+        const u64 s = gmix(c) & t.mask;
+        const u64 cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int res = cur == c ? (int)s : claim_row<NK>(A, r, c, s, cur, i);
         if (res < 0) overflow = true;
         A.sidx[i] = res;
     }
@@ -328,24 +349,25 @@ __device__ __forceinline__ bool row_group(const Col* k, uint32_t epoch, const Ta
     if (s < 0) return false;
     RowKey r;
     (void)row_key<NK>(k, i, r);
-    const long long rp = t.rep[s];
+    const Slot sr = t.slot[s];
+    const long long rp = sr.rep;
     const bool cur = (unsigned)((unsigned long long)rp >> 32) == epoch;
     const long long rr = (long long)(unsigned)rp;
-    bool same = t.knull[s] == r.nullm;
+    bool same = sr.knull == r.nullm;
     if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
 #pragma unroll
         for (int p = 0; p < NK; ++p)
             if (r.s[p]) {
-                u8* dst = arena + t.kw[(u64)s * kMaxKeys + p];
+                u8* dst = arena + sr.kw[p];
                 for (unsigned j = 0; j < r.len[p]; ++j) dst[j] = r.s[p][j];
             }
     } else {
 #pragma unroll
         for (int p = 0; p < NK; ++p) {
             if (!same || ((r.nullm >> p) & 1)) continue;
-            const u64 kwv = t.kw[(u64)s * kMaxKeys + p];
+            const u64 kwv = sr.kw[p];
             if (r.s[p]) {
-                const unsigned kl = t.klen[(u64)s * kMaxKeys + p];
+                const unsigned kl = sr.klen[p];
                 const u8* other = cur ? (const u8*)k[p].values + k[p].offsets[rr] : arena + kwv;
                 same = kl == r.len[p] && bytes_eq(r.s[p], other, kl);
             } else {
@@ -354,7 +376,7 @@ __device__ __forceinline__ bool row_group(const Col* k, uint32_t epoch, const Ta
         }
     }
     if (same) {
-        g = t.gid[s];
+        g = sr.gid;
         return true;
     }
     const u64 at = atomicAdd(&hdr->collided, 1ull);  // two keys, one hash: the host merges this row
@@ -398,65 +420,149 @@ __global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
 
 // --------------------------------------------------- bucketed accumulation
 // (groupby.h "Bucketed accumulation"). The rank and scatter passes run
-// kBucketBlocks blocks of 256 threads over the same rows per block (the same
-// grid-stride), so a block's rows of a bucket fill exactly its positions.
+// kBucketBlocks blocks of 256 threads over the same tiles of kRankRows rows
+// per block, so a block's rows of a bucket fill exactly its positions.
+constexpr int kRankU = 4;                   // rows per thread per tile (independent load chains)
+constexpr int kRankRows = 256 * kRankU;
+
 template <int NK>
 __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
     __shared__ unsigned cnt[kBucketMax];
     for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
-        unsigned g = 0;
-        const bool ok = row_group<NK>(A.k, A.epoch, A.t, A.arena, A.hdr, A.coll_rows, A.sidx, i, g);
-        A.rg[i] = ok ? g : ~0u;
-        if (ok) atomicAdd(&cnt[g / A.gpb], 1u);
+    const Table& t = A.t;
+    for (long long t0 = (long long)blockIdx.x * kRankRows; t0 < A.m; t0 += (long long)gridDim.x * kRankRows) {
+        // the row_group chain of kRankU rows at once: slots, keys, the slots' words, then the decisions
+        int sl[kRankU];
+        RowKey r[kRankU];
+        Slot sr[kRankU];
+#pragma unroll
+        for (int u = 0; u < kRankU; ++u) {
+            const long long i = t0 + threadIdx.x + 256 * u;
+            sl[u] = i < A.m ? A.sidx[i] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kRankU; ++u) {
+            const long long i = t0 + threadIdx.x + 256 * u;
+            const int s = sl[u] < 0 ? 0 : sl[u];
+            if (sl[u] >= 0) (void)row_key<NK, false>(A.k, i, r[u]);
+            sr[u] = t.slot[s];
+        }
+#pragma unroll
+        for (int u = 0; u < kRankU; ++u) {
+            const long long i = t0 + threadIdx.x + 256 * u;
+            if (i >= A.m) break;
+            const int s = sl[u];
+            bool ok = false;
+            if (s >= 0) {
+                const bool cur = (unsigned)((unsigned long long)sr[u].rep >> 32) == A.epoch;
+                const long long rr = (long long)(unsigned)sr[u].rep;
+                bool same = sr[u].knull == r[u].nullm;
+                if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
+#pragma unroll
+                    for (int p = 0; p < NK; ++p)
+                        if (r[u].s[p]) {
+                            u8* dst = A.arena + sr[u].kw[p];
+                            for (unsigned j = 0; j < r[u].len[p]; ++j) dst[j] = r[u].s[p][j];
+                        }
+                } else {
+#pragma unroll
+                    for (int p = 0; p < NK; ++p) {
+                        if (!same || ((r[u].nullm >> p) & 1)) continue;
+                        if (r[u].s[p]) {
+                            const unsigned kl = sr[u].klen[p];
+                            const u8* other = cur ? (const u8*)A.k[p].values + A.k[p].offsets[rr] : A.arena + sr[u].kw[p];
+                            same = kl == r[u].len[p] && bytes_eq(r[u].s[p], other, kl);
+                        } else {
+                            same = sr[u].kw[p] == r[u].w[p];
+                        }
+                    }
+                }
+                if (same) {
+                    ok = true;
+                } else {  // two keys, one hash: the host merges this row
+                    const u64 at = atomicAdd(&A.hdr->collided, 1ull);
+                    A.coll_rows[at] = (int)i;
+                }
+            }
+            A.rg[i] = ok ? sr[u].gid : ~0u;
+            if (ok) atomicAdd(&cnt[sr[u].gid >> A.gshift], 1u);
+        }
     }
     __syncthreads();
     for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) A.bh[b * kBucketBlocks + blockIdx.x] = cnt[b];
 }
 
-// Exclusive scan of n counts (one block): base[i] = sum of cnt[0 .. i), base[n] the total.
-__global__ __launch_bounds__(1024) void k_group_scan(const unsigned* cnt, unsigned* base, int n) {
-    __shared__ unsigned part[1024];
-    const int t = threadIdx.x;
-    const int per = (n + 1023) / 1024;
-    const int i0 = t * per < n ? t * per : n, i1 = i0 + per < n ? i0 + per : n;
-    unsigned s = 0;
-    for (int i = i0; i < i1; ++i) s += cnt[i];
-    part[t] = s;
+// One block of kBucketBlocks threads per bucket: its per-block counts turned
+// into exclusive prefixes in place, the bucket's total into tot[b].
+__global__ __launch_bounds__(kBucketBlocks) void k_group_scan(unsigned* bh, unsigned* tot) {
+    __shared__ unsigned wsum[kBucketBlocks / 64];
+    unsigned* c = bh + (u64)blockIdx.x * kBucketBlocks;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const unsigned v = c[t];
+    const unsigned incl = (unsigned)wave_incl_scan((u64)v, lane);
+    if (lane == 63) wsum[w] = incl;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const unsigned v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    unsigned before = 0, all = 0;
+    for (int q = 0; q < kBucketBlocks / 64; ++q) {
+        if (q < w) before += wsum[q];
+        all += wsum[q];
     }
-    unsigned run = t ? part[t - 1] : 0u;
-    for (int i = i0; i < i1; ++i) {
-        base[i] = run;
-        run += cnt[i];
+    c[t] = before + incl - v;
+    if (t == 0) tot[blockIdx.x] = all;
+}
+
+// The first position of every bucket (exclusive prefix of the totals) into
+// LDS, start[nb] the placed rows (256 threads, kBucketMax / 256 buckets each).
+__device__ __forceinline__ void bucket_starts(const unsigned* tot, int nb, unsigned* start) {
+    constexpr int P = kBucketMax / 256;
+    __shared__ unsigned wtot[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    unsigned v[P], sum = 0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        v[k] = t * P + k < nb ? tot[t * P + k] : 0u;
+        sum += v[k];
     }
-    if (t == 1023) base[n] = part[1023];
+    const unsigned incl = wave_incl_scan32(sum, lane);
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    unsigned run = incl - sum, all = 0;
+    for (int q = 0; q < 4; ++q) {
+        if (q < w) run += wtot[q];
+        all += wtot[q];
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        if (t * P + k < nb) start[t * P + k] = run;
+        run += v[k];
+    }
+    if (t == 0) start[nb] = all;
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void k_group_scatter(const ScatterArgs A) {
-    __shared__ unsigned cur[kBucketMax];
-    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cur[b] = A.base[b * kBucketBlocks + blockIdx.x];
+    __shared__ unsigned cur[kBucketMax + 1];
+    bucket_starts(A.tot, A.nbuckets, cur);
+    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cur[b] += A.base[b * kBucketBlocks + blockIdx.x];
     __syncthreads();
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
-        const unsigned g = A.rg[i];
-        if (g == ~0u) continue;
-        const unsigned pos = atomicAdd(&cur[g / A.gpb], 1u);
-        A.pg[pos] = g;
-        if (A.pn) {
-            unsigned nm = 0;
-            for (int j = 0; j < A.naggs; ++j)
-                if (!valid_at(A.arg[j], i)) nm |= 1u << j;
-            A.pn[pos] = nm;
+    for (long long t0 = (long long)blockIdx.x * kRankRows; t0 < A.m; t0 += (long long)gridDim.x * kRankRows) {
+#pragma unroll
+        for (int u = 0; u < kRankU; ++u) {
+            const long long i = t0 + threadIdx.x + 256 * u;
+            if (i >= A.m) break;
+            const unsigned g = A.rg[i];
+            if (g == ~0u) continue;
+            const unsigned pos = atomicAdd(&cur[g >> A.gshift], 1u);
+            A.pg[pos] = g;
+            if (A.pn) {
+                unsigned nm = 0;
+                for (int j = 0; j < A.naggs; ++j)
+                    if (!valid_at(A.arg[j], i)) nm |= 1u << j;
+                A.pn[pos] = nm;
+            }
+            for (int c = 0; c < A.npay; ++c) A.pv[(u64)c * (u64)A.m + pos] = key_bits(A.pay[c], i);
         }
-        for (int c = 0; c < A.npay; ++c) A.pv[(u64)c * (u64)A.m + pos] = key_bits(A.pay[c], i);
     }
 }
 
@@ -531,6 +637,8 @@ __device__ __forceinline__ void lds_agg_dispatch(const AggCol& ac, u64* rec, boo
 // add; flags: or; MIN / MAX keys: min / max) -- lanes over consecutive words.
 __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
     extern __shared__ u64 lrec[];
+    __shared__ unsigned start[kBucketMax + 1];
+    bucket_starts(A.tot, A.nbuckets, start);
     const int b = blockIdx.x / A.splits, sp = blockIdx.x % A.splits;
     const u64 g0 = (u64)b * A.gpb;
     const u64 left = A.ngroups - g0;
@@ -538,8 +646,7 @@ __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
     const int W = A.words;
     for (unsigned x = threadIdx.x; x < nb * (unsigned)W; x += blockDim.x) lrec[x] = A.pattern[x % (unsigned)W];
     __syncthreads();
-    const unsigned r0 = A.base[b * kBucketBlocks], r1 = A.base[(b + 1) * kBucketBlocks];
-    const unsigned len = r1 - r0;
+    const unsigned r0 = start[b], len = start[b + 1] - start[b];
     const unsigned q0 = r0 + (unsigned)((u64)len * (u64)sp / (u64)A.splits);
     const unsigned q1 = r0 + (unsigned)((u64)len * (u64)(sp + 1) / (u64)A.splits);
     for (unsigned pos = q0 + threadIdx.x; pos < q1; pos += blockDim.x) {
@@ -578,13 +685,7 @@ __global__ __launch_bounds__(256) void k_group_rehash(const Table o, const Table
         if (!c) continue;
         u64 q = gmix(c) & n.mask;
         while (atomicCAS(&n.ctl[q], 0ull, c) != 0ull) q = (q + 1) & n.mask;
-        n.rep[q] = o.rep[s];
-        n.gid[q] = o.gid[s];
-        n.knull[q] = o.knull[s];
-        for (int p = 0; p < kMaxKeys; ++p) {
-            n.kw[q * kMaxKeys + p] = o.kw[s * kMaxKeys + p];
-            n.klen[q * kMaxKeys + p] = o.klen[s * kMaxKeys + p];
-        }
+        n.slot[q] = o.slot[s];
     }
 }
 
@@ -595,11 +696,12 @@ __global__ __launch_bounds__(256) void k_group_compact(const Table t, int nkeys,
     const u64 cap = t.mask + 1;
     for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (u64)gridDim.x * blockDim.x) {
         if (!t.ctl[s]) continue;
-        const u64 g = t.gid[s];
-        knull[g] = t.knull[s];
+        const Slot sr = t.slot[s];
+        const u64 g = sr.gid;
+        knull[g] = sr.knull;
         for (int p = 0; p < nkeys; ++p) {
-            kw[g * nkeys + p] = t.kw[s * kMaxKeys + p];
-            klen[g * nkeys + p] = t.klen[s * kMaxKeys + p];
+            kw[g * nkeys + p] = sr.kw[p];
+            klen[g * nkeys + p] = sr.klen[p];
         }
     }
 }
@@ -779,6 +881,24 @@ hipError_t launch_init(u64* acc, const u64* pattern, int words, u64 g0, u64 g1, 
     if (g1 <= g0) return hipSuccess;
     hipLaunchKernelGGL(k_group_init, dim3(grid_for((long long)((g1 - g0) * words))), dim3(256), 0, st, acc, pattern,
                        words, g0, g1);
+    return hipGetLastError();
+}
+
+hipError_t launch_buckets(const RankArgs& r, ScatterArgs s, BucketArgs b, hipStream_t st) {
+    const dim3 g(kBucketBlocks), blk(256);
+    if (r.nbuckets > kBucketMax || b.gpb != (1u << r.gshift)) return hipErrorInvalidValue;
+    switch (r.nkeys) {
+        case 1: hipLaunchKernelGGL(k_group_rank<1>, g, blk, 0, st, r); break;
+        case 2: hipLaunchKernelGGL(k_group_rank<2>, g, blk, 0, st, r); break;
+        case 3: hipLaunchKernelGGL(k_group_rank<3>, g, blk, 0, st, r); break;
+        case 4: hipLaunchKernelGGL(k_group_rank<4>, g, blk, 0, st, r); break;
+        default: return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k_group_scan, dim3(r.nbuckets), dim3(kBucketBlocks), 0, st, r.bh, (unsigned*)s.tot);
+    hipLaunchKernelGGL(k_group_scatter, g, blk, 0, st, s);
+    const size_t lds = (size_t)b.gpb * (size_t)b.words * 8;
+    if (lds > 57344 || b.nbuckets > kBucketMax || b.splits < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_group_bucket, dim3(b.nbuckets * b.splits), blk, lds, st, b);
     return hipGetLastError();
 }
 

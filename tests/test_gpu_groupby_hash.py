@@ -310,3 +310,56 @@ def test_group_by_device_finish_rounding(monkeypatch):
     f64 = {int(v[0].bits) for v in run_multi(s, b, None, [Column(0)], aggs_e)[1] if not v[0].is_null}
     assert 0x7FF0000000000000 in f64 or 0xFFF0000000000000 in f64
     assert 0x8000000000000000 in f64
+
+
+def _bucketed_batches():
+    import ctypes as C
+    L = _abi.lib()
+    L.dfmi_internal_group_bucketed_batches.restype = C.c_long
+    return L.dfmi_internal_group_bucketed_batches()
+
+
+def test_group_by_bucketed_accumulation_forced(monkeypatch):
+    """The bucketed passes (groupby.h: rank, scan, scatter, per-bucket LDS
+    sums) forced on small batches (DFMI_GROUP_BUCKETS=1): two keys with a
+    predicate over many batches, the rounding table's specials, Int32 SUM /
+    MIN / MAX with NULLs, keys forced onto shared hashes (the rank pass lists
+    the colliding rows) -- every group bit-identical to the oracle."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_GROUP_BUCKETS", "1")
+    before = _bucketed_batches()
+    rng = np.random.default_rng(70)
+    s, b = _table(rng, 40_013)
+    pred = BinaryExpr(Column(4), Operator.Lt, Literal(Float64(0.6)))
+    for p in (None, pred):
+        out = run_multi(s, b, p, [Column(0), Column(1)], AGGS(s), batch_rows=6_007)
+        assert out is not None and len(out[0]) > 3000
+    out = run_multi(s, b, None, [Column(3)], AGGS(s), batch_rows=9_001)  # Boolean key: 3 groups, heavy contention
+    assert out is not None and len(out[0]) == 3
+    s2, b2 = _rounding_table(rng, 50_000)
+    aggs2 = [agg("SUM", Column(1), s2), agg("SUM", Column(2), s2), agg("COUNT", Column(1), s2),
+             agg("MIN", Column(2), s2), agg("MAX", Column(1), s2)]
+    assert run_multi(s2, b2, None, [Column(0)], aggs2, batch_rows=20_000) is not None
+    monkeypatch.setenv("DFMI_GROUP_HASH_BITS", "3")
+    out = run_multi(s, b, None, [Column(1)], AGGS(s), batch_rows=8_000)
+    assert out is not None and len(out[0]) > 20
+    assert _bucketed_batches() > before
+
+
+def test_group_by_bucketed_accumulation_chosen():
+    """A batch of 2^21 rows over 1,000 keys (many rows per group): the
+    bucketed passes are chosen without any diagnostics switch, and the
+    groups equal the oracle's."""
+    rng = np.random.default_rng(71)
+    n = 1 << 21
+    s = Schema([Field("k", DataType.Int64, True), Field("x", DataType.Float64, True), Field("v", DataType.Int32, True)])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Int64, rng.integers(0, 1000, n) * 1_000_003, rng.random(n) >= 0.01),
+                        Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.1),
+                        Array.from_numpy(DataType.Int32, rng.integers(-2 ** 31, 2 ** 31 - 1, n).astype(np.int32),
+                                         rng.random(n) >= 0.1)])
+    aggs_e = [agg("SUM", Column(1), s), agg("COUNT", Column(1), s), agg("MIN", Column(1), s),
+              agg("MAX", Column(2), s), agg("SUM", Column(2), s)]
+    before = _bucketed_batches()
+    out = run_multi(s, b, None, [Column(0)], aggs_e)
+    assert out is not None and len(out[0]) == 1001
+    assert _bucketed_batches() == before + 1
