@@ -13,7 +13,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -105,6 +107,36 @@ struct HashDev {
 // left as it is):
 // keys (null bits, words: the value bits or the Utf8 arena offset, lengths),
 // the records, the Utf8 arena, and `order` -- the group ids in key order.
+// Pinned host memory that keeps its capacity (a finish's copies land here by
+// DMA; no zero-fill, no page faults once warm).
+template <typename T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    HostBuf() = default;
+    HostBuf(const HostBuf&) = delete;
+    HostBuf& operator=(const HostBuf&) = delete;
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    void resize(size_t want) {
+        if (want > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            const size_t c = std::max<size_t>(want + want / 4, 16);
+            HIP_TRY(hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault));
+            cap = c;
+        }
+        n = want;
+    }
+    T* data() { return p; }
+    const T* data() const { return p; }
+    size_t size() const { return n; }
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+};
+
 struct FlatGroups {
     bool rounded = false;  // acc: the device finish's compact records (groupby.h RoundArgs), the table kept
     uint64_t ng = 0;
@@ -112,9 +144,9 @@ struct FlatGroups {
     int words = 0;
     std::vector<int> off;
     std::vector<uint32_t> order;
-    std::vector<unsigned> knull, klen;
-    std::vector<uint64_t> kw, acc;
-    std::vector<uint8_t> arena;
+    HostBuf<unsigned> knull, klen;
+    HostBuf<uint64_t> kw, acc;
+    HostBuf<uint8_t> arena;
 };
 
 struct dfmi_agg_state {
@@ -140,6 +172,7 @@ struct dfmi_agg_state {
     std::shared_ptr<GroupMap> shown;  // groups dfmi_shard_agg_finish_grouped merged (else `groups`)
     HashDev* hd = nullptr;            // device hash table (created on first use)
     std::unique_ptr<FlatGroups> flat; // a finish's groups, not yet in `groups` (finish_flat)
+    std::unique_ptr<FlatGroups> spare_flat;  // a used one, its pinned buffers kept for the next drain
     // integer keys: the per-batch key window comes from MIN / MAX of the key
     // over the batch's selected rows (a pre-pass through this same extension)
     dfmi_aggregate* mm[2] = {nullptr, nullptr};
@@ -1027,7 +1060,11 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
                         uint32_t flags) {
     HashDev& H = hashdev(ctx, st);
     std::vector<dfmi::gb::Col> cols;
+    const bool prof = getenv("DFMI_DIAG") && getenv("DFMI_FINISH_PROFILE");
+    const auto t0 = std::chrono::steady_clock::now();
     const int64_t m = eval_grouped(ctx, st, pred, in, flags, cols);
+    if (prof) HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const auto t1 = std::chrono::steady_clock::now();
     if (m <= 0) return;
     if (m > 0x7fffffffll) throw Fail{DFMI_ERR_NOT_IMPLEMENTED, "GROUP BY batch of 2^31 selected rows or more"};
     const size_t nk = st->keys.size(), n = st->aggs.size();
@@ -1065,6 +1102,7 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
         grow_table(ctx, H);
     }
     const uint64_t ng = H.hh->ngroups, aend = H.hh->arena_end;
+    const auto t2 = std::chrono::steady_clock::now();
     if (ng > H.acc_cap) {
         uint64_t want = H.acc_cap;
         while (want < ng) want *= 2;
@@ -1108,6 +1146,11 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
     HIP_TRY(dfmi::gb::launch_accumulate(aa, stream));
     }
     read_hdr(ctx, H);
+    if (prof) {
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[dfmi add] %lld rows, %llu groups: eval %.1f us, claim %.1f us, accumulate %.1f us\n",
+                (long long)m, (unsigned long long)ng, us(t0, t1), us(t1, t2), us(t2, std::chrono::steady_clock::now()));
+    }
     H.ngroups = ng;
     H.rows_since_norm += (uint64_t)m;
     const uint64_t nc = H.hh->collided;
@@ -1222,28 +1265,33 @@ void sort_flat(const dfmi_agg_state* st, FlatGroups& f) {
             id.push_back((uint32_t)g);
         }
         const size_t m = kv.size();
-        if (m < 65536) {
+        if (m < 1024) {
             std::vector<std::pair<uint64_t, uint32_t>> ko(m);
             for (size_t i = 0; i < m; ++i) ko[i] = {kv[i], id[i]};
             std::sort(ko.begin(), ko.end());
             for (size_t i = 0; i < m; ++i) f.order[i] = ko[i].second;
         } else {
+            // LSD radix sort, digits of D bits (8 below 2^18 groups: the counts stay in L1; 16 above);
+            // a digit every key shares moves nothing and is skipped (one histogram pass finds them all)
+            const int D = m < (1u << 18) ? 8 : 16, P = 64 / D;
+            const size_t R = (size_t)1 << D;
             kv2.resize(m);
             id2.resize(m);
-            std::vector<size_t> cnt(65536);
-            for (int pass = 0; pass < 4; ++pass) {
-                const int sh = 16 * pass;
-                std::fill(cnt.begin(), cnt.end(), 0);
-                for (size_t i = 0; i < m; ++i) ++cnt[(kv[i] >> sh) & 0xffff];
-                if (cnt[kv[0] >> sh & 0xffff] == m) continue;  // one digit value: this pass moves nothing
-                size_t sum = 0;
-                for (auto& c : cnt) {
-                    const size_t t = c;
-                    c = sum;
+            std::vector<uint32_t> cnt(R * P, 0);
+            for (size_t i = 0; i < m; ++i)
+                for (int p = 0; p < P; ++p) ++cnt[(size_t)p * R + ((kv[i] >> (D * p)) & (R - 1))];
+            for (int p = 0; p < P; ++p) {
+                uint32_t* c = &cnt[(size_t)p * R];
+                const int sh = D * p;
+                if (c[(kv[0] >> sh) & (R - 1)] == m) continue;  // one digit value: this pass moves nothing
+                uint32_t sum = 0;
+                for (size_t d = 0; d < R; ++d) {
+                    const uint32_t t = c[d];
+                    c[d] = sum;
                     sum += t;
                 }
                 for (size_t i = 0; i < m; ++i) {
-                    const size_t d = cnt[(kv[i] >> sh) & 0xffff]++;
+                    const uint32_t d = c[(kv[i] >> sh) & (R - 1)]++;
                     kv2[d] = kv[i];
                     id2[d] = id[i];
                 }
@@ -1329,6 +1377,13 @@ void unflatten(dfmi_agg_state* st) {
     if (!st->flat) return;
     std::unique_ptr<FlatGroups> f = std::move(st->flat);
     if (!f->rounded) materialize_flat(st, *f);
+    st->spare_flat = std::move(f);
+}
+
+std::unique_ptr<FlatGroups> take_flat(dfmi_agg_state* st) {
+    std::unique_ptr<FlatGroups> f = st->spare_flat ? std::move(st->spare_flat) : std::make_unique<FlatGroups>();
+    f->order.clear();
+    return f;
 }
 
 // The groups the device hash table holds merged into st->groups, and the
@@ -1336,9 +1391,10 @@ void unflatten(dfmi_agg_state* st) {
 void drain_hashed(dfmi_context* ctx, dfmi_agg_state* st) {
     unflatten(st);
     if (!st->hd || !st->hd->ngroups) return;
-    FlatGroups f;
-    read_table(ctx, st, f);
-    materialize_flat(st, f);
+    std::unique_ptr<FlatGroups> f = take_flat(st);
+    read_table(ctx, st, *f);
+    materialize_flat(st, *f);
+    st->spare_flat = std::move(f);
 }
 
 // The finish of a state whose groups all sit in the device hash table (no
@@ -1352,9 +1408,15 @@ bool finish_flat(dfmi_context* ctx, dfmi_agg_state* st) {
     if (st->flat && !st->flat->rounded && st->hd && st->hd->ngroups) return false;  // (a batch unflattens first)
     if (!st->flat) {
         if (!st->hd || !st->hd->ngroups) return false;
-        auto f = std::make_unique<FlatGroups>();
+        std::unique_ptr<FlatGroups> f = take_flat(st);
+        const auto t0 = std::chrono::steady_clock::now();
         read_table(ctx, st, *f, !(getenv("DFMI_DIAG") && getenv("DFMI_GROUP_HOST_FINISH")));
+        const auto t1 = std::chrono::steady_clock::now();
         sort_flat(st, *f);
+        if (getenv("DFMI_DIAG") && getenv("DFMI_FINISH_PROFILE"))
+            fprintf(stderr, "[dfmi finish] %llu groups: read_table %.1f us, sort %.1f us\n", (unsigned long long)f->ng,
+                    std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count());
         st->flat = std::move(f);
     }
     st->shown.reset();
@@ -1397,7 +1459,7 @@ void emit_flat(const dfmi_agg_state* st, const FlatGroups& f, int64_t cap, dfmi_
             }
         }
     };
-    parallel_ranges(f.ng, 4096, emit_range);
+    parallel_ranges(f.ng, 32768, emit_range);  // (a thread's start costs more than ~10^4 groups' emission)
 }
 
 void emit_key_bytes_flat(const FlatGroups& f, int part, int32_t* offsets, int64_t num_offsets, uint8_t* data,
@@ -1723,7 +1785,11 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
         }
         HIP_TRY(hipSetDevice(ctx->device));
         if (finish_flat(ctx, st)) {
+            const auto t0 = std::chrono::steady_clock::now();
             emit_flat(st, *st->flat, cap, keys, values, num_groups);
+            if (getenv("DFMI_DIAG") && getenv("DFMI_FINISH_PROFILE"))
+                fprintf(stderr, "[dfmi finish] emit %.1f us\n",
+                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
             return DFMI_OK;
         }
         collect_groups(ctx, st);
@@ -1783,7 +1849,7 @@ extern "C" int32_t dfmi_agg_state_reset(dfmi_context* ctx, dfmi_agg_state* st, d
         st->failure = dfmi_error{};
         st->index.clear();
         st->groups.clear();
-        st->flat.reset();
+        if (st->flat) st->spare_flat = std::move(st->flat);
         st->shown.reset();
         st->win_width = -1;
         st->dirty = false;
