@@ -420,10 +420,11 @@ __global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
 
 // --------------------------------------------------- bucketed accumulation
 // (groupby.h "Bucketed accumulation"). The rank and scatter passes run
-// kBucketBlocks blocks of 256 threads over the same tiles of kRankRows rows
+// kBucketBlocks blocks of 256 threads over the same tiles of kScatterTile rows
 // per block, so a block's rows of a bucket fill exactly its positions.
-constexpr int kRankU = 4;                   // rows per thread per tile (independent load chains)
+constexpr int kRankU = 4;                   // rows per thread per sub-tile (independent load chains)
 constexpr int kRankRows = 256 * kRankU;
+constexpr int kScatterTile = 4096;          // rows per block per tile (rank and scatter alike)
 
 template <int NK>
 __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
@@ -431,7 +432,8 @@ __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
     for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
     const Table& t = A.t;
-    for (long long t0 = (long long)blockIdx.x * kRankRows; t0 < A.m; t0 += (long long)gridDim.x * kRankRows) {
+    for (long long T0 = (long long)blockIdx.x * kScatterTile; T0 < A.m; T0 += (long long)gridDim.x * kScatterTile)
+    for (long long t0 = T0; t0 < T0 + kScatterTile && t0 < A.m; t0 += kRankRows) {
         // the row_group chain of kRankU rows at once: slots, keys, the slots' words, then the decisions
         int sl[kRankU];
         RowKey r[kRankU];
@@ -493,6 +495,66 @@ __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
     for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) A.bh[b * kBucketBlocks + blockIdx.x] = cnt[b];
 }
 
+// k_group_rank for keys without Utf8 parts: no representative row to consult
+// (the claim persisted every fixed-width key word), so each row reads only its
+// slot's group id, null mask and key words, kRankFixedU rows at once.
+constexpr int kRankFixedU = 8;
+
+template <int NK>
+__global__ __launch_bounds__(256) void k_group_rank_fixed(const RankArgs A) {
+    __shared__ unsigned cnt[kBucketMax];
+    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    const Slot* slot = A.t.slot;
+    constexpr int rows = 256 * kRankFixedU;
+    static_assert(kScatterTile % rows == 0, "sub-tiles of the scatter's tile");
+    for (long long T0 = (long long)blockIdx.x * kScatterTile; T0 < A.m; T0 += (long long)gridDim.x * kScatterTile)
+    for (long long t0 = T0; t0 < T0 + kScatterTile && t0 < A.m; t0 += rows) {
+        int sl[kRankFixedU];
+        unsigned gid[kRankFixedU], kn[kRankFixedU];
+        u64 kw[kRankFixedU][NK];
+#pragma unroll
+        for (int u = 0; u < kRankFixedU; ++u) {
+            const long long i = t0 + threadIdx.x + 256 * u;
+            sl[u] = i < A.m ? A.sidx[i] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kRankFixedU; ++u) {
+            const Slot& q = slot[sl[u] < 0 ? 0 : sl[u]];
+            gid[u] = q.gid;
+            kn[u] = q.knull;
+#pragma unroll
+            for (int p = 0; p < NK; ++p) kw[u][p] = q.kw[p];
+        }
+#pragma unroll
+        for (int u = 0; u < kRankFixedU; ++u) {
+            const long long i = t0 + threadIdx.x + 256 * u;
+            if (i >= A.m) break;
+            bool ok = false;
+            if (sl[u] >= 0) {
+                unsigned nullm = 0;
+                bool same = true;
+#pragma unroll
+                for (int p = 0; p < NK; ++p) {
+                    if (!valid_at(A.k[p], i)) nullm |= 1u << p;
+                    else same = same && kw[u][p] == key_bits(A.k[p], i);
+                }
+                same = same && nullm == kn[u];
+                if (same) {
+                    ok = true;
+                } else {  // two keys, one hash: the host merges this row
+                    const u64 at = atomicAdd(&A.hdr->collided, 1ull);
+                    A.coll_rows[at] = (int)i;
+                }
+            }
+            A.rg[i] = ok ? gid[u] : ~0u;
+            if (ok) atomicAdd(&cnt[gid[u] >> A.gshift], 1u);
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) A.bh[b * kBucketBlocks + blockIdx.x] = cnt[b];
+}
+
 // One block of kBucketBlocks threads per bucket: its per-block counts turned
 // into exclusive prefixes in place, the bucket's total into tot[b].
 __global__ __launch_bounds__(kBucketBlocks) void k_group_scan(unsigned* bh, unsigned* tot) {
@@ -541,20 +603,73 @@ __device__ __forceinline__ void bucket_starts(const unsigned* tot, int nb, unsig
     __syncthreads();
 }
 
+// a[0 .. nb) -> its exclusive prefix in place, a[nb] the total (LDS; 256
+// threads, kBucketMax / 256 entries each).
+__device__ __forceinline__ void lds_excl_scan(unsigned* a, int nb) {
+    constexpr int P = kBucketMax / 256;
+    __shared__ unsigned wtot[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    unsigned v[P], sum = 0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        v[k] = t * P + k < nb ? a[t * P + k] : 0u;
+        sum += v[k];
+    }
+    const unsigned incl = wave_incl_scan32(sum, lane);
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    unsigned run = incl - sum, all = 0;
+    for (int q = 0; q < 4; ++q) {
+        if (q < w) run += wtot[q];
+        all += wtot[q];
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        if (t * P + k < nb) a[t * P + k] = run;
+        run += v[k];
+    }
+    if (t == 0) a[nb] = all;
+    __syncthreads();
+}
+
+// Per tile, the placed rows are first ordered by bucket in LDS, then written
+// out: consecutive lanes write consecutive positions of a bucket's run (whole
+// lines), where a per-row store would leave each of the ~buckets x resident
+// blocks open lines half written in L2.
 __global__ __launch_bounds__(256) void k_group_scatter(const ScatterArgs A) {
-    __shared__ unsigned cur[kBucketMax + 1];
+    constexpr int PER = kScatterTile / 256;
+    __shared__ unsigned cur[kBucketMax + 1];    // the block's next position per bucket
+    __shared__ unsigned tcnt[kBucketMax + 1];   // the tile's rows per bucket, then their exclusive prefix
+    __shared__ unsigned sg[kScatterTile];       // the tile's placed rows in bucket order: group id ...
+    __shared__ unsigned short si[kScatterTile]; // ... and row within the tile
     bucket_starts(A.tot, A.nbuckets, cur);
     for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cur[b] += A.base[b * kBucketBlocks + blockIdx.x];
+    for (int b = threadIdx.x; b <= A.nbuckets; b += blockDim.x) tcnt[b] = 0;
     __syncthreads();
-    for (long long t0 = (long long)blockIdx.x * kRankRows; t0 < A.m; t0 += (long long)gridDim.x * kRankRows) {
+    for (long long T0 = (long long)blockIdx.x * kScatterTile; T0 < A.m; T0 += (long long)gridDim.x * kScatterTile) {
+        unsigned g[PER], r[PER];
 #pragma unroll
-        for (int u = 0; u < kRankU; ++u) {
-            const long long i = t0 + threadIdx.x + 256 * u;
-            if (i >= A.m) break;
-            const unsigned g = A.rg[i];
-            if (g == ~0u) continue;
-            const unsigned pos = atomicAdd(&cur[g >> A.gshift], 1u);
-            A.pg[pos] = g;
+        for (int u = 0; u < PER; ++u) {
+            const long long i = T0 + threadIdx.x + 256 * u;
+            g[u] = i < A.m ? A.rg[i] : ~0u;
+            r[u] = g[u] != ~0u ? atomicAdd(&tcnt[g[u] >> A.gshift], 1u) : 0u;
+        }
+        __syncthreads();
+        lds_excl_scan(tcnt, A.nbuckets);
+#pragma unroll
+        for (int u = 0; u < PER; ++u)
+            if (g[u] != ~0u) {
+                const unsigned sp = tcnt[g[u] >> A.gshift] + r[u];
+                sg[sp] = g[u];
+                si[sp] = (unsigned short)(threadIdx.x + 256 * u);
+            }
+        __syncthreads();
+        const unsigned placed = tcnt[A.nbuckets];
+        for (unsigned e = threadIdx.x; e < placed; e += blockDim.x) {
+            const unsigned gg = sg[e], b = gg >> A.gshift;
+            const unsigned pos = cur[b] + (e - tcnt[b]);
+            const long long i = T0 + si[e];
+            A.pg[pos] = gg;
             if (A.pn) {
                 unsigned nm = 0;
                 for (int j = 0; j < A.naggs; ++j)
@@ -563,6 +678,11 @@ __global__ __launch_bounds__(256) void k_group_scatter(const ScatterArgs A) {
             }
             for (int c = 0; c < A.npay; ++c) A.pv[(u64)c * (u64)A.m + pos] = key_bits(A.pay[c], i);
         }
+        __syncthreads();
+        for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cur[b] += tcnt[b + 1] - tcnt[b];
+        __syncthreads();
+        for (int b = threadIdx.x; b <= A.nbuckets; b += blockDim.x) tcnt[b] = 0;
+        __syncthreads();
     }
 }
 
@@ -887,11 +1007,17 @@ hipError_t launch_init(u64* acc, const u64* pattern, int words, u64 g0, u64 g1, 
 hipError_t launch_buckets(const RankArgs& r, ScatterArgs s, BucketArgs b, hipStream_t st) {
     const dim3 g(kBucketBlocks), blk(256);
     if (r.nbuckets > kBucketMax || b.gpb != (1u << r.gshift)) return hipErrorInvalidValue;
-    switch (r.nkeys) {
-        case 1: hipLaunchKernelGGL(k_group_rank<1>, g, blk, 0, st, r); break;
-        case 2: hipLaunchKernelGGL(k_group_rank<2>, g, blk, 0, st, r); break;
-        case 3: hipLaunchKernelGGL(k_group_rank<3>, g, blk, 0, st, r); break;
-        case 4: hipLaunchKernelGGL(k_group_rank<4>, g, blk, 0, st, r); break;
+    bool fixed = true;
+    for (int p = 0; p < r.nkeys && p < kMaxKeys; ++p) fixed = fixed && r.k[p].type != kTypeUtf8;
+    switch (r.nkeys * 2 + (fixed ? 1 : 0)) {
+        case 2: hipLaunchKernelGGL(k_group_rank<1>, g, blk, 0, st, r); break;
+        case 3: hipLaunchKernelGGL(k_group_rank_fixed<1>, g, blk, 0, st, r); break;
+        case 4: hipLaunchKernelGGL(k_group_rank<2>, g, blk, 0, st, r); break;
+        case 5: hipLaunchKernelGGL(k_group_rank_fixed<2>, g, blk, 0, st, r); break;
+        case 6: hipLaunchKernelGGL(k_group_rank<3>, g, blk, 0, st, r); break;
+        case 7: hipLaunchKernelGGL(k_group_rank_fixed<3>, g, blk, 0, st, r); break;
+        case 8: hipLaunchKernelGGL(k_group_rank<4>, g, blk, 0, st, r); break;
+        case 9: hipLaunchKernelGGL(k_group_rank_fixed<4>, g, blk, 0, st, r); break;
         default: return hipErrorInvalidValue;
     }
     hipLaunchKernelGGL(k_group_scan, dim3(r.nbuckets), dim3(kBucketBlocks), 0, st, r.bh, (unsigned*)s.tot);
