@@ -997,6 +997,7 @@ void accumulate_bucketed(dfmi_context* ctx, dfmi_agg_state* st, HashDev& H, cons
     ra.m = m;
     ra.t = H.t;
     ra.arena = H.arena;
+    ra.arena_cap = H.arena_cap;
     ra.sidx = H.sidx;
     ra.hdr = H.hdr;
     ra.coll_rows = H.coll;
@@ -1132,6 +1133,7 @@ void group_batch_hashed(dfmi_context* ctx, dfmi_agg_state* st, const dfmi_progra
     aa.m = m;
     aa.t = H.t;
     aa.arena = H.arena;
+    aa.arena_cap = H.arena_cap;
     aa.sidx = H.sidx;
     for (size_t j = 0; j < n; ++j) {
         aa.a[j].c = cols[nk + j];

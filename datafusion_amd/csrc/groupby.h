@@ -47,10 +47,13 @@ struct Col {
 
 // A slot's record: one 64-byte line piece, so a row's check of its slot
 // (k_group_rank / row_group) is one random access, not one per field.
+constexpr unsigned kNullBits = 0xffu;   // Slot::knull: the null bits of the key parts
+constexpr unsigned kInline = 1u << 8;   // Slot::knull: a one-part Utf8 key of <= 24 bytes, its bytes in kw[1..3]
+
 struct alignas(64) Slot {
     long long rep;                    // (epoch << 32) | representative row of the claiming batch
     unsigned gid;                     // dense group id
-    unsigned knull;                   // bit p: key part p is null
+    unsigned knull;                   // bit p: key part p is null; kInline
     unsigned long long kw[kMaxKeys];  // persisted key words (Utf8: arena offset)
     unsigned klen[kMaxKeys];          // Utf8 key bytes
 };
@@ -103,6 +106,7 @@ struct AccArgs {
     long long m;
     Table t;
     unsigned char* arena;          // Utf8 key bytes of every group
+    unsigned long long arena_cap;  // its allocated bytes
     const int32_t* sidx;
     AggCol a[kMaxAggs];
     int32_t naggs;
@@ -142,6 +146,7 @@ struct RankArgs {
     long long m;
     Table t;
     unsigned char* arena;
+    unsigned long long arena_cap;
     const int32_t* sidx;
     Hdr* hdr;
     int32_t* coll_rows;

@@ -50,21 +50,48 @@ __device__ __forceinline__ u64 key_bits(const Col& c, long long i) {
 
 constexpr int kTypeUtf8 = 12;
 
-__device__ __forceinline__ u64 hash_bytes(const u8* p, unsigned len, u64 h) {
+// Bytes [8j, 8j + 8) of the len bytes at p as a little-endian word, zero
+// past len: one unaligned load where it cannot read past `endp` (the
+// column's last byte + 1), else byte loads -- the same word either way.
+__device__ __forceinline__ u64 load_word(const u8* p, unsigned len, unsigned j, const u8* endp) {
+    const unsigned b0 = 8 * j;
+    if (len <= b0) return 0;
+    const unsigned vb = len - b0 < 8 ? len - b0 : 8;
+    if (p + b0 + 8 <= endp) {
+        const u64 x = *(const u64_ua*)(p + b0);
+        return vb == 8 ? x : x & ((1ull << (8 * vb)) - 1);
+    }
+    u64 t = 0;
+    for (unsigned q = 0; q < vb; ++q) t |= (u64)p[b0 + q] << (8 * q);
+    return t;
+}
+
+__device__ __forceinline__ u64 hash_bytes(const u8* p, unsigned len, u64 h, const u8* endp) {
     unsigned j = 0;
     for (; j + 8 <= len; j += 8) h = gmix(h ^ *(const u64_ua*)(p + j)) + 0x9E3779B97F4A7C15ull;
-    u64 t = 0;
-    for (unsigned s = 0; j < len; ++j, s += 8) t |= (u64)p[j] << s;
+    const u64 t = load_word(p, len, j >> 3, endp);
     return gmix(h ^ t ^ ((u64)len << 56));
 }
 
-__device__ __forceinline__ bool bytes_eq(const u8* a, const u8* b, unsigned len) {
+__device__ __forceinline__ bool bytes_eq(const u8* a, const u8* b, unsigned len, const u8* enda, const u8* endb) {
     unsigned j = 0;
     for (; j + 8 <= len; j += 8)
         if (*(const u64_ua*)(a + j) != *(const u64_ua*)(b + j)) return false;
-    for (; j < len; ++j)
-        if (a[j] != b[j]) return false;
-    return true;
+    return j == len || load_word(a, len, j >> 3, enda) == load_word(b, len, j >> 3, endb);
+}
+
+// A one-part Utf8 key of at most 24 bytes is kept in the slot itself too
+// (Slot::kw[1..3], groupby.h kInline), so that checking a row against its
+// slot reads no arena and no representative row.
+
+__device__ __forceinline__ void inline_pack(const u8* p, unsigned len, u64 (&w)[3]) {
+    w[0] = w[1] = w[2] = 0;
+    for (unsigned j = 0; j < len; ++j) w[j >> 3] |= (u64)p[j] << (8 * (j & 7));
+}
+
+__device__ __forceinline__ bool inline_eq(const u8* p, unsigned len, const u64* w, const u8* endp) {
+    return load_word(p, len, 0, endp) == w[0] && (len <= 8 || load_word(p, len, 1, endp) == w[1]) &&
+           (len <= 16 || load_word(p, len, 2, endp) == w[2]);
 }
 
 // The row's key: null mask, fixed-width bits, Utf8 (start, length); its hash.
@@ -73,10 +100,11 @@ struct RowKey {
     u64 w[kMaxKeys];
     const u8* s[kMaxKeys];
     unsigned len[kMaxKeys];
+    const u8* end[kMaxKeys];  // Utf8: the column's last byte + 1
 };
 
 template <int NK, bool HASH = true>
-__device__ __forceinline__ u64 row_key(const Col* k, long long i, RowKey& r) {
+__device__ __forceinline__ u64 row_key(const Col* k, long long i, long long m, RowKey& r) {
     u64 h = 0x243F6A8885A308D3ull;
     r.nullm = 0;
 #pragma unroll
@@ -92,7 +120,8 @@ __device__ __forceinline__ u64 row_key(const Col* k, long long i, RowKey& r) {
             const int a = c.offsets[i], b = c.offsets[i + 1];
             r.s[p] = (const u8*)c.values + a;
             r.len[p] = (unsigned)(b - a);
-            if (HASH) h = hash_bytes(r.s[p], r.len[p], h + (u64)p);
+            r.end[p] = (const u8*)c.values + c.offsets[m];
+            if (HASH) h = hash_bytes(r.s[p], r.len[p], h + (u64)p, r.end[p]);
         } else {
             r.w[p] = key_bits(c, i);
             h = gmix(h ^ (r.w[p] * 0xD6E8FEB86659FD93ull + (u64)p));
@@ -141,6 +170,16 @@ __device__ __forceinline__ int claim_row(const ClaimArgs& A, const RowKey& r, u6
                     sr.kw[p] = w;
                     sr.klen[p] = r.len[p];
                 }
+                // a one-part Utf8 key of at most 24 bytes: its bytes in the slot's spare
+                // words too (the same for two- and three-part keys measured slower)
+                if (NK == 1 && r.s[0] && r.len[0] <= 24) {
+                    u64 w[3];
+                    inline_pack(r.s[0], r.len[0], w);
+                    sr.kw[1] = w[0];
+                    sr.kw[2] = w[1];
+                    sr.kw[3] = w[2];
+                    sr.knull = r.nullm | kInline;
+                }
                 return (int)s;
             }
         }
@@ -159,7 +198,7 @@ __global__ __launch_bounds__(256) void k_group_claim(const ClaimArgs A) {
     bool overflow = false;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < A.m; i += stride) {
         RowKey r;
-        const u64 c = (row_key<NK>(A.k, i, r) & A.hash_mask) | 1ull;
+        const u64 c = (row_key<NK>(A.k, i, A.m, r) & A.hash_mask) | 1ull;
         const u64 s = gmix(c) & t.mask;
         const u64 cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int res = cur == c ? (int)s : claim_row<NK>(A, r, c, s, cur, i);
@@ -343,17 +382,18 @@ __device__ __forceinline__ void agg_dispatch(const AggCol& ac, u64* rec, long lo
 // earlier batch; a row whose key differs (two keys, one hash) is listed for
 // the host merge. False: not added on the device.
 template <int NK>
-__device__ __forceinline__ bool row_group(const Col* k, uint32_t epoch, const Table& t, unsigned char* arena, Hdr* hdr,
-                                          int32_t* coll_rows, const int32_t* sidx, long long i, unsigned& g) {
+__device__ __forceinline__ bool row_group(const Col* k, long long m, uint32_t epoch, const Table& t, unsigned char* arena,
+                                          unsigned long long arena_cap, Hdr* hdr, int32_t* coll_rows, const int32_t* sidx,
+                                          long long i, unsigned& g) {
     const int s = sidx[i];
     if (s < 0) return false;
     RowKey r;
-    (void)row_key<NK>(k, i, r);
+    (void)row_key<NK, false>(k, i, m, r);
     const Slot sr = t.slot[s];
     const long long rp = sr.rep;
     const bool cur = (unsigned)((unsigned long long)rp >> 32) == epoch;
     const long long rr = (long long)(unsigned)rp;
-    bool same = sr.knull == r.nullm;
+    bool same = (sr.knull & kNullBits) == r.nullm;
     if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
 #pragma unroll
         for (int p = 0; p < NK; ++p)
@@ -368,8 +408,12 @@ __device__ __forceinline__ bool row_group(const Col* k, uint32_t epoch, const Ta
             const u64 kwv = sr.kw[p];
             if (r.s[p]) {
                 const unsigned kl = sr.klen[p];
+                if (NK == 1 && (sr.knull & kInline)) {
+                    same = kl == r.len[p] && inline_eq(r.s[p], kl, &sr.kw[1], r.end[p]);
+                    continue;
+                }
                 const u8* other = cur ? (const u8*)k[p].values + k[p].offsets[rr] : arena + kwv;
-                same = kl == r.len[p] && bytes_eq(r.s[p], other, kl);
+                same = kl == r.len[p] && bytes_eq(r.s[p], other, kl, r.end[p], cur ? r.end[p] : arena + arena_cap);
             } else {
                 same = kwv == r.w[p];
             }
@@ -396,7 +440,7 @@ __global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
     for (long long base = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < A.m; base += stride) {
         const long long i = base + lane;
         unsigned g = 0;
-        const bool ok = i < A.m && row_group<NK>(A.k, A.epoch, A.t, A.arena, A.hdr, A.coll_rows, A.sidx, i, g);
+        const bool ok = i < A.m && row_group<NK>(A.k, A.m, A.epoch, A.t, A.arena, A.arena_cap, A.hdr, A.coll_rows, A.sidx, i, g);
         u64 active = __ballot(ok);
         int singles = 0;
         while (active) {
@@ -447,7 +491,7 @@ __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
         for (int u = 0; u < kRankU; ++u) {
             const long long i = t0 + threadIdx.x + 256 * u;
             const int s = sl[u] < 0 ? 0 : sl[u];
-            if (sl[u] >= 0) (void)row_key<NK, false>(A.k, i, r[u]);
+            if (sl[u] >= 0) (void)row_key<NK, false>(A.k, i, A.m, r[u]);
             sr[u] = t.slot[s];
         }
 #pragma unroll
@@ -459,7 +503,7 @@ __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
             if (s >= 0) {
                 const bool cur = (unsigned)((unsigned long long)sr[u].rep >> 32) == A.epoch;
                 const long long rr = (long long)(unsigned)sr[u].rep;
-                bool same = sr[u].knull == r[u].nullm;
+                bool same = (sr[u].knull & kNullBits) == r[u].nullm;
                 if (cur && rr == i) {  // the representative row: persist its Utf8 key bytes
 #pragma unroll
                     for (int p = 0; p < NK; ++p)
@@ -473,8 +517,13 @@ __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
                         if (!same || ((r[u].nullm >> p) & 1)) continue;
                         if (r[u].s[p]) {
                             const unsigned kl = sr[u].klen[p];
+                            if (NK == 1 && (sr[u].knull & kInline)) {
+                                same = kl == r[u].len[p] && inline_eq(r[u].s[p], kl, &sr[u].kw[1], r[u].end[p]);
+                                continue;
+                            }
                             const u8* other = cur ? (const u8*)A.k[p].values + A.k[p].offsets[rr] : A.arena + sr[u].kw[p];
-                            same = kl == r[u].len[p] && bytes_eq(r[u].s[p], other, kl);
+                            same = kl == r[u].len[p] &&
+                                   bytes_eq(r[u].s[p], other, kl, r[u].end[p], cur ? r[u].end[p] : A.arena + A.arena_cap);
                         } else {
                             same = sr[u].kw[p] == r[u].w[p];
                         }
@@ -522,7 +571,7 @@ __global__ __launch_bounds__(256) void k_group_rank_fixed(const RankArgs A) {
         for (int u = 0; u < kRankFixedU; ++u) {
             const Slot& q = slot[sl[u] < 0 ? 0 : sl[u]];
             gid[u] = q.gid;
-            kn[u] = q.knull;
+            kn[u] = q.knull & kNullBits;
 #pragma unroll
             for (int p = 0; p < NK; ++p) kw[u][p] = q.kw[p];
         }
@@ -818,7 +867,7 @@ __global__ __launch_bounds__(256) void k_group_compact(const Table t, int nkeys,
         if (!t.ctl[s]) continue;
         const Slot sr = t.slot[s];
         const u64 g = sr.gid;
-        knull[g] = sr.knull;
+        knull[g] = sr.knull & kNullBits;
         for (int p = 0; p < nkeys; ++p) {
             kw[g * nkeys + p] = sr.kw[p];
             klen[g * nkeys + p] = sr.klen[p];

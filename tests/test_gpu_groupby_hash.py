@@ -223,11 +223,15 @@ def test_grouped_partials_utf8_and_multi_key_merge():
                 assert [None if mk[g][p].is_null else got[g] for g in range(len(mk))] == strs
 
 
-def test_finish_then_more_rows_partial_and_reset():
-    """The finish's flat groups (aggregate.cpp finish_flat: emitted from the
-    drained table without the host map): a second finish gives the same
-    groups; rows added after a finish merge with the finished groups; the
-    grouped partial after a finish holds every group; reset empties."""
+@pytest.mark.parametrize("buckets", ["0", "1"])
+def test_finish_then_more_rows_partial_and_reset(monkeypatch, buckets):
+    """The finish's flat groups (aggregate.cpp finish_flat: finished on the
+    device, the table kept): a second finish gives the same groups; rows
+    added after a finish merge with the finished groups; the grouped partial
+    after a finish holds every group; reset empties -- with the atomic
+    accumulate pass and with the bucketed passes (DFMI_GROUP_BUCKETS)."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_GROUP_BUCKETS", buckets)
     rng = np.random.default_rng(68)
     s, b = _table(rng, 24_000)
     aggs_e = AGGS(s)
@@ -363,3 +367,31 @@ def test_group_by_bucketed_accumulation_chosen():
     out = run_multi(s, b, None, [Column(0)], aggs_e)
     assert out is not None and len(out[0]) == 1001
     assert _bucketed_batches() == before + 1
+
+
+@pytest.mark.parametrize("buckets", ["0", "1"])
+@pytest.mark.parametrize("hash_bits", [None, "3"])
+def test_group_by_utf8_keys_inline_and_long(monkeypatch, buckets, hash_bits):
+    """Utf8 keys of 0-60 bytes: those of at most 24 bytes are checked
+    against the copy kept in their slot (groupby.h kInline), longer ones
+    against the representative row / the arena -- over several batches, with
+    every key forced onto 8 hash values (DFMI_GROUP_HASH_BITS=3: rows of
+    other keys meet inline and long slot keys), atomic and bucketed passes."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_GROUP_BUCKETS", buckets)
+    if hash_bits:
+        monkeypatch.setenv("DFMI_GROUP_HASH_BITS", hash_bits)
+    rng = np.random.default_rng(72)
+    n = 30_000
+    words = [bytes(rng.integers(97, 123, int(ln)).astype(np.uint8)) for ln in rng.integers(0, 61, 400)]
+    words += [b"x" * 24, b"x" * 25, b"x" * 23, b"y" * 8, b"y" * 16, b"\xff" * 24]
+    s = Schema([Field("k", DataType.Utf8, True), Field("x", DataType.Float64, True), Field("j", DataType.Int64, True)])
+    b = RecordBatch(s, [Array.from_strings([None if rng.random() < 0.02 else words[i]
+                                            for i in rng.integers(0, len(words), n)]),
+                        Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.05),
+                        Array.from_numpy(DataType.Int64, rng.integers(0, 3, n), rng.random(n) >= 0.02)])
+    aggs_e = [agg("SUM", Column(1), s), agg("COUNT", Column(1), s), agg("MAX", Column(1), s)]
+    # one part (24 inline bytes), two and three parts (the arena / representative row)
+    for keys in ([Column(0)], [Column(2), Column(0)], [Column(0), Column(2), Column(2)]):
+        out = run_multi(s, b, None, keys, aggs_e, batch_rows=11_000)
+        assert out is not None and len(out[0]) > 380
