@@ -133,20 +133,23 @@ __device__ __forceinline__ u64 row_key(const Col* k, long long i, long long m, R
 // ------------------------------------------------------------ claim pass
 // One row's slot: linear probing from slot s, whose probe word the caller has
 // already loaded (`cur`); an empty slot is claimed with a CAS. -1: no slot
-// (the table is at its load limit, or the probe ran past kProbeMax slots: the
-// host grows the table and runs the pass again -- every row again, so a row
-// given up here is placed then).
+// (the table is at its load limit, or past it after 8 probes, or the probe
+// ran past kProbeMax slots: the host grows the table and runs the pass again
+// -- every row again, so a row given up here is placed then).
 constexpr u64 kProbeMax = 4096;
 
 template <int NK>
 __device__ __forceinline__ int claim_row(const ClaimArgs& A, const RowKey& r, u64 c, u64 s, u64 cur, long long i) {
     const Table& t = A.t;
-    if (__hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit) return -1;
     for (u64 probe = 0; probe <= t.mask && probe < kProbeMax; ++probe) {
         if (probe) {
             s = (s + 1) & t.mask;
             cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        // a long probe into a table past its load limit (claims racing past the
+        // limit can fill it): give up, the pass reruns on the grown table
+        if (probe == 8 && __hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit)
+            return -1;
         if (cur == 0) {
             if (__hip_atomic_load(&A.hdr->ngroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.limit) return -1;
             cur = atomicCAS(&t.ctl[s], 0ull, c);
