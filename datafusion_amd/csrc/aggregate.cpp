@@ -977,6 +977,9 @@ bool use_buckets(const dfmi_agg_state* st, const HashDev& H, int64_t m, uint64_t
     if (!b.gpb || b.nbuckets > dfmi::gb::kBucketMax || st->aggs.size() > 32) return false;
     if (getenv("DFMI_DIAG"))
         if (const char* e = getenv("DFMI_GROUP_BUCKETS")) return atoi(e) != 0;
+    // the partitioned copy of the batch (group id, NULL mask, one 8-byte word
+    // per argument) stays within 16 GiB of the 288 GB
+    if ((uint64_t)m * (12 + 8 * st->aggs.size()) > (16ull << 30)) return false;
     // ~4 record atomics per row against each block adding a touched group's
     // ~10 moved words once: many rows per group and split
     return (uint64_t)m >= 4ull * ng * (uint64_t)b.splits && m >= (1 << 20);
