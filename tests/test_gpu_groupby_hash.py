@@ -395,3 +395,37 @@ def test_group_by_utf8_keys_inline_and_long(monkeypatch, buckets, hash_bits):
     for keys in ([Column(0)], [Column(2), Column(0)], [Column(0), Column(2), Column(2)]):
         out = run_multi(s, b, None, keys, aggs_e, batch_rows=11_000)
         assert out is not None and len(out[0]) > 380
+
+
+@pytest.mark.parametrize("buckets", ["0", "1"])
+def test_group_by_every_argument_type(monkeypatch, buckets):
+    """SUM / MIN / MAX / COUNT of every numeric argument type (Int8 ... UInt64,
+    Float32) with NULLs, grouped by a Float64 key (the hash table), through the
+    atomic accumulate pass and the bucketed passes (LDS records): signed
+    values sign-extended, unsigned zero-extended, integer SUM wrapping."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_GROUP_BUCKETS", buckets)
+    rng = np.random.default_rng(73)
+    n = 25_000
+    types = [DataType.Int8, DataType.Int16, DataType.UInt8, DataType.UInt16, DataType.UInt32, DataType.UInt64,
+             DataType.Float32]
+    np_t = [np.int8, np.int16, np.uint8, np.uint16, np.uint32, np.uint64, np.float32]
+    fields = [Field("g", DataType.Float64, True)] + [Field("c%d" % j, t, True) for j, t in enumerate(types)]
+    cols = [Array.from_numpy(DataType.Float64, rng.integers(0, 300, n) / 3.0, rng.random(n) >= 0.02)]
+    for t, nt in zip(types, np_t):
+        if nt == np.float32:
+            vals = (rng.standard_normal(n) * 1e3).astype(np.float32)
+        else:
+            info = np.iinfo(nt)
+            vals = rng.integers(int(info.min), int(info.max), n, dtype=np.int64 if info.min < 0 else np.uint64,
+                                endpoint=True).astype(nt)
+        cols.append(Array.from_numpy(t, vals, rng.random(n) >= 0.1))
+    s = Schema(fields)
+    b = RecordBatch(s, cols)
+    aggs_e = []
+    for j in range(len(types)):
+        for fn in ("SUM", "MIN", "MAX", "COUNT"):
+            aggs_e.append(agg(fn, Column(1 + j), s))
+    for start in range(0, len(aggs_e), 14):  # at most 15 aggregates per grouped state
+        out = run_multi(s, b, None, [Column(0)], aggs_e[start:start + 14], batch_rows=9_000)
+        assert out is not None and len(out[0]) > 290
