@@ -950,8 +950,9 @@ void regrow(dfmi_context* ctx, T*& p, size_t keep, size_t want) {
 // Bucketed accumulation (groupby.h): worth it when the batch has many rows per
 // group -- the per-bucket sums then replace ~(2 + 3 per float SUM) scattered
 // record atomics per row by LDS atomics, and each (bucket, split) block adds
-// a group's moved words once. Needs the bucket's records in 56 KiB of LDS
-// and at most kBucketMax buckets. DFMI_DIAG=1 DFMI_GROUP_BUCKETS=0 / 1
+// a group's moved words once. Needs the bucket's records in the LDS left
+// beside the bucket starts (groupby.h kBucketRecordLds) and at most
+// kBucketMax buckets. DFMI_DIAG=1 DFMI_GROUP_BUCKETS=0 / 1
 // forces the choice (tests run small batches through both).
 constexpr size_t kBucketBuf = kDrainBuf + 8;
 
@@ -963,7 +964,7 @@ struct BucketShape {
 
 BucketShape bucket_shape(const HashDev& H, uint64_t ng) {
     BucketShape b;
-    const size_t fit = 57344 / ((size_t)H.words * 8);  // records in 56 KiB of LDS (+ the block's bucket starts)
+    const size_t fit = (size_t)dfmi::gb::kBucketRecordLds / ((size_t)H.words * 8);  // records in LDS beside the bucket starts
     if (!fit || !ng) return b;
     while ((2ull << b.gshift) <= fit) ++b.gshift;
     b.gpb = 1u << b.gshift;
@@ -1428,6 +1429,80 @@ bool finish_flat(dfmi_context* ctx, dfmi_agg_state* st) {
     return true;
 }
 
+// The finish of one fixed-width key with many groups, ordered and emitted on
+// the device (groupby.h EmitArgs): round, compact, sort values, radix sort,
+// emission; only the caller's dfmi_agg_value arrays cross PCIe. Taken from
+// kDeviceEmitMin groups (below, the host's sort and emission cost less than
+// the launches; at 10^4 groups the device path saves 0.7 ms per finish, at
+// 10^6 ~35 ms); DFMI_DIAG=1 DFMI_GROUP_DEVICE_EMIT=0 / 1 forces the choice.
+constexpr uint64_t kDeviceEmitMin = 2048;
+constexpr size_t kEmitBuf = kBucketBuf + 8;
+static_assert(sizeof(dfmi_agg_value) == 24, "dfmi_agg_value as groupby.hip AggValue");
+
+bool finish_device(dfmi_context* ctx, dfmi_agg_state* st, int64_t cap, dfmi_agg_value* keys, dfmi_agg_value* values,
+                   int64_t* num_groups) {
+    if (st->keys.size() != 1 || st->keys[0].type == DFMI_TYPE_UTF8 || !st->hd ||
+        st->aggs.size() > (size_t)dfmi::gb::kMaxAggs)
+        return false;
+    const bool diag = getenv("DFMI_DIAG") != nullptr;
+    if (diag && getenv("DFMI_GROUP_HOST_FINISH")) return false;
+    const char* force = diag ? getenv("DFMI_GROUP_DEVICE_EMIT") : nullptr;
+    if (force && !atoi(force)) return false;
+    flush_groups(ctx, st);
+    if (!st->groups.empty() || (st->flat && !st->flat->rounded)) return false;
+    HashDev& H = *st->hd;
+    const uint64_t ng = H.ngroups;
+    if (!ng || (!force && ng < kDeviceEmitMin)) return false;
+    *num_groups = (int64_t)ng;
+    if (*num_groups > cap) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "group capacity too small"};
+    if (!keys || !values) throw Fail{DFMI_ERR_INVALID_ARGUMENT, "NULL argument"};
+    if (st->flat) st->spare_flat = std::move(st->flat);
+    const size_t n = st->aggs.size();
+    hipStream_t stream = ctx->stream;
+    dfmi::gb::RoundArgs ra{};
+    ra.acc = H.acc;
+    ra.words = H.words;
+    ra.naggs = (int)n;
+    dfmi::gb::EmitArgs ea{};
+    for (size_t j = 0; j < n; ++j) {
+        ra.off[j] = H.off[j];
+        const int t = st->aggs[j]->arg.type;
+        ra.kind[j] = st->aggs[j]->fn == DFMI_AGG_SUM && is_float_type(t) ? (t == DFMI_TYPE_FLOAT32 ? 2 : 1) : 0;
+        ea.fn[j] = st->aggs[j]->fn;
+        ea.atype[j] = t;
+        ea.rtype[j] = st->aggs[j]->ret_type;
+    }
+    ra.ngroups = ng;
+    ra.out = (unsigned long long*)hd_buf(H, kDrainBuf + 3, ng * (1 + 4 * n) * 8);
+    HIP_TRY(dfmi::gb::launch_round(ra, stream));
+    unsigned* dnull = (unsigned*)hd_buf(H, kDrainBuf, ng * 4);
+    unsigned long long* dkw = (unsigned long long*)hd_buf(H, kDrainBuf + 1, ng * 8);
+    unsigned* dklen = (unsigned*)hd_buf(H, kDrainBuf + 2, ng * 4);
+    HIP_TRY(dfmi::gb::launch_compact(H.t, 1, dnull, dkw, dklen, stream));
+    ea.rec = ra.out;
+    ea.knull = dnull;
+    ea.kw = dkw;
+    ea.ngroups = ng;
+    ea.ktype = st->keys[0].type;
+    ea.naggs = (int)n;
+    ea.keys = hd_buf(H, kEmitBuf, ng * sizeof(dfmi_agg_value));
+    ea.values = hd_buf(H, kEmitBuf + 1, ng * n * sizeof(dfmi_agg_value));
+    auto* sk = (unsigned long long*)hd_buf(H, kEmitBuf + 2, ng * 8);
+    auto* sk2 = (unsigned long long*)hd_buf(H, kEmitBuf + 3, ng * 8);
+    auto* sv = (unsigned*)hd_buf(H, kEmitBuf + 4, ng * 4);
+    auto* sv2 = (unsigned*)hd_buf(H, kEmitBuf + 5, ng * 4);
+    auto* null_at = (unsigned*)hd_buf(H, kEmitBuf + 6, 8);
+    size_t tb = 0;
+    HIP_TRY(dfmi::gb::launch_emit(ea, sk, sk2, sv, sv2, null_at, nullptr, &tb, stream));
+    void* tmp = hd_buf(H, kEmitBuf + 7, tb);
+    HIP_TRY(dfmi::gb::launch_emit(ea, sk, sk2, sv, sv2, null_at, tmp, &tb, stream));
+    HIP_TRY(hipMemcpyAsync(keys, ea.keys, ng * sizeof(dfmi_agg_value), hipMemcpyDeviceToHost, stream));
+    if (n) HIP_TRY(hipMemcpyAsync(values, ea.values, ng * n * sizeof(dfmi_agg_value), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    st->shown.reset();
+    return true;
+}
+
 void emit_flat(const dfmi_agg_state* st, const FlatGroups& f, int64_t cap, dfmi_agg_value* keys,
                dfmi_agg_value* values, int64_t* num_groups) {
     *num_groups = (int64_t)f.ng;
@@ -1789,6 +1864,15 @@ extern "C" int32_t dfmi_agg_state_finish_grouped(dfmi_context* ctx, dfmi_agg_sta
             return st->failure.code;
         }
         HIP_TRY(hipSetDevice(ctx->device));
+        {
+            const auto t0 = std::chrono::steady_clock::now();
+            if (finish_device(ctx, st, cap, keys, values, num_groups)) {
+                if (getenv("DFMI_DIAG") && getenv("DFMI_FINISH_PROFILE"))
+                    fprintf(stderr, "[dfmi finish] %lld groups on the device: %.1f us\n", (long long)*num_groups,
+                            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+                return DFMI_OK;
+            }
+        }
         if (finish_flat(ctx, st)) {
             const auto t0 = std::chrono::steady_clock::now();
             emit_flat(st, *st->flat, cap, keys, values, num_groups);

@@ -136,7 +136,10 @@ struct AccArgs {
 //                    each record word that moved added once into the
 //                    group's global record (atomics over contiguous words)
 // Integer digit sums are order-free: the records equal the accumulate pass's.
-constexpr int kBucketMax = 1024;  // buckets per pass
+constexpr int kBucketMax = 1024;  // buckets per pass (4,096 measured slower: 1e8 rows x 10k keys 4.6 -> 5.5 ms,
+                                  // the rank / scatter LDS counters cost occupancy; 1e5 keys unchanged)
+// LDS bytes of a bucket block's records: 64 KiB less its bucket starts (and the scan's scratch)
+constexpr int kBucketRecordLds = 65536 - 4 * (kBucketMax + 1) - 1024;
 constexpr int kBucketBlocks = 1024;  // blocks of the rank and scatter passes (= k_group_scan's block size)
 
 struct RankArgs {
@@ -208,6 +211,31 @@ struct RoundArgs {
     unsigned long long* out;        // [ngroups][1 + 4 * naggs]
 };
 constexpr unsigned long long kRoundZero = 1ull << 32;
+
+// The finish's ordering and emission on the device (one fixed-width key part:
+// aggregate.cpp finish_device): every group's sort value (key_ord restated,
+// the null group ~0 and moved last afterwards), a radix sort of (value, group
+// id), then one dfmi_agg_value per key and per aggregate in key order, from
+// the compact records of k_group_round -- aggregate.cpp finish_normalized
+// restated.
+struct EmitArgs {
+    const unsigned long long* rec;   // [ngroups][1 + 4 * naggs] compact records
+    const unsigned* knull;           // [ngroups] the key's null bit
+    const unsigned long long* kw;    // [ngroups] the key's bits
+    const unsigned* order;           // [ngroups] group ids in key order (the null group anywhere)
+    const unsigned* null_at;         // [2]: the null group's id (~0u: none), its position in `order`
+    unsigned long long ngroups;
+    int32_t ktype;
+    int32_t naggs;
+    int32_t fn[kMaxAggs], atype[kMaxAggs], rtype[kMaxAggs];
+    void* keys;                      // [ngroups] dfmi_agg_value
+    void* values;                    // [ngroups][naggs] dfmi_agg_value
+};
+// Sort values and group ids (k_group_sortkey), their radix sort (rocPRIM, the
+// temporary storage `tmp` of `tmp_bytes`; tmp == nullptr: *tmp_bytes is set),
+// the null group's position, the emission.
+hipError_t launch_emit(EmitArgs a, unsigned long long* sk, unsigned long long* sk2, unsigned* sv, unsigned* sv2,
+                       unsigned* null_at, void* tmp, size_t* tmp_bytes, hipStream_t stream);
 
 // groupby.hip: launches on `stream` (asynchronous)
 hipError_t launch_claim(const ClaimArgs& a, hipStream_t stream);

@@ -9,6 +9,7 @@
 // SUM is the exact sum of 32-bit digits in units of 2^-1074, MIN / MAX use
 // the order-preserving key (NaN never keyed, -0.0 below +0.0).
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/dfmi.h"
 #include "groupby.h"
@@ -1008,6 +1009,131 @@ __global__ __launch_bounds__(kRoundBlock) void k_group_round(const RoundArgs A) 
     }
 }
 
+// ------------------------------------------------------- device emission
+__device__ __forceinline__ u64 sort_value(int t, u64 bits) {  // key_ord as an unsigned 64-bit order
+    switch (t) {
+        case 11: return (bits >> 63) ? ~bits : (bits | (1ull << 63));  // Float64: totalOrder
+        case 10: {
+            const unsigned b = (unsigned)bits;
+            return (u64)((b >> 31) ? ~b : (b | 0x80000000u));
+        }
+        case 2: case 3: case 4: case 5: return bits ^ (1ull << 63);  // signed: sign-extended bits
+        default: return bits;  // unsigned, Boolean
+    }
+}
+
+__global__ __launch_bounds__(256) void k_group_sortkey(int kt, u64 ng, const unsigned* knull, const u64* kw, u64* sk,
+                                                       unsigned* sv, unsigned* null_at) {
+    for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (u64)gridDim.x * blockDim.x) {
+        const bool null = knull[g] & 1;
+        sk[g] = null ? ~0ull : sort_value(kt, kw[g]);
+        sv[g] = (unsigned)g;
+        if (null) null_at[0] = (unsigned)g;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_group_nullpos(const unsigned* order, u64 ng, unsigned* null_at) {
+    const unsigned ngid = null_at[0];
+    if (ngid == ~0u) return;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += (u64)gridDim.x * blockDim.x)
+        if (order[i] == ngid) null_at[1] = (unsigned)i;
+}
+
+struct AggValue {  // dfmi_agg_value
+    int type;
+    int is_null;
+    long long count;
+    u64 bits;
+};
+
+__device__ __forceinline__ u64 narrow_bits(u64 v, int t) {
+    switch (t) {
+        case 2: return (u64)(i64)(i8)v;
+        case 3: return (u64)(i64)(i16)v;
+        case 4: return (u64)(i64)(i32)v;
+        case 6: return v & 0xffull;
+        case 7: return v & 0xffffull;
+        case 8: return v & 0xffffffffull;
+        default: return v;
+    }
+}
+
+__device__ __forceinline__ u64 key_value_bits(u64 key, int t) {  // aggregate.cpp key_to_bits
+    switch (t) {
+        case 11: return (key >> 63) ? (key & ~(1ull << 63)) : ~key;
+        case 10: {
+            const unsigned k = (unsigned)key;
+            return (k >> 31) ? (u64)(k & 0x7fffffffu) : (u64)(unsigned)~k;
+        }
+        case 2: case 3: case 4: case 5: return key ^ (1ull << 63);
+        default: return key;
+    }
+}
+
+// aggregate.cpp rec_partial + finish_normalized over a compact record.
+__device__ __forceinline__ AggValue finish_value(const u64* rec, int off, int fn, int t, int ret) {
+    const u64* w = rec + off;
+    AggValue r;
+    r.type = ret;
+    r.is_null = 0;
+    r.bits = 0;
+    const u64 count = rec[0] - w[0];
+    r.count = (long long)count;
+    if (fn == DFMI_AGG_COUNT) {
+        r.bits = count;
+        return r;
+    }
+    if (count == 0) {
+        r.is_null = 1;
+        return r;
+    }
+    const bool f32 = t == 10, flt = t == 10 || t == 11;
+    const u64 qnan = f32 ? 0x7FC00000ull : 0x7FF8000000000000ull;
+    if (fn == DFMI_AGG_SUM) {
+        if (!flt) {
+            r.bits = narrow_bits(w[3], t);
+            return r;
+        }
+        const u64 flags = (w[1] & 0xffffffffull) | (count > w[3] ? (u64)AGGF_NONNEGZERO : 0ull);
+        if ((flags & AGGF_NAN) || ((flags & AGGF_PINF) && (flags & AGGF_NINF))) {
+            r.bits = qnan;
+        } else if (flags & (AGGF_PINF | AGGF_NINF)) {
+            const bool pos = flags & AGGF_PINF;
+            r.bits = f32 ? (pos ? 0x7F800000ull : 0xFF800000ull) : (pos ? 0x7FF0000000000000ull : 0xFFF0000000000000ull);
+        } else {
+            double v = __builtin_bit_cast(double, w[2]);
+            if (w[1] & kRoundZero) v = (flags & AGGF_NONNEGZERO) ? 0.0 : -0.0;
+            r.bits = f32 ? (u64)__builtin_bit_cast(unsigned, (float)v) : __builtin_bit_cast(u64, v);
+        }
+        return r;
+    }
+    // MIN / MAX
+    const bool value = count > w[3];
+    r.bits = value ? key_value_bits(w[2], t) : qnan;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_group_emit(const EmitArgs A) {
+    const unsigned ngid = A.null_at[0], npos = A.null_at[1];
+    const int cw = 1 + 4 * A.naggs;
+    AggValue* keys = (AggValue*)A.keys;
+    AggValue* vals = (AggValue*)A.values;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < A.ngroups; i += (u64)gridDim.x * blockDim.x) {
+        unsigned g;
+        if (ngid == ~0u) g = A.order[i];
+        else if (i == A.ngroups - 1) g = ngid;  // the null group last
+        else g = A.order[i < npos ? i : i + 1];
+        const u64* rec = A.rec + (u64)g * (u64)cw;
+        AggValue k;
+        k.type = A.ktype;
+        k.is_null = (A.knull[g] & 1) ? 1 : 0;
+        k.count = (long long)rec[0];
+        k.bits = k.is_null ? 0ull : (A.ktype == 1 ? A.kw[g] : narrow_bits(A.kw[g], A.ktype));
+        keys[i] = k;
+        for (int j = 0; j < A.naggs; ++j) vals[i * (u64)A.naggs + j] = finish_value(rec, 1 + 4 * j, A.fn[j], A.atype[j], A.rtype[j]);
+    }
+}
+
 static int grid_for(long long items, int per_block = 256, int cap = 8192) {
     long long g = (items + per_block - 1) / per_block;
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -1075,8 +1201,26 @@ hipError_t launch_buckets(const RankArgs& r, ScatterArgs s, BucketArgs b, hipStr
     hipLaunchKernelGGL(k_group_scan, dim3(r.nbuckets), dim3(kBucketBlocks), 0, st, r.bh, (unsigned*)s.tot);
     hipLaunchKernelGGL(k_group_scatter, g, blk, 0, st, s);
     const size_t lds = (size_t)b.gpb * (size_t)b.words * 8;
-    if (lds > 57344 || b.nbuckets > kBucketMax || b.splits < 1) return hipErrorInvalidValue;
+    if (lds > (size_t)kBucketRecordLds || b.nbuckets > kBucketMax || b.splits < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_group_bucket, dim3(b.nbuckets * b.splits), blk, lds, st, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit(EmitArgs a, u64* sk, u64* sk2, unsigned* sv, unsigned* sv2, unsigned* null_at, void* tmp,
+                       size_t* tmp_bytes, hipStream_t st) {
+    if (!tmp) return rocprim::radix_sort_pairs(nullptr, *tmp_bytes, sk, sk2, sv, sv2, a.ngroups, 0, 64, st);
+    const u64 ng = a.ngroups;
+    hipError_t e = hipMemsetAsync(null_at, 0xff, 8, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_group_sortkey, dim3(grid_for((long long)ng)), dim3(256), 0, st, a.ktype, ng, a.knull, a.kw, sk,
+                       sv, null_at);
+    e = rocprim::radix_sort_pairs(tmp, *tmp_bytes, sk, sk2, sv, sv2, ng, 0, 64, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_group_nullpos, dim3(grid_for((long long)ng)), dim3(256), 0, st, (const unsigned*)sv2, ng,
+                       null_at);
+    a.order = sv2;
+    a.null_at = null_at;
+    hipLaunchKernelGGL(k_group_emit, dim3(grid_for((long long)ng)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -429,3 +429,57 @@ def test_group_by_every_argument_type(monkeypatch, buckets):
     for start in range(0, len(aggs_e), 14):  # at most 15 aggregates per grouped state
         out = run_multi(s, b, None, [Column(0)], aggs_e[start:start + 14], batch_rows=9_000)
         assert out is not None and len(out[0]) > 290
+
+
+@pytest.mark.parametrize("kt", ["int64", "uint64", "float64", "float32", "int8", "boolean"])
+def test_group_by_device_emission(monkeypatch, kt):
+    """The finish ordered and emitted on the device (aggregate.cpp
+    finish_device: sort values, rocPRIM radix sort, the null group moved
+    last, dfmi_agg_value records built on the device), forced on small
+    tables (DFMI_GROUP_DEVICE_EMIT=1): keys at their type's extremes next to
+    the null group (INT64_MAX and UINT64_MAX sort like the null group's
+    ~0 before it is moved), Float64 / Float32 keys with NaN, -0.0 and
+    infinities; SUM / COUNT / MIN / MAX of every kind -- equal to the oracle."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_GROUP_DEVICE_EMIT", "1")
+    rng = np.random.default_rng(74)
+    n = 20_000
+    dts = {"int64": (DataType.Int64, np.int64), "uint64": (DataType.UInt64, np.uint64),
+           "float64": (DataType.Float64, np.float64), "float32": (DataType.Float32, np.float32),
+           "int8": (DataType.Int8, np.int8), "boolean": (DataType.Boolean, np.bool_)}
+    dt, nt = dts[kt]
+    if kt in ("int64", "uint64", "int8"):
+        info = np.iinfo(nt)
+        pool = np.array([info.min, info.max, 0, 1, info.max - 1, info.min + 1] +
+                        list(rng.integers(int(info.min), int(info.max), 500, endpoint=True,
+                                          dtype=np.int64 if info.min < 0 else np.uint64)), dtype=nt)
+    elif kt == "boolean":
+        pool = np.array([False, True])
+    else:
+        pool = np.array([np.nan, -np.nan, 0.0, -0.0, np.inf, -np.inf, 1.5, -1.5] +
+                        list(rng.standard_normal(500)), dtype=nt)
+    keys = pool[rng.integers(0, len(pool), n)]
+    s2, b2 = _rounding_table(rng, n)
+    s = Schema([Field("k", dt, True)] + list(s2.fields[1:]) + [Field("i", DataType.Int16, True)])
+    b = RecordBatch(s, [Array.from_numpy(dt, keys, rng.random(n) >= 0.03)] + list(b2.columns[1:]) +
+                    [Array.from_numpy(DataType.Int16, rng.integers(-2 ** 15, 2 ** 15, n).astype(np.int16),
+                                      rng.random(n) >= 0.1)])
+    aggs_e = [agg("SUM", Column(1), s), agg("SUM", Column(2), s), agg("COUNT", Column(1), s),
+              agg("MIN", Column(2), s), agg("MAX", Column(1), s), agg("SUM", Column(3), s),
+              agg("MIN", Column(3), s), agg("MAX", Column(3), s)]
+    for br in (0, 7_000):
+        out = run_multi(s, b, None, [Column(0)], aggs_e, batch_rows=br)
+        assert out is not None and len(out[0]) >= 3
+
+
+def test_group_by_device_emission_chosen():
+    """2^17 distinct Int64 keys (more than kDeviceEmitMin groups): the finish
+    is ordered and emitted on the device without a diagnostics switch, and
+    equals the oracle."""
+    rng = np.random.default_rng(75)
+    n = 1 << 18
+    s = Schema([Field("k", DataType.Int64, True), Field("x", DataType.Float64, True)])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Int64, rng.permutation(n) // 2 * 1_000_003, rng.random(n) >= 0.01),
+                        Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.1)])
+    out = run_multi(s, b, None, [Column(0)], [agg("SUM", Column(1), s), agg("COUNT", Column(1), s)])
+    assert out is not None and len(out[0]) > 130_000  # (keys whose two rows are both NULL fold into the null group)

@@ -8,8 +8,10 @@ keys Int64 x Utf8 (the device hash table: aggregate.cpp group_batch_hashed)
 warm-up, and the host-merge A/B (DFMI_DIAG=1 DFMI_GROUP_HOST=1) on the same
 batches; --sweep: Float64 keys of 4 ... 1e6 distinct values instead.
 --card=C1,C2: the sweep at those cardinalities only; --phases: add and
-finish timed apart (add synchronised).
-usage: groupby_probe.py [rows] [--no-host] [--sweep] [--card=...] [--phases]"""
+finish timed apart (add synchronised); --reuse: one state per case, reset
+before each run (the hash table keeps the size it grew to, as a state that
+takes many batches does).
+usage: groupby_probe.py [rows] [--no-host] [--sweep] [--card=...] [--phases] [--reuse]"""
 import os
 import sys
 import time
@@ -36,6 +38,7 @@ v = Array.from_numpy(DataType.Float64, rng.random(n)).to(dev)
 words = [("w%d_" % i + "x" * (i % 17)) for i in range(10_000)]
 CARDS = (4, 16, 100, 1000, 10_000, 100_000, 1_000_000)
 PHASES = "--phases" in sys.argv
+REUSE = "--reuse" in sys.argv  # one state per case, reset before each run (the table keeps its size)
 for a in sys.argv:
     if a.startswith("--card="):
         CARDS = tuple(int(float(c)) for c in a[7:].split(","))
@@ -65,8 +68,12 @@ def run(name, kcols, reps=3):
     cs = [compile_expr(None, a, s, AGG) for a in aggs]
     kp = [compile_scalar_expr(None, Column(i), s, AGG) for i in range(nk)]
     best, groups, split = None, 0, None
+    st = eng.grouped_agg_state(kp if nk > 1 else kp[0], cs) if REUSE else None
     for rep in range(reps + 1):  # rep 0 warms up (code objects, allocations, clocks)
-        st = eng.grouped_agg_state(kp if nk > 1 else kp[0], cs)
+        if REUSE:
+            st.reset()
+        else:
+            st = eng.grouped_agg_state(kp if nk > 1 else kp[0], cs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st.add(None, b, AGG)
