@@ -962,13 +962,22 @@ struct BucketShape {
     int nbuckets = 0, splits = 0;
 };
 
+// Records per bucket: as many as fit the LDS a block keeps beside its bucket
+// starts with two blocks per CU (kBucketRecordLds); when that needs more than
+// kBucketMax buckets, as many as fit one block per CU (kBucketRecordLdsBig,
+// 160 KiB per workgroup on gfx950).
 BucketShape bucket_shape(const HashDev& H, uint64_t ng) {
     BucketShape b;
-    const size_t fit = (size_t)dfmi::gb::kBucketRecordLds / ((size_t)H.words * 8);  // records in LDS beside the bucket starts
-    if (!fit || !ng) return b;
-    while ((2ull << b.gshift) <= fit) ++b.gshift;
-    b.gpb = 1u << b.gshift;
-    b.nbuckets = (int)((ng + b.gpb - 1) / b.gpb);
+    if (!ng) return b;
+    for (int budget : {dfmi::gb::kBucketRecordLds, dfmi::gb::kBucketRecordLdsBig}) {
+        const size_t fit = (size_t)budget / ((size_t)H.words * 8);
+        if (!fit) continue;
+        b.gshift = 0;
+        while ((2ull << b.gshift) <= fit) ++b.gshift;
+        b.gpb = 1u << b.gshift;
+        b.nbuckets = (int)((ng + b.gpb - 1) / b.gpb);
+        if (b.nbuckets <= dfmi::gb::kBucketMax) break;
+    }
     b.splits = std::max(1, std::min(1024, 2048 / std::max(1, b.nbuckets)));
     return b;
 }

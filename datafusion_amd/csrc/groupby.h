@@ -140,6 +140,7 @@ constexpr int kBucketMax = 1024;  // buckets per pass (4,096 measured slower: 1e
                                   // the rank / scatter LDS counters cost occupancy; 1e5 keys unchanged)
 // LDS bytes of a bucket block's records: 64 KiB less its bucket starts (and the scan's scratch)
 constexpr int kBucketRecordLds = 65536 - 4 * (kBucketMax + 1) - 1024;
+constexpr int kBucketRecordLdsBig = 163840 - 4 * (kBucketMax + 1) - 1024;  // one block per CU
 constexpr int kBucketBlocks = 1024;  // blocks of the rank and scatter passes (= k_group_scan's block size)
 
 struct RankArgs {

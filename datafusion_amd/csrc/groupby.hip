@@ -1201,7 +1201,13 @@ hipError_t launch_buckets(const RankArgs& r, ScatterArgs s, BucketArgs b, hipStr
     hipLaunchKernelGGL(k_group_scan, dim3(r.nbuckets), dim3(kBucketBlocks), 0, st, r.bh, (unsigned*)s.tot);
     hipLaunchKernelGGL(k_group_scatter, g, blk, 0, st, s);
     const size_t lds = (size_t)b.gpb * (size_t)b.words * 8;
-    if (lds > (size_t)kBucketRecordLds || b.nbuckets > kBucketMax || b.splits < 1) return hipErrorInvalidValue;
+    if (lds > (size_t)kBucketRecordLdsBig || b.nbuckets > kBucketMax || b.splits < 1) return hipErrorInvalidValue;
+    if (lds > (size_t)kBucketRecordLds) {  // more than 64 KiB per workgroup: raise the kernel's limit (once)
+        static const hipError_t raised = hipFuncSetAttribute((const void*)k_group_bucket,
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                             kBucketRecordLdsBig);
+        if (raised != hipSuccess) return raised;
+    }
     hipLaunchKernelGGL(k_group_bucket, dim3(b.nbuckets * b.splits), blk, lds, st, b);
     return hipGetLastError();
 }

@@ -483,3 +483,22 @@ def test_group_by_device_emission_chosen():
                         Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.1)])
     out = run_multi(s, b, None, [Column(0)], [agg("SUM", Column(1), s), agg("COUNT", Column(1), s)])
     assert out is not None and len(out[0]) > 130_000  # (keys whose two rows are both NULL fold into the null group)
+
+
+def test_group_by_bucketed_large_lds(monkeypatch):
+    """~38,000 groups of three exact Float64 SUMs: with 64 KiB of LDS a
+    bucket holds 32 records, past the 1,024 buckets, so the bucket pass takes
+    one 160 KiB workgroup per CU (64 records per bucket) -- the groups equal
+    the oracle's (bucketed passes forced for the 1.2e5-row batch)."""
+    monkeypatch.setenv("DFMI_DIAG", "1")
+    monkeypatch.setenv("DFMI_GROUP_BUCKETS", "1")
+    rng = np.random.default_rng(76)
+    n = 120_000
+    s = Schema([Field("k", DataType.Int64, True)] + [Field(c, DataType.Float64, True) for c in "xyz"])
+    b = RecordBatch(s, [Array.from_numpy(DataType.Int64, rng.integers(0, 40_000, n) * 7, rng.random(n) >= 0.01)] +
+                    [Array.from_numpy(DataType.Float64, wild_doubles(rng, n), rng.random(n) >= 0.05) for _ in range(3)])
+    before = _bucketed_batches()
+    aggs_e = [agg("SUM", Column(1), s), agg("SUM", Column(2), s), agg("SUM", Column(3), s), agg("COUNT", Column(1), s)]
+    out = run_multi(s, b, None, [Column(0)], aggs_e, batch_rows=60_000)
+    assert out is not None and len(out[0]) > 37_000
+    assert _bucketed_batches() == before + 2
