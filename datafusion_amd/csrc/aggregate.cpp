@@ -1321,7 +1321,7 @@ void sort_flat(const dfmi_agg_state* st, FlatGroups& f) {
     for (uint64_t g = 0; g < ng; ++g) f.order[g] = (uint32_t)g;
     std::vector<int> kt(nk);
     for (size_t p = 0; p < nk; ++p) kt[p] = st->keys[p].type;
-    std::sort(f.order.begin(), f.order.end(), [&](uint32_t a, uint32_t b) {
+    auto less = [&](uint32_t a, uint32_t b) {
         for (size_t p = 0; p < nk; ++p) {
             const bool na = (f.knull[a] >> p) & 1, nb = (f.knull[b] >> p) & 1;
             if (na != nb) return !na;
@@ -1337,7 +1337,73 @@ void sort_flat(const dfmi_agg_state* st, FlatGroups& f) {
             }
         }
         return false;
-    });
+    };
+    if (ng < 256) {
+        std::sort(f.order.begin(), f.order.end(), less);
+        return;
+    }
+    // Composite words per group, compared lexicographically: per part a null
+    // flag (the null last) and a value -- a fixed-width part its order value,
+    // a Utf8 part its first 8 bytes big-endian, zero-padded. LSD radix over the
+    // words (8-bit digits, a digit every group shares skipped), then the runs
+    // the prefixes cannot order re-sorted with the full comparator.
+    const size_t W = 2 * nk;
+    std::vector<uint64_t> cw(ng * W);
+    bool any_utf8 = false;
+    for (uint64_t g = 0; g < ng; ++g)
+        for (size_t p = 0; p < nk; ++p) {
+            const bool null = (f.knull[g] >> p) & 1;
+            uint64_t v = 0;
+            if (!null) {
+                const uint64_t w = f.kw[g * nk + p];
+                if (kt[p] == DFMI_TYPE_UTF8) {
+                    any_utf8 = true;
+                    const unsigned len = f.klen[g * nk + p];
+                    const uint8_t* c = f.arena.data() + w;
+                    for (unsigned q = 0; q < 8; ++q) v = (v << 8) | (q < len ? c[q] : 0u);
+                } else {
+                    const __int128 o = key_ord(kt[p], w);
+                    v = is_signed_type(kt[p]) ? (uint64_t)(int64_t)o ^ (1ull << 63) : (uint64_t)o;
+                }
+            }
+            cw[g * W + 2 * p] = null ? 1 : 0;
+            cw[g * W + 2 * p + 1] = v;
+        }
+    std::vector<uint32_t> tmp(ng);
+    std::vector<uint32_t> cnt(256);
+    for (size_t q = W; q-- > 0;) {
+        const int digits = (q & 1) ? 8 : 1;
+        for (int d = 0; d < digits; ++d) {
+            const int sh = 8 * d;
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (uint64_t i = 0; i < ng; ++i) ++cnt[(cw[(size_t)f.order[i] * W + q] >> sh) & 0xff];
+            if (cnt[(cw[(size_t)f.order[0] * W + q] >> sh) & 0xff] == ng) continue;
+            uint32_t sum = 0;
+            for (auto& c : cnt) {
+                const uint32_t t = c;
+                c = sum;
+                sum += t;
+            }
+            for (uint64_t i = 0; i < ng; ++i) tmp[cnt[(cw[(size_t)f.order[i] * W + q] >> sh) & 0xff]++] = f.order[i];
+            std::copy(tmp.begin(), tmp.end(), f.order.begin());
+        }
+    }
+    if (!any_utf8) return;
+    // the word order is exact up to the first Utf8 part's prefix: groups that
+    // agree on every word up to it may be out of order (the rest of that part
+    // decides before any later part), so each such run is re-sorted in full
+    size_t p1 = 0;
+    while (kt[p1] != DFMI_TYPE_UTF8) ++p1;
+    const size_t E = 2 * p1 + 2;
+    auto same = [&](uint32_t a, uint32_t b) {
+        return std::equal(cw.begin() + (size_t)a * W, cw.begin() + (size_t)a * W + E, cw.begin() + (size_t)b * W);
+    };
+    for (uint64_t i = 0; i < ng;) {
+        uint64_t j = i + 1;
+        while (j < ng && same(f.order[i], f.order[j])) ++j;
+        if (j - i > 1) std::sort(f.order.begin() + i, f.order.begin() + j, less);
+        i = j;
+    }
 }
 
 // Aggregate j's partial of group record `rec` (the device record layout:
