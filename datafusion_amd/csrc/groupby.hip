@@ -174,15 +174,27 @@ __device__ __forceinline__ int claim_row(const ClaimArgs& A, const RowKey& r, u6
                     sr.kw[p] = w;
                     sr.klen[p] = r.len[p];
                 }
-                // a one-part Utf8 key of at most 24 bytes: its bytes in the slot's spare
-                // words too (the same for two- and three-part keys measured slower)
-                if (NK == 1 && r.s[0] && r.len[0] <= 24) {
-                    u64 w[3];
-                    inline_pack(r.s[0], r.len[0], w);
-                    sr.kw[1] = w[0];
-                    sr.kw[2] = w[1];
-                    sr.kw[3] = w[2];
-                    sr.knull = r.nullm | kInline;
+                // a key whose only non-null Utf8 part fits the slot's spare words
+                // (kw[NK..3]: 24 bytes with one part, 16 with two, 8 with three): its
+                // bytes in the slot too
+                if (NK < kMaxKeys) {
+                    int nu = 0;
+                    const u8* ps = nullptr;
+                    unsigned pl = 0;
+#pragma unroll
+                    for (int p = 0; p < NK; ++p)
+                        if (r.s[p]) {
+                            ++nu;
+                            ps = r.s[p];
+                            pl = r.len[p];
+                        }
+                    if (nu == 1 && pl <= 8u * (kMaxKeys - NK)) {
+                        u64 w[3];
+                        inline_pack(ps, pl, w);
+#pragma unroll
+                        for (int q = NK; q < kMaxKeys; ++q) sr.kw[q] = w[q - NK];
+                        sr.knull = r.nullm | kInline;
+                    }
                 }
                 return (int)s;
             }
@@ -412,8 +424,8 @@ __device__ __forceinline__ bool row_group(const Col* k, long long m, uint32_t ep
             const u64 kwv = sr.kw[p];
             if (r.s[p]) {
                 const unsigned kl = sr.klen[p];
-                if (NK == 1 && (sr.knull & kInline)) {
-                    same = kl == r.len[p] && inline_eq(r.s[p], kl, &sr.kw[1], r.end[p]);
+                if (NK < kMaxKeys && (sr.knull & kInline)) {
+                    same = kl == r.len[p] && inline_eq(r.s[p], kl, &sr.kw[NK], r.end[p]);
                     continue;
                 }
                 const u8* other = cur ? (const u8*)k[p].values + k[p].offsets[rr] : arena + kwv;
@@ -470,18 +482,21 @@ __global__ __launch_bounds__(256) void k_group_accumulate(const AccArgs A) {
 // (groupby.h "Bucketed accumulation"). The rank and scatter passes run
 // kBucketBlocks blocks of 256 threads over the same tiles of kScatterTile rows
 // per block, so a block's rows of a bucket fill exactly its positions.
-constexpr int kRankU = 4;                   // rows per thread per sub-tile (independent load chains)
-constexpr int kRankRows = 256 * kRankU;
+// rows per thread per sub-tile (independent load chains): 4, or 2 with several key
+// parts (their keys and slot words in registers: 147 VGPRs, 3 waves / SIMD, at 4)
+template <int NK>
+constexpr int rank_u() { return NK >= 2 ? 2 : 4; }
 constexpr int kScatterTile = 4096;          // rows per block per tile (rank and scatter alike)
 
 template <int NK>
 __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
+    constexpr int kRankU = rank_u<NK>();
     __shared__ unsigned cnt[kBucketMax];
     for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
     const Table& t = A.t;
     for (long long T0 = (long long)blockIdx.x * kScatterTile; T0 < A.m; T0 += (long long)gridDim.x * kScatterTile)
-    for (long long t0 = T0; t0 < T0 + kScatterTile && t0 < A.m; t0 += kRankRows) {
+    for (long long t0 = T0; t0 < T0 + kScatterTile && t0 < A.m; t0 += 256 * kRankU) {
         // the row_group chain of kRankU rows at once: slots, keys, the slots' words, then the decisions
         int sl[kRankU];
         RowKey r[kRankU];
@@ -521,8 +536,8 @@ __global__ __launch_bounds__(256) void k_group_rank(const RankArgs A) {
                         if (!same || ((r[u].nullm >> p) & 1)) continue;
                         if (r[u].s[p]) {
                             const unsigned kl = sr[u].klen[p];
-                            if (NK == 1 && (sr[u].knull & kInline)) {
-                                same = kl == r[u].len[p] && inline_eq(r[u].s[p], kl, &sr[u].kw[1], r[u].end[p]);
+                            if (NK < kMaxKeys && (sr[u].knull & kInline)) {
+                                same = kl == r[u].len[p] && inline_eq(r[u].s[p], kl, &sr[u].kw[NK], r[u].end[p]);
                                 continue;
                             }
                             const u8* other = cur ? (const u8*)A.k[p].values + A.k[p].offsets[rr] : A.arena + sr[u].kw[p];
