@@ -145,7 +145,7 @@ __device__ __forceinline__ int claim_row(const ClaimArgs& A, const RowKey& r, u6
     for (u64 probe = 0; probe <= t.mask && probe < kProbeMax; ++probe) {
         if (probe) {
             s = (s + 1) & t.mask;
-            cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         // a long probe into a table past its load limit (claims racing past the
         // limit can fill it): give up, the pass reruns on the grown table
@@ -216,7 +216,10 @@ __global__ __launch_bounds__(256) void k_group_claim(const ClaimArgs A) {
         RowKey r;
         const u64 c = (row_key<NK>(A.k, i, A.m, r) & A.hash_mask) | 1ull;
         const u64 s = gmix(c) & t.mask;
-        const u64 cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (workgroup scope: a plain, L1-cached load -- a stale 0 only sends the row to the
+        // CAS, which returns the slot's real word; with few keys every CU reads the same
+        // few lines, which agent-scope loads would take from one L2 channel each time)
+        const u64 cur = __hip_atomic_load(&t.ctl[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int res = cur == c ? (int)s : claim_row<NK>(A, r, c, s, cur, i);
         if (res < 0) overflow = true;
         A.sidx[i] = res;
@@ -832,13 +835,17 @@ __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
     const u64 left = A.ngroups - g0;
     const unsigned nb = (unsigned)(left < (u64)A.gpb ? left : (u64)A.gpb);
     const int W = A.words;
-    for (unsigned x = threadIdx.x; x < nb * (unsigned)W; x += blockDim.x) lrec[x] = A.pattern[x % (unsigned)W];
+    // (C copies of a small bucket's records, the lanes spread over them, measured
+    // no faster at 4 and 16 groups: 1.23 ms per 1e8 rows either way)
+    constexpr unsigned C = 1;
+    for (unsigned x = threadIdx.x; x < C * nb * (unsigned)W; x += blockDim.x) lrec[x] = A.pattern[x % (unsigned)W];
     __syncthreads();
     const unsigned r0 = start[b], len = start[b + 1] - start[b];
     const unsigned q0 = r0 + (unsigned)((u64)len * (u64)sp / (u64)A.splits);
     const unsigned q1 = r0 + (unsigned)((u64)len * (u64)(sp + 1) / (u64)A.splits);
+    u64* const mine = lrec + (u64)(threadIdx.x & (C - 1)) * nb * (u64)W;
     for (unsigned pos = q0 + threadIdx.x; pos < q1; pos += blockDim.x) {
-        u64* rec = lrec + (u64)(A.pg[pos] - (unsigned)g0) * (u64)W;
+        u64* rec = mine + (u64)(A.pg[pos] - (unsigned)g0) * (u64)W;
         atomicAdd(&rec[0], 1ull);
         const unsigned nm = A.pn ? A.pn[pos] : 0u;
         for (int j = 0; j < A.naggs; ++j) {
@@ -849,16 +856,21 @@ __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
     __syncthreads();
     for (unsigned x = threadIdx.x; x < nb * (unsigned)W; x += blockDim.x) {
         const int w = (int)(x % (unsigned)W);
-        const u64 v = lrec[x];
-        if (v == A.pattern[w]) continue;
-        u64* dst = A.acc + (g0 + x / (unsigned)W) * (u64)W + (u64)w;
         int j = -1;  // the aggregate owning word w (w = 0: the group's rows)
         for (int q = 0; q < A.naggs; ++q)
             if (A.a[q].off <= w) j = q;
         const int r = j < 0 ? -1 : w - A.a[j].off;
-        if (r == 1) atomicOr(dst, v);
-        else if (r == 2 && A.a[j].fn == DFMI_AGG_MIN) atomicMin(dst, v);
-        else if (r == 2 && A.a[j].fn == DFMI_AGG_MAX) atomicMax(dst, v);
+        const int op = r == 1 ? 1 : (r == 2 && A.a[j].fn == DFMI_AGG_MIN) ? 2 : (r == 2 && A.a[j].fn == DFMI_AGG_MAX) ? 3 : 0;
+        u64 v = lrec[x];
+        for (unsigned c = 1; c < C; ++c) {
+            const u64 o = lrec[(u64)c * nb * (u64)W + x];
+            v = op == 1 ? (v | o) : op == 2 ? (o < v ? o : v) : op == 3 ? (o > v ? o : v) : v + o;
+        }
+        if (v == A.pattern[w]) continue;
+        u64* dst = A.acc + (g0 + x / (unsigned)W) * (u64)W + (u64)w;
+        if (op == 1) atomicOr(dst, v);
+        else if (op == 2) atomicMin(dst, v);
+        else if (op == 3) atomicMax(dst, v);
         else atomicAdd(dst, v);
     }
 }
