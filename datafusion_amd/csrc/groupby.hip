@@ -835,17 +835,15 @@ __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
     const u64 left = A.ngroups - g0;
     const unsigned nb = (unsigned)(left < (u64)A.gpb ? left : (u64)A.gpb);
     const int W = A.words;
-    // (C copies of a small bucket's records, the lanes spread over them, measured
-    // no faster at 4 and 16 groups: 1.23 ms per 1e8 rows either way)
-    constexpr unsigned C = 1;
-    for (unsigned x = threadIdx.x; x < C * nb * (unsigned)W; x += blockDim.x) lrec[x] = A.pattern[x % (unsigned)W];
+    // (copies of a small bucket's records, the lanes spread over them, measured no
+    // faster at 4 and 16 groups: 1.23 ms per 1e8 rows either way -- one copy)
+    for (unsigned x = threadIdx.x; x < nb * (unsigned)W; x += blockDim.x) lrec[x] = A.pattern[x % (unsigned)W];
     __syncthreads();
     const unsigned r0 = start[b], len = start[b + 1] - start[b];
     const unsigned q0 = r0 + (unsigned)((u64)len * (u64)sp / (u64)A.splits);
     const unsigned q1 = r0 + (unsigned)((u64)len * (u64)(sp + 1) / (u64)A.splits);
-    u64* const mine = lrec + (u64)(threadIdx.x & (C - 1)) * nb * (u64)W;
     for (unsigned pos = q0 + threadIdx.x; pos < q1; pos += blockDim.x) {
-        u64* rec = mine + (u64)(A.pg[pos] - (unsigned)g0) * (u64)W;
+        u64* rec = lrec + (u64)(A.pg[pos] - (unsigned)g0) * (u64)W;
         atomicAdd(&rec[0], 1ull);
         const unsigned nm = A.pn ? A.pn[pos] : 0u;
         for (int j = 0; j < A.naggs; ++j) {
@@ -861,11 +859,7 @@ __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
             if (A.a[q].off <= w) j = q;
         const int r = j < 0 ? -1 : w - A.a[j].off;
         const int op = r == 1 ? 1 : (r == 2 && A.a[j].fn == DFMI_AGG_MIN) ? 2 : (r == 2 && A.a[j].fn == DFMI_AGG_MAX) ? 3 : 0;
-        u64 v = lrec[x];
-        for (unsigned c = 1; c < C; ++c) {
-            const u64 o = lrec[(u64)c * nb * (u64)W + x];
-            v = op == 1 ? (v | o) : op == 2 ? (o < v ? o : v) : op == 3 ? (o > v ? o : v) : v + o;
-        }
+        const u64 v = lrec[x];
         if (v == A.pattern[w]) continue;
         u64* dst = A.acc + (g0 + x / (unsigned)W) * (u64)W + (u64)w;
         if (op == 1) atomicOr(dst, v);
