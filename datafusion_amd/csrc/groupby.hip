@@ -842,13 +842,30 @@ __global__ __launch_bounds__(256) void k_group_bucket(const BucketArgs A) {
     const unsigned r0 = start[b], len = start[b + 1] - start[b];
     const unsigned q0 = r0 + (unsigned)((u64)len * (u64)sp / (u64)A.splits);
     const unsigned q1 = r0 + (unsigned)((u64)len * (u64)(sp + 1) / (u64)A.splits);
-    for (unsigned pos = q0 + threadIdx.x; pos < q1; pos += blockDim.x) {
-        u64* rec = lrec + (u64)(A.pg[pos] - (unsigned)g0) * (u64)W;
-        atomicAdd(&rec[0], 1ull);
-        const unsigned nm = A.pn ? A.pn[pos] : 0u;
+    // kBucketU rows per thread per round: their loads issued together (the
+    // streamed group ids and argument words are the pass's only global reads)
+    constexpr unsigned kBucketU = 4;
+    for (unsigned base = q0 + threadIdx.x; base < q1; base += kBucketU * blockDim.x) {
+        unsigned lg[kBucketU], nm[kBucketU];
+#pragma unroll
+        for (unsigned u = 0; u < kBucketU; ++u) {
+            const unsigned pos = base + u * blockDim.x;
+            lg[u] = pos < q1 ? A.pg[pos] - (unsigned)g0 : ~0u;
+            nm[u] = pos < q1 && A.pn ? A.pn[pos] : 0u;
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kBucketU; ++u)
+            if (lg[u] != ~0u) atomicAdd(&lrec[(u64)lg[u] * (u64)W], 1ull);
         for (int j = 0; j < A.naggs; ++j) {
-            const u64 bits = A.pcol[j] >= 0 ? A.pv[(u64)A.pcol[j] * (u64)A.m + pos] : 0ull;
-            lds_agg_dispatch(A.a[j], rec, (nm >> j) & 1, bits);
+            u64 bits[kBucketU];
+#pragma unroll
+            for (unsigned u = 0; u < kBucketU; ++u) {
+                const unsigned pos = base + u * blockDim.x;
+                bits[u] = A.pcol[j] >= 0 && pos < q1 ? A.pv[(u64)A.pcol[j] * (u64)A.m + pos] : 0ull;
+            }
+#pragma unroll
+            for (unsigned u = 0; u < kBucketU; ++u)
+                if (lg[u] != ~0u) lds_agg_dispatch(A.a[j], lrec + (u64)lg[u] * (u64)W, (nm[u] >> j) & 1, bits[u]);
         }
     }
     __syncthreads();
