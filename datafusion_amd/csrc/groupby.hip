@@ -736,18 +736,39 @@ __global__ __launch_bounds__(256) void k_group_scatter(const ScatterArgs A) {
             }
         __syncthreads();
         const unsigned placed = tcnt[A.nbuckets];
-        for (unsigned e = threadIdx.x; e < placed; e += blockDim.x) {
-            const unsigned gg = sg[e], b = gg >> A.gshift;
-            const unsigned pos = cur[b] + (e - tcnt[b]);
-            const long long i = T0 + si[e];
-            A.pg[pos] = gg;
-            if (A.pn) {
-                unsigned nm = 0;
-                for (int j = 0; j < A.naggs; ++j)
-                    if (!valid_at(A.arg[j], i)) nm |= 1u << j;
-                A.pn[pos] = nm;
+        // four staged rows per thread per round: their argument loads issued before any store
+        for (unsigned e0 = threadIdx.x; e0 < placed; e0 += 4 * blockDim.x) {
+            unsigned gg[4], pos[4];
+            long long i[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const unsigned e = e0 + u * blockDim.x;
+                const bool in = e < placed;
+                gg[u] = in ? sg[e] : 0u;
+                const unsigned b = gg[u] >> A.gshift;
+                pos[u] = in ? cur[b] + (e - tcnt[b]) : ~0u;
+                i[u] = T0 + (in ? si[e] : 0);
             }
-            for (int c = 0; c < A.npay; ++c) A.pv[(u64)c * (u64)A.m + pos] = key_bits(A.pay[c], i);
+            if (A.pn) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    unsigned nm = 0;
+                    for (int j = 0; j < A.naggs; ++j)
+                        if (!valid_at(A.arg[j], i[u])) nm |= 1u << j;
+                    if (pos[u] != ~0u) A.pn[pos[u]] = nm;
+                }
+            }
+            for (int c = 0; c < A.npay; ++c) {
+                u64 x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = pos[u] != ~0u ? key_bits(A.pay[c], i[u]) : 0ull;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (pos[u] != ~0u) A.pv[(u64)c * (u64)A.m + pos[u]] = x[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (pos[u] != ~0u) A.pg[pos[u]] = gg[u];
         }
         __syncthreads();
         for (int b = threadIdx.x; b < A.nbuckets; b += blockDim.x) cur[b] += tcnt[b + 1] - tcnt[b];
