@@ -205,8 +205,9 @@ __device__ __forceinline__ int claim_row(const ClaimArgs& A, const RowKey& r, u6
 }
 
 // NK: key parts (a template parameter so a row's key stays in registers).
-// One row per thread (4 rows per thread with their first probes loaded
-// together measured slower: 0.90 -> 1.13 ms per 1e8 rows).
+// One row per thread (4 rows per thread with their keys, hashes and first
+// probes loaded together measured slower, twice: 0.90 -> 1.13 ms per 1e8 rows
+// with agent-scope probes, 0.89 -> 1.04 ms with L1-cached ones).
 template <int NK>
 __global__ __launch_bounds__(256) void k_group_claim(const ClaimArgs A) {
     const long long stride = (long long)gridDim.x * blockDim.x;
