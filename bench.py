@@ -1184,8 +1184,8 @@ def groupby_line(eng, dev, rank, world, steps, warmup, dist, rows=GROUPBY_ROWS):
                      "frac": round(n * bpr / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "pass_bytes_per_row": round(pbr, 3),
                      "pass_gbs": round(n * pbr / (ms * 1e-3) / 1e9, 1),
-                     "bound": "the passes' dependent table reads (claim, rank), the scatter's LDS position "
-                              "atomics and the bucket pass's LDS atomics; the whole step incl. finish"}
+                     "bound": "the claim and rank passes' dependent random table reads, the scatter and bucket "
+                              "passes' streamed-load latency; the whole step incl. the finish (DESIGN.md §6)"}
     del utf8, data, offs, cases
     return out
 
